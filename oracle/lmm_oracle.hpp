@@ -1,0 +1,218 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+// A single-threaded CPU restatement of SimGrid's linear max-min (LMM) solver, used exclusively
+// as the parity checker by tests/, __graft_entry__.smoke() and the cpu_baseline leg of bench.py.
+// Nothing in simgrid_amd/ links, loads or calls this code.
+//
+// It restates the *semantics* of (file:line in gc00/simgrid @ 3.23.3-dev):
+//   src/kernel/lmm/maxmin.hpp:141-557     Element / Constraint / Variable / System / FairBottleneck
+//   src/kernel/lmm/maxmin.cpp:30-58       element concurrency accounting (w >= 1 counts as 1)
+//   src/kernel/lmm/maxmin.cpp:106-232     var_free / constraint_new / variable_new / variable_free
+//   src/kernel/lmm/maxmin.cpp:234-323     expand / expand_add (first-matching-element rule)
+//   src/kernel/lmm/maxmin.cpp:397-424     saturated constraint / variable set updates (exact == ties)
+//   src/kernel/lmm/maxmin.cpp:487-693     lmm_solve (weighted progressive filling)
+//   src/kernel/lmm/maxmin.cpp:703-937     update_* / staging / selective-update closure
+//   src/kernel/lmm/maxmin.cpp:948-967     Constraint::get_usage / get_variable_amount
+//   src/kernel/lmm/fair_bottleneck.cpp:23-153  FairBottleneck::bottleneck_solve
+//   src/surf/surf_interface.hpp:34-54     double_update / double_positive / double_equals
+//
+// The reference keeps its sets in boost::intrusive lists; this restatement uses a small
+// hand-written intrusive list with the same push_front / push_back / erase order semantics so
+// that iteration orders (and therefore floating-point summation orders, staging decisions and
+// the print() layout pinned by the tesh goldens) are identical.  Boost is absent from this
+// image, so the reference itself cannot be compiled here (see DESIGN.md "Oracle").
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace lmm_oracle {
+
+extern double g_maxmin_precision;  // maxmin.cpp:12  (--cfg=maxmin/precision)
+extern int g_concurrency_limit;    // maxmin.cpp:14  (--cfg=maxmin/concurrency-limit)
+
+enum class Policy : int { FATPIPE = 0, SHARED = 1 };  // include/simgrid/s4u/Link.hpp:35
+
+// ---------------------------------------------------------------------------------------------
+// Minimal intrusive doubly-linked list.  A Link lives inside the owning object and remembers its
+// owner, so an object may sit in several lists at once (as the reference's hooks allow).
+// ---------------------------------------------------------------------------------------------
+struct Link {
+  Link* prev = nullptr;
+  Link* next = nullptr;
+  void* owner = nullptr;
+  bool linked() const { return prev != nullptr; }
+};
+
+template <class T, Link T::*L> class Chain {
+  Link head_;  // sentinel
+  size_t n_ = 0;
+
+public:
+  Chain() { head_.prev = head_.next = &head_; }
+  Chain(const Chain&) = delete;
+  Chain& operator=(const Chain&) = delete;
+
+  bool empty() const { return n_ == 0; }
+  size_t size() const { return n_; }
+  T& front() { return *static_cast<T*>(head_.next->owner); }
+
+  void insert_before(Link* pos, T& x) {
+    Link* l = &(x.*L);
+    l->owner = &x;
+    l->prev = pos->prev;
+    l->next = pos;
+    pos->prev->next = l;
+    pos->prev = l;
+    ++n_;
+  }
+  void push_front(T& x) { insert_before(head_.next, x); }
+  void push_back(T& x) { insert_before(&head_, x); }
+  void erase(T& x) {
+    Link* l = &(x.*L);
+    l->prev->next = l->next;
+    l->next->prev = l->prev;
+    l->prev = l->next = nullptr;
+    --n_;
+  }
+  void pop_front() { erase(front()); }
+  void clear() {
+    while (!empty())
+      pop_front();
+  }
+  // next object after x, or nullptr at the end
+  T* after(T& x) {
+    Link* n = (x.*L).next;
+    return n == &head_ ? nullptr : static_cast<T*>(n->owner);
+  }
+  T* first() { return n_ ? &front() : nullptr; }
+
+  struct iterator {
+    Link* p;
+    Link* end;
+    T& operator*() const { return *static_cast<T*>(p->owner); }
+    iterator& operator++() {
+      p = p->next;
+      return *this;
+    }
+    bool operator!=(const iterator& o) const { return p != o.p; }
+  };
+  iterator begin() { return iterator{head_.next, &head_}; }
+  iterator end() { return iterator{&head_, &head_}; }
+};
+
+struct Constraint;
+struct Variable;
+class System;
+
+struct Element {  // maxmin.hpp:141-162
+  Link enabled_link, disabled_link, active_link;
+  Constraint* cnst = nullptr;
+  Variable* var = nullptr;
+  double weight = 0.0;  // consumption_weight
+
+  int concurrency() const { return weight >= 1 ? 1 : 0; }  // maxmin.cpp:30-40
+  void dec_concurrency();
+  void inc_concurrency();
+};
+
+struct Light {  // ConstraintLight, maxmin.hpp:164-168
+  double remaining_over_usage;
+  Constraint* cnst;
+};
+
+struct Constraint {  // maxmin.hpp:179-282
+  Link all_link, active_link, modified_link, saturated_link;
+  Chain<Element, &Element::enabled_link> enabled;
+  Chain<Element, &Element::disabled_link> disabled;
+  Chain<Element, &Element::active_link> active;
+  double remaining = 0.0, usage = 0.0, bound = 0.0;
+  int conc_current = 0, conc_maximum = 0, conc_limit = -1;
+  Policy policy = Policy::SHARED;
+  int rank = 0;
+  Light* light = nullptr;
+  // recorded by the last lmm_solve init (the tesh 'Constraint ... usage: remaining:' lines)
+  double init_usage = 0.0, init_remaining = 0.0;
+  bool init_recorded = false;
+
+  int slack() const;  // maxmin.hpp:220-223
+  double get_usage();
+  int variable_amount();
+};
+
+struct Variable {  // maxmin.hpp:290-365
+  Link all_link, saturated_link;
+  std::vector<Element> elems;
+  double penalty = 0.0, staged_penalty = 0.0, bound = -1.0, value = 0.0, mu = 0.0;
+  int share = 1;  // concurrency_share_
+  int rank = 0;
+  unsigned visited = 0;
+  void* user = nullptr;  // the Action* in the reference (opaque here)
+  bool in_modified_set = false;
+
+  int min_slack() const;  // maxmin.cpp:730-743
+  bool can_enable() const { return staged_penalty > 0 && min_slack() >= share; }
+};
+
+class System {  // maxmin.hpp:380-545
+public:
+  explicit System(bool selective);
+  virtual ~System();
+
+  Constraint* constraint_new(double bound);
+  Variable* variable_new(void* user, double penalty, double bound, size_t n_cnst);
+  void variable_free(Variable* v);
+  void variable_free_all();
+  void expand(Constraint* c, Variable* v, double w);
+  void expand_add(Constraint* c, Variable* v, double w);
+  void update_variable_bound(Variable* v, double b);
+  void update_variable_penalty(Variable* v, double p);
+  void update_constraint_bound(Constraint* c, double b);
+  void set_concurrency_limit(Constraint* c, int limit);
+  bool constraint_used(Constraint* c) const { return c->active_link.linked(); }
+
+  void lmm_solve();
+  virtual void solve() { lmm_solve(); }
+
+  bool modified = false;
+  bool selective;
+  Chain<Variable, &Variable::all_link> variables;
+  Chain<Constraint, &Constraint::active_link> active_cnsts;
+  Chain<Variable, &Variable::saturated_link> saturated_vars;
+  Chain<Constraint, &Constraint::saturated_link> saturated_cnsts;
+  Chain<Constraint, &Constraint::all_link> all_cnsts;
+  Chain<Constraint, &Constraint::modified_link> modified_cnsts;
+  std::vector<Variable*> modified_actions;  // Action::ModifiedSet (selective mode)
+  unsigned visited_counter = 1;
+  int next_var_rank = 1, next_cnst_rank = 1;  // per-system (reference: global statics)
+  long long last_rounds = 0;                  // number of outer rounds of the last solve
+
+protected:
+  void var_free(Variable* v);
+  void enable_var(Variable* v);
+  void disable_var(Variable* v);
+  void on_disabled_var(Constraint* c);
+  void make_cnst_active(Constraint* c) {
+    if (!c->active_link.linked())
+      active_cnsts.push_back(*c);
+  }
+  void make_cnst_inactive(Constraint* c) {
+    if (c->active_link.linked())
+      active_cnsts.erase(*c);
+    if (c->modified_link.linked())
+      modified_cnsts.erase(*c);
+  }
+  void update_modified_set(Constraint* c);
+  void update_modified_set_rec(Constraint* c);
+  void remove_all_modified_set();
+  template <class List> void solve_list(List& list);
+};
+
+class FairBottleneck : public System {  // maxmin.hpp:547-554
+public:
+  explicit FairBottleneck(bool selective) : System(selective) {}
+  void solve() override;
+};
+
+}  // namespace lmm_oracle
