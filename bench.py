@@ -1,0 +1,180 @@
+#!/usr/bin/env python
+"""LMM solve throughput on MI355X (BASELINE.json metric: "LMM solve throughput (vars/s) at
+1/2/4/8 GPUs; % of HBM peak").
+
+Workload (BASELINE.json configs[1]): a maxmin_bench-style synthetic system of
+10^6 constraints x 10^7 variables x 8 elements/variable, built through the lmm::System API and
+solved with System::lmm_solve semantics on one MI355X.  One step = one full solve of that system
+with its inputs already resident in HBM (flatten + upload happen before the timed region, like
+maxmin_bench.cpp:81-83 times only solve()).  With --gpus N every rank solves its own independent
+system (seed = rank + 1): a parameter sweep, weak scaling, no data-path collective.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a `roofline` object for the
+dominant kernel (HIP events on the solver's own stream, per-launch algorithmic bytes from the
+per-round work profile) and a `cpu_baseline` object (the oracle, single-threaded, on a bounded
+1/10-scale sample of the same generator).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_scan_vars", 3: "mm_fix_vars", 4: "mm_update_cnsts"}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def kernel_bytes(slot, nV, nC, av, ae):
+    """Algorithmic bytes one launch must move, given alive variables `av` and their elements `ae`
+    at the start of the round (DESIGN.md §5 derives each term)."""
+    if slot == 2:  # mm_scan_vars: vst(1/var) ; alive: var_ptr 8 + vtmp 8 ; per elem: cnst idx 4 + ratio 8
+        return nV * 1 + av * 16 + ae * 12
+    if slot == 3:  # mm_fix_vars: vst ; alive: vtmp, var_ptr, pen, vbound 32 ; per elem idx 4 + ratio 8 + bad 1
+        return nV * 1 + av * 32 + ae * 13
+    if slot == 4:  # mm_update_cnsts: ratio 8 per constraint
+        return nC * 8
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cnst", type=int, default=1_000_000)
+    ap.add_argument("--vars", type=int, default=10_000_000)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-div", type=int, default=10, help="CPU baseline sample = 1/div of the workload")
+    ap.add_argument("--traffic-json", default=None, help="per-kernel HBM bytes from a rocprofv3 --pmc pass")
+    ap.add_argument("--profile-json", default=None, help="write the per-launch profile here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    from simgrid_amd import lmm
+
+    assert torch.cuda.is_available(), "bench.py needs an MI355X"
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- construction (not timed) ----
+    t = time.time()
+    s = lmm.System(False)
+    s.gen_synthetic(args.cnst, args.vars, args.k, seed=rank + 1, want_vars=False)
+    t_gen = time.time() - t
+    t = time.time()
+    s.prepare()  # flatten + upload: inputs resident in HBM from here on
+    st = s.last_stats()
+    log(f"[rank {rank}] built {args.cnst}x{args.vars}x{args.k} in {t_gen:.1f}s, flatten {st['flatten_ms']:.0f} ms,"
+        f" upload {st['upload_ms']:.0f} ms: nV={st['n_var']} nC={st['n_cnst']} nnz={st['nnz']}")
+
+    for _ in range(args.warmup):
+        s.device_solve()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s.device_solve()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = s.last_stats()
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    n_vars_total = args.vars * world * args.steps
+    value = n_vars_total / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # ---- profiled solve: per-launch HIP events on the solver's stream + per-round work ----
+    s.set_profiling(True)
+    s.device_solve()
+    s.set_profiling(False)
+    slot, rnd, ms = s.launch_profile()
+    av, ae = s.round_profile()
+    nV, nC, nnz, rounds = st["n_var"], st["n_cnst"], st["nnz"], st["rounds"]
+    per_kernel = {}
+    for k in sorted(set(slot.tolist())):
+        sel = slot == k
+        byts = 0
+        for r in rnd[sel]:
+            if r >= 0 and r < len(av):
+                byts += kernel_bytes(int(k), nV, nC, int(av[r]), int(ae[r]))
+            elif r < 0:
+                byts += kernel_bytes(int(k), nV, nC, nV, nnz)
+        per_kernel[SLOT_NAMES[int(k)]] = dict(launches=int(sel.sum()), total_ms=float(ms[sel].sum()),
+                                              avg_us=float(1000 * ms[sel].mean()), alg_bytes=int(byts))
+    dom = max(per_kernel, key=lambda n: per_kernel[n]["total_ms"])
+    d = per_kernel[dom]
+    achieved = d["alg_bytes"] / (d["total_ms"] * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if dom in tj:
+            traffic = tj[dom].get("hbm_bytes_per_launch")
+    solve_alg = 56 * nnz + 24 * nV + 32 * nC
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+                "kernel_avg_us": round(d["avg_us"], 2), "kernel_launches": d["launches"],
+                "alg_bytes_per_launch": int(d["alg_bytes"] / max(1, d["launches"])),
+                "solve_alg_bytes": int(solve_alg),
+                "solve_frac": round(solve_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    if args.profile_json and rank == 0:
+        with open(args.profile_json, "w") as f:
+            json.dump(dict(per_kernel=per_kernel, rounds=rounds, alive_vars=av.tolist(), alive_elems=ae.tolist(),
+                           device_ms=st["device_ms"]), f)
+
+    # ---- CPU baseline: the oracle (single-threaded restatement), bounded sample, rank 0, N=1 ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import pyoracle as O
+
+        div = args.cpu_sample_div
+        o = O.System(False)
+        o.gen_synthetic(args.cnst // div, args.vars // div, args.k, seed=1, want_vars=False)
+        tcpu = o.timed_solve()
+        cpu = {"value": round((args.vars // div) / tcpu, 1), "unit": "vars/s", "cores": 1, "kind": "port",
+               "sample": f"same generator at 1/{div} scale ({args.cnst // div} cnst x {args.vars // div} vars x {args.k}),"
+                         f" one solve() timed with steady_clock: {tcpu:.2f} s, {o.last_rounds} sequential rounds"}
+        del o
+
+    if rank == 0:
+        out = {
+            "metric": "LMM solve throughput (vars/s)", "value": round(value, 1), "unit": "vars/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (maxmin_bench-style generator, splitmix64 seed = rank+1)",
+            "config": {"workload": "C2: 1e6 constraints x 1e7 variables x 8 elements/var, one lmm_solve per step",
+                       "nb_cnst": args.cnst, "nb_var": args.vars, "elems_per_var": args.k,
+                       "active_vars": nV, "active_cnsts": nC, "nnz": nnz, "device_rounds": rounds,
+                       "parallelism": f"replicas x{world} (independent systems per rank)"},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,101 @@
+/* lmm_hip.h — device-side C ABI of the MI355X (gfx950) LMM solver.
+ *
+ * This is the boundary a SimGrid maintainer binds from src/kernel/lmm: the reference's
+ * System::lmm_solve() (src/kernel/lmm/maxmin.cpp:487-500, called directly by Lazy models at
+ * src/kernel/resource/Model.cpp:43 and through the virtual System::solve(), maxmin.hpp:450, by
+ * Full models at Model.cpp:105) and FairBottleneck::solve() (maxmin.hpp:550 ->
+ * fair_bottleneck.cpp:23) flatten their constraint x variable incidence into CSR and hand it
+ * here.  Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a negative LMMHIP_E* code on failure; the
+ *     thread-local message is available from lmmhip_last_error();
+ *   - host pointers are borrowed for the duration of the call; device memory is owned by the
+ *     context; one context per host thread (it owns one HIP stream);
+ *   - the flattened system holds only the *active* elements (the ones lmm_solve's init loop,
+ *     maxmin.cpp:520-540, would make active): enabled variable (penalty > 0), consumption
+ *     weight > 0, constraint bound > bound * precision.  For FAIR_BOTTLENECK: enabled
+ *     variables with weight > 0 on active constraints (fair_bottleneck.cpp:29-50).
+ */
+#ifndef LMM_HIP_H
+#define LMM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LMMHIP_OK 0
+#define LMMHIP_E_NODEVICE (-1)   /* no HIP device visible: the product has no CPU fallback */
+#define LMMHIP_E_HIP (-2)        /* a HIP runtime call failed                                */
+#define LMMHIP_E_ARG (-3)        /* invalid argument / shape                                 */
+#define LMMHIP_E_STATE (-4)      /* call out of order (e.g. solve before upload)             */
+#define LMMHIP_E_NOCONVERGE (-5) /* round guard tripped (solver bug; never expected)         */
+
+#define LMMHIP_KIND_MAXMIN 0         /* System::lmm_solve           maxmin.cpp:502-693       */
+#define LMMHIP_KIND_FAIR_BOTTLENECK 1 /* FairBottleneck::bottleneck_solve fair_bottleneck.cpp:23 */
+
+typedef struct lmmhip_ctx lmmhip_ctx;
+
+typedef struct lmmhip_stats {
+  int64_t rounds;          /* device rounds of the last solve                               */
+  int64_t n_var, n_cnst, nnz;
+  double device_ms;        /* HIP-event time of the last solve (solve kernels only)         */
+  double kernel_ms[8];     /* per-phase accumulated time, when profiling is enabled         */
+  int64_t kernel_launches[8];
+} lmmhip_stats;
+
+/* Create a context on HIP device `device` (-1 = current device). */
+int lmmhip_ctx_create(int device, lmmhip_ctx** out);
+int lmmhip_ctx_destroy(lmmhip_ctx* ctx);
+
+/* Upload a flattened system (replaces any previous one).
+ *   n_var / n_cnst / nnz : sizes (nnz < 2^31)
+ *   var_ptr[n_var+1]     : CSR row offsets (variable-major), int64
+ *   cnst_idx[nnz]        : constraint index of each element, int32 in [0, n_cnst)
+ *   weight[nnz]          : consumption weight of each element (> 0), fp64
+ *   penalty[n_var]       : sharing penalty (> 0), fp64
+ *   var_bound[n_var]     : variable bound (<= 0: unbounded), fp64
+ *   cnst_bound[n_cnst]   : constraint bound, fp64
+ *   cnst_flags[n_cnst]   : bit0 = FATPIPE (s4u::Link::SharingPolicy::FATPIPE),
+ *                          bit1 = has an enabled zero-weight element (FairBottleneck FATPIPE quirk,
+ *                                 fair_bottleneck.cpp:118-123)
+ * The CSC (constraint-major) mirror is built by the library. */
+int lmmhip_upload(lmmhip_ctx* ctx, int64_t n_var, int64_t n_cnst, int64_t nnz, const int64_t* var_ptr,
+                  const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
+                  const double* cnst_bound, const uint8_t* cnst_flags);
+
+/* Update per-variable penalty/bound or per-constraint bound in place (no structural change). */
+int lmmhip_update_vars(lmmhip_ctx* ctx, const double* penalty, const double* var_bound);
+int lmmhip_update_cnsts(lmmhip_ctx* ctx, const double* cnst_bound);
+
+/* Solve on the device; values stay resident in HBM until lmmhip_get_values(). */
+int lmmhip_solve(lmmhip_ctx* ctx, int kind, double precision);
+
+/* Copy the solved values (n_var doubles, CSR variable order) to host memory. */
+int lmmhip_get_values(lmmhip_ctx* ctx, double* values_out);
+/* Device pointer of the values (for device-resident consumers, e.g. model update kernels). */
+int lmmhip_values_device_ptr(lmmhip_ctx* ctx, const double** dptr);
+
+int lmmhip_get_stats(lmmhip_ctx* ctx, lmmhip_stats* out);
+/* 1 = bracket every launch with HIP events (no host synchronisation) and accumulate per-phase
+ * times into lmmhip_stats.kernel_ms; per-launch records via lmmhip_launch_profile(). */
+int lmmhip_set_profiling(lmmhip_ctx* ctx, int on);
+/* Per-launch records of the last profiled solve: phase slot (0/1 init, 2/3/4 round phases),
+ * round index (-1 = init), duration in ms.  Returns the number of records (fills up to cap). */
+int lmmhip_launch_profile(lmmhip_ctx* ctx, int* slot, int* round, float* ms, int cap);
+/* Work profile of the last solve: alive variables / their elements at the start of each round
+ * (from the per-variable exit round).  Returns the number of rounds. */
+int lmmhip_round_profile(lmmhip_ctx* ctx, int64_t* alive_vars, int64_t* alive_elems, int cap);
+
+/* Number of visible HIP devices (0 when none; never initialises a context). */
+int lmmhip_device_count(void);
+
+const char* lmmhip_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LMM_HIP_H */

@@ -1,0 +1,96 @@
+/* lmm_system.h — System-level C ABI of the MI355X LMM solver (liblmm_amd.so).
+ *
+ * One function per method of the reference's lmm::System / Constraint / Variable
+ * (src/kernel/lmm/maxmin.hpp:179-557), so a SimGrid build (or a ctypes / cffi binding) can use the
+ * GPU solver as a drop-in through the same call sequence the models already make:
+ *   network_cm02.cpp:215-270, cpu_cas01.cpp:206-215, ptask_L07.cpp:181-201, maxmin_bench.cpp:45-83.
+ * Handles: lmm_sys* is opaque; constraints and variables are int64 ids (>= 0) owned by the system.
+ * Errors: functions returning int give 0 on success and a negative code on failure with the message
+ * in lmm_last_error(); API misuse the reference would xbt_assert on (e.g. "Too much constraints")
+ * is reported the same way instead of aborting the process.
+ */
+#ifndef LMM_SYSTEM_H
+#define LMM_SYSTEM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lmm_sys lmm_sys;
+
+/* globals — maxmin.cpp:12-14 (--cfg=maxmin/precision, --cfg=maxmin/concurrency-limit) */
+void lmm_set_precision(double precision);
+double lmm_get_precision(void);
+void lmm_set_default_concurrency_limit(int limit);
+
+/* make_new_maxmin_system (maxmin.cpp:25) / make_new_fair_bottleneck_system (fair_bottleneck.cpp:18) */
+lmm_sys* lmm_system_new(int selective_update, int kind /* 0 maxmin, 1 fair bottleneck */);
+void lmm_system_free(lmm_sys* s);
+
+int64_t lmm_constraint_new(lmm_sys* s, double bound);                                  /* maxmin.hpp:395 */
+int lmm_constraint_unshare(lmm_sys* s, int64_t c);                                     /* :185 */
+int lmm_constraint_is_shared(lmm_sys* s, int64_t c);                                   /* :188 */
+int lmm_constraint_set_concurrency_limit(lmm_sys* s, int64_t c, int limit);            /* :195 */
+int lmm_constraint_concurrency(lmm_sys* s, int64_t c, int* current, int* maximum, int* limit);
+int lmm_constraint_reset_concurrency_maximum(lmm_sys* s, int64_t c);                   /* :210 */
+double lmm_constraint_get_usage(lmm_sys* s, int64_t c);                                /* :191 */
+int lmm_constraint_get_variable_amount(lmm_sys* s, int64_t c);                         /* :192 */
+double lmm_constraint_get_bound(lmm_sys* s, int64_t c);
+int lmm_constraint_rank(lmm_sys* s, int64_t c);
+int lmm_constraint_used(lmm_sys* s, int64_t c);                                        /* :441 */
+/* elements in System::print() order (enabled then disabled); returns the count, fills up to cap */
+int lmm_constraint_elements(lmm_sys* s, int64_t c, int* var_rank, double* weight, double* value, int* enabled,
+                            int cap);
+
+int64_t lmm_variable_new(lmm_sys* s, double penalty, double bound, int64_t n_cnst);   /* :404 */
+int lmm_variable_free(lmm_sys* s, int64_t v);                                         /* :411 */
+int lmm_variable_free_all(lmm_sys* s);                                                /* :414 */
+int lmm_variable_set_concurrency_share(lmm_sys* s, int64_t v, int share);             /* :305 */
+double lmm_variable_get_value(lmm_sys* s, int64_t v);                                 /* :296 */
+double lmm_variable_get_bound(lmm_sys* s, int64_t v);                                 /* :299 */
+double lmm_variable_get_penalty(lmm_sys* s, int64_t v);                               /* :331 */
+int lmm_variable_rank(lmm_sys* s, int64_t v);
+int lmm_variable_number_of_constraints(lmm_sys* s, int64_t v);                        /* :325 */
+int lmm_get_values(lmm_sys* s, const int64_t* vars, int64_t n, double* out);
+int lmm_system_variables(lmm_sys* s, int64_t* out, int cap);          /* variable_set order      */
+int lmm_system_active_constraints(lmm_sys* s, int64_t* out, int cap); /* active_constraint_set   */
+int lmm_modified_actions(lmm_sys* s, int64_t* out, int cap);          /* Action::ModifiedSet     */
+int lmm_clear_modified_actions(lmm_sys* s);
+
+int lmm_expand(lmm_sys* s, int64_t c, int64_t v, double w);                            /* :422 */
+int lmm_expand_add(lmm_sys* s, int64_t c, int64_t v, double w);                        /* :430 */
+int lmm_update_variable_bound(lmm_sys* s, int64_t v, double bound);                    /* :433 */
+int lmm_update_variable_penalty(lmm_sys* s, int64_t v, double penalty);                /* :436 */
+int lmm_update_constraint_bound(lmm_sys* s, int64_t c, double bound);                  /* :439 */
+
+int lmm_solve(lmm_sys* s);     /* virtual System::solve (maxmin.hpp:450 / :550)  */
+int lmm_lmm_solve(lmm_sys* s); /* System::lmm_solve (maxmin.hpp:447)             */
+int lmm_is_modified(lmm_sys* s);
+/* split solve: flatten+upload / device-only solve (inputs resident in HBM) / D2H + scatter */
+int lmm_prepare(lmm_sys* s);
+int lmm_device_solve(lmm_sys* s);
+int lmm_fetch(lmm_sys* s);
+/* stats of the last solve: rounds, n_var, n_cnst, nnz (int64[4]); device/flatten/upload/fetch ms */
+int lmm_last_stats(lmm_sys* s, int64_t* counts4, double* ms4);
+/* The device context a system solves on (created on the current HIP device on first use);
+ * gives access to the lmmhip_* measurement calls (profiling, per-round work profile). */
+struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s);
+/* Solve n independent systems as one device launch sequence (disjoint union). */
+int lmm_solve_batch(lmm_sys** systems, int n);
+
+/* generators (input construction through the API above): maxmin_bench class 0..3, run index */
+int lmm_gen_maxmin_bench(lmm_sys* s, int klass, int run, int64_t* cnst_out, int64_t* var_out, int* check_start,
+                         int* check_solve);
+int64_t lmm_gen_synthetic(lmm_sys* s, int64_t nb_cnst, int64_t nb_var, int k, uint64_t seed, int max_share,
+                          int penalty_mix, int bounded_permille, int fatpipe_permille, int64_t* var_out);
+
+int lmm_device_count(void);
+const char* lmm_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LMM_SYSTEM_H */

@@ -1,0 +1,242 @@
+// lmm_capi.cpp — extern "C" surface of include/lmm/lmm_system.h over simgrid_amd::lmm::System.
+// No exception crosses the ABI: every C++ error becomes a negative return code + lmm_last_error().
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/lmm/lmm_hip.h"
+#include "../../include/lmm/lmm_system.h"
+#include "lmm_generators.hpp"
+#include "lmm_system.hpp"
+
+using simgrid_amd::lmm::Id;
+using simgrid_amd::lmm::SolverKind;
+using simgrid_amd::lmm::System;
+
+struct lmm_sys {
+  System sys;
+  lmm_sys(bool sel, SolverKind k) : sys(sel, k) {}
+};
+
+namespace {
+thread_local std::string g_err;
+
+#define GUARD(body)                    \
+  try {                                \
+    body;                              \
+    return 0;                          \
+  } catch (const std::exception& ex) { \
+    g_err = ex.what();                 \
+    return -1;                         \
+  }
+
+bool cnst_ok(lmm_sys* s, int64_t c) { return s && c >= 0 && c < int64_t(1) << 31; }
+
+struct Builder {
+  using Cnst = Id;
+  using Var = Id;
+  System* s;
+  Cnst constraint_new(double b) { return s->constraint_new(nullptr, b); }
+  void set_concurrency_limit(Cnst c, int l) { s->set_concurrency_limit(c, l); }
+  void unshare(Cnst c) { s->unshare(c); }
+  Var variable_new(double p, double b, int n) { return s->variable_new(nullptr, p, b, size_t(n)); }
+  void set_concurrency_share(Var v, int sh) { s->set_concurrency_share(v, sh); }
+  void expand(Cnst c, Var v, double w) { s->expand(c, v, w); }
+  void expand_add(Cnst c, Var v, double w) { s->expand_add(c, v, w); }
+};
+}  // namespace
+
+extern "C" {
+
+void lmm_set_precision(double p) { simgrid_amd::lmm::maxmin_precision = p; }
+double lmm_get_precision(void) { return simgrid_amd::lmm::maxmin_precision; }
+void lmm_set_default_concurrency_limit(int l) { simgrid_amd::lmm::concurrency_limit = l; }
+const char* lmm_last_error(void) { return g_err.c_str(); }
+int lmm_device_count(void) { return lmmhip_device_count(); }
+
+lmm_sys* lmm_system_new(int selective, int kind) {
+  try {
+    return new lmm_sys(selective != 0, kind == 1 ? SolverKind::FAIR_BOTTLENECK : SolverKind::MAXMIN);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return nullptr;
+  }
+}
+void lmm_system_free(lmm_sys* s) { delete s; }
+
+int64_t lmm_constraint_new(lmm_sys* s, double bound) {
+  try {
+    return s->sys.constraint_new(nullptr, bound);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+int lmm_constraint_unshare(lmm_sys* s, int64_t c) { GUARD(s->sys.unshare(Id(c))) }
+int lmm_constraint_is_shared(lmm_sys* s, int64_t c) {
+  return s->sys.cnst(Id(c)).policy != simgrid_amd::lmm::SharingPolicy::FATPIPE;
+}
+int lmm_constraint_set_concurrency_limit(lmm_sys* s, int64_t c, int l) {
+  GUARD(s->sys.set_concurrency_limit(Id(c), l))
+}
+int lmm_constraint_concurrency(lmm_sys* s, int64_t c, int* cur, int* max, int* lim) {
+  if (!cnst_ok(s, c))
+    return -1;
+  const auto& k = s->sys.cnst(Id(c));
+  *cur = k.conc_current;
+  *max = k.conc_maximum;
+  *lim = k.conc_limit;
+  return 0;
+}
+int lmm_constraint_reset_concurrency_maximum(lmm_sys* s, int64_t c) { GUARD(s->sys.reset_concurrency_maximum(Id(c))) }
+double lmm_constraint_get_usage(lmm_sys* s, int64_t c) { return s->sys.get_usage(Id(c)); }
+int lmm_constraint_get_variable_amount(lmm_sys* s, int64_t c) { return s->sys.get_variable_amount(Id(c)); }
+double lmm_constraint_get_bound(lmm_sys* s, int64_t c) { return s->sys.cnst(Id(c)).bound; }
+int lmm_constraint_rank(lmm_sys* s, int64_t c) { return s->sys.cnst(Id(c)).rank; }
+int lmm_constraint_used(lmm_sys* s, int64_t c) { return s->sys.constraint_used(Id(c)); }
+int lmm_constraint_elements(lmm_sys* s, int64_t c, int* var_rank, double* w, double* val, int* enabled, int cap) {
+  auto els = s->sys.constraint_elements(Id(c));
+  int n = 0;
+  for (Id e : els) {
+    if (n < cap) {
+      const auto& x = s->sys.elem(e);
+      var_rank[n] = s->sys.var(x.var).rank;
+      w[n] = x.weight;
+      val[n] = s->sys.var(x.var).value;
+      enabled[n] = x.where == 1;
+    }
+    n++;
+  }
+  return n;
+}
+
+int64_t lmm_variable_new(lmm_sys* s, double penalty, double bound, int64_t n_cnst) {
+  try {
+    return s->sys.variable_new(nullptr, penalty, bound, size_t(n_cnst));
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+int lmm_variable_free(lmm_sys* s, int64_t v) { GUARD(s->sys.variable_free(Id(v))) }
+int lmm_variable_free_all(lmm_sys* s) { GUARD(s->sys.variable_free_all()) }
+int lmm_variable_set_concurrency_share(lmm_sys* s, int64_t v, int sh) { GUARD(s->sys.set_concurrency_share(Id(v), sh)) }
+double lmm_variable_get_value(lmm_sys* s, int64_t v) { return s->sys.get_value(Id(v)); }
+double lmm_variable_get_bound(lmm_sys* s, int64_t v) { return s->sys.get_bound(Id(v)); }
+double lmm_variable_get_penalty(lmm_sys* s, int64_t v) { return s->sys.get_penalty(Id(v)); }
+int lmm_variable_rank(lmm_sys* s, int64_t v) { return s->sys.var(Id(v)).rank; }
+int lmm_variable_number_of_constraints(lmm_sys* s, int64_t v) { return s->sys.number_of_constraints(Id(v)); }
+int lmm_get_values(lmm_sys* s, const int64_t* vars, int64_t n, double* out) {
+  for (int64_t i = 0; i < n; i++)
+    out[i] = s->sys.get_value(Id(vars[i]));
+  return 0;
+}
+int lmm_system_variables(lmm_sys* s, int64_t* out, int cap) {
+  auto v = s->sys.variables_in_order();
+  for (int i = 0; i < int(v.size()) && i < cap; i++)
+    out[i] = v[i];
+  return int(v.size());
+}
+int lmm_system_active_constraints(lmm_sys* s, int64_t* out, int cap) {
+  auto v = s->sys.active_constraints_in_order();
+  for (int i = 0; i < int(v.size()) && i < cap; i++)
+    out[i] = v[i];
+  return int(v.size());
+}
+int lmm_modified_actions(lmm_sys* s, int64_t* out, int cap) {
+  auto& v = s->sys.modified_actions();
+  for (int i = 0; i < int(v.size()) && i < cap; i++)
+    out[i] = v[i];
+  return int(v.size());
+}
+int lmm_clear_modified_actions(lmm_sys* s) { GUARD(s->sys.clear_modified_actions()) }
+
+int lmm_expand(lmm_sys* s, int64_t c, int64_t v, double w) { GUARD(s->sys.expand(Id(c), Id(v), w)) }
+int lmm_expand_add(lmm_sys* s, int64_t c, int64_t v, double w) { GUARD(s->sys.expand_add(Id(c), Id(v), w)) }
+int lmm_update_variable_bound(lmm_sys* s, int64_t v, double b) { GUARD(s->sys.update_variable_bound(Id(v), b)) }
+int lmm_update_variable_penalty(lmm_sys* s, int64_t v, double p) { GUARD(s->sys.update_variable_penalty(Id(v), p)) }
+int lmm_update_constraint_bound(lmm_sys* s, int64_t c, double b) { GUARD(s->sys.update_constraint_bound(Id(c), b)) }
+
+int lmm_solve(lmm_sys* s) { GUARD(s->sys.solve()) }
+int lmm_lmm_solve(lmm_sys* s) { GUARD(s->sys.lmm_solve()) }
+int lmm_is_modified(lmm_sys* s) { return s->sys.modified(); }
+int lmm_prepare(lmm_sys* s) { GUARD(s->sys.prepare()) }
+int lmm_device_solve(lmm_sys* s) { GUARD(s->sys.device_solve()) }
+int lmm_fetch(lmm_sys* s) { GUARD(s->sys.fetch()) }
+int lmm_last_stats(lmm_sys* s, int64_t* counts4, double* ms4) {
+  const auto& st = s->sys.last_stats();
+  counts4[0] = st.rounds;
+  counts4[1] = st.n_var;
+  counts4[2] = st.n_cnst;
+  counts4[3] = st.nnz;
+  ms4[0] = st.device_ms;
+  ms4[1] = st.flatten_ms;
+  ms4[2] = st.upload_ms;
+  ms4[3] = st.fetch_ms;
+  return 0;
+}
+struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s) {
+  try {
+    return s->sys.ctx();
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return nullptr;
+  }
+}
+int lmm_solve_batch(lmm_sys** systems, int n) {
+  try {
+    std::vector<System*> v(size_t(n > 0 ? n : 0));
+    for (int i = 0; i < n; i++)
+      v[size_t(i)] = &systems[i]->sys;
+    simgrid_amd::lmm::solve_batch(v.data(), n);
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int lmm_gen_maxmin_bench(lmm_sys* s, int klass, int run, int64_t* cnst_out, int64_t* var_out, int* check_start,
+                         int* check_solve) {
+  if (klass < 0 || klass > 3)
+    return -1;
+  try {
+    Builder b{&s->sys};
+    std::vector<Id> cs, vs;
+    lmm_gen::maxmin_bench(b, lmm_gen::kBenchClasses[klass], run, check_start, check_solve, &cs, &vs);
+    for (size_t i = 0; cnst_out && i < cs.size(); i++)
+      cnst_out[i] = cs[i];
+    for (size_t i = 0; var_out && i < vs.size(); i++)
+      var_out[i] = vs[i];
+    return int(vs.size());
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int64_t lmm_gen_synthetic(lmm_sys* s, int64_t nb_cnst, int64_t nb_var, int k, uint64_t seed, int max_share,
+                          int penalty_mix, int bounded_permille, int fatpipe_permille, int64_t* var_out) {
+  try {
+    Builder b{&s->sys};
+    lmm_gen::SynthParams p;
+    p.nb_cnst = nb_cnst;
+    p.nb_var = nb_var;
+    p.elems_per_var = k;
+    p.seed = seed;
+    p.max_share = max_share;
+    p.penalty_mix = penalty_mix;
+    p.bounded_permille = bounded_permille;
+    p.fatpipe_permille = fatpipe_permille;
+    std::vector<Id> vs;
+    lmm_gen::synthetic(b, p, nullptr, var_out ? &vs : nullptr);
+    for (size_t i = 0; var_out && i < vs.size(); i++)
+      var_out[i] = vs[i];
+    return nb_var;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,859 @@
+// lmm_system.cpp — host bookkeeping of the MI355X LMM solver (see lmm_system.hpp).
+//
+// Mutation semantics follow the reference line by line where they decide *which* variables are
+// enabled (concurrency staging) — those are integer decisions and must be exact:
+//   expand / expand_add           maxmin.cpp:234-323
+//   enable_var / disable_var      maxmin.cpp:749-795
+//   on_disabled_var               maxmin.cpp:804-843
+//   update_variable_penalty       maxmin.cpp:846-881
+//   var_free                      maxmin.cpp:106-138
+//   selective-update closure      maxmin.cpp:898-937 (iterative here: no recursion depth limit)
+// The solve itself runs on the GPU (lmm_hip.hip); this file only flattens and scatters.
+#include "lmm_system.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <limits>
+#include <stdexcept>
+
+#include "../../include/lmm/lmm_hip.h"
+
+namespace simgrid_amd {
+namespace lmm {
+
+double maxmin_precision = 1e-5;
+int concurrency_limit = -1;
+
+[[noreturn]] void fatal(const std::string& msg) { throw std::runtime_error("lmm: " + msg); }
+
+static inline void check(bool cond, const char* msg) {
+  if (!cond)
+    fatal(msg);
+}
+
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+int CnstRec::slack() const {
+  return conc_limit < 0 ? std::numeric_limits<int>::max() : conc_limit - conc_current;
+}
+
+System::System(bool selective_update, SolverKind kind) : selective_(selective_update), kind_(kind) {}
+
+System::~System() {
+  if (ctx_)
+    lmmhip_ctx_destroy(ctx_);
+}
+
+lmmhip_ctx* System::ctx() {
+  if (!ctx_) {
+    int rc = lmmhip_ctx_create(-1, &ctx_);
+    if (rc)
+      fatal(std::string("cannot create HIP context: ") + lmmhip_last_error());
+  }
+  return ctx_;
+}
+
+// ------------------------------------------------------------------------------------------
+// index-linked lists
+// ------------------------------------------------------------------------------------------
+void System::en_push_front(Id c, Id e) {
+  CnstRec& k = cnsts_[c];
+  ElemRec& x = elems_[e];
+  x.prev = kNone;
+  x.next = k.en_head;
+  if (k.en_head != kNone)
+    elems_[k.en_head].prev = e;
+  else
+    k.en_tail = e;
+  k.en_head = e;
+  x.where = 1;
+  k.n_en++;
+}
+
+void System::dis_push_back(Id c, Id e) {
+  CnstRec& k = cnsts_[c];
+  ElemRec& x = elems_[e];
+  x.next = kNone;
+  x.prev = k.dis_tail;
+  if (k.dis_tail != kNone)
+    elems_[k.dis_tail].next = e;
+  else
+    k.dis_head = e;
+  k.dis_tail = e;
+  x.where = 2;
+  k.n_dis++;
+}
+
+void System::elem_unlink(Id e) {
+  ElemRec& x = elems_[e];
+  if (!x.where)
+    return;
+  CnstRec& k = cnsts_[x.cnst];
+  Id& head = x.where == 1 ? k.en_head : k.dis_head;
+  Id& tail = x.where == 1 ? k.en_tail : k.dis_tail;
+  if (x.prev != kNone)
+    elems_[x.prev].next = x.next;
+  else
+    head = x.next;
+  if (x.next != kNone)
+    elems_[x.next].prev = x.prev;
+  else
+    tail = x.prev;
+  (x.where == 1 ? k.n_en : k.n_dis)--;
+  x.prev = x.next = kNone;
+  x.where = 0;
+}
+
+void System::vset_push_front(Id v) {
+  VarRec& r = vars_[v];
+  r.prev = kNone;
+  r.next = vset_head_;
+  if (vset_head_ != kNone)
+    vars_[vset_head_].prev = v;
+  else
+    vset_tail_ = v;
+  vset_head_ = v;
+}
+void System::vset_push_back(Id v) {
+  VarRec& r = vars_[v];
+  r.next = kNone;
+  r.prev = vset_tail_;
+  if (vset_tail_ != kNone)
+    vars_[vset_tail_].next = v;
+  else
+    vset_head_ = v;
+  vset_tail_ = v;
+}
+void System::vset_erase(Id v) {
+  VarRec& r = vars_[v];
+  if (r.prev != kNone)
+    vars_[r.prev].next = r.next;
+  else
+    vset_head_ = r.next;
+  if (r.next != kNone)
+    vars_[r.next].prev = r.prev;
+  else
+    vset_tail_ = r.prev;
+  r.prev = r.next = kNone;
+}
+
+void System::make_cnst_active(Id c) {
+  CnstRec& k = cnsts_[c];
+  if (k.in_active)
+    return;
+  k.in_active = true;
+  k.act_next = kNone;
+  k.act_prev = act_tail_;
+  if (act_tail_ != kNone)
+    cnsts_[act_tail_].act_next = c;
+  else
+    act_head_ = c;
+  act_tail_ = c;
+  flat_valid_ = false;
+}
+
+void System::make_cnst_inactive(Id c) {
+  CnstRec& k = cnsts_[c];
+  if (k.in_active) {
+    if (k.act_prev != kNone)
+      cnsts_[k.act_prev].act_next = k.act_next;
+    else
+      act_head_ = k.act_next;
+    if (k.act_next != kNone)
+      cnsts_[k.act_next].act_prev = k.act_prev;
+    else
+      act_tail_ = k.act_prev;
+    k.act_prev = k.act_next = kNone;
+    k.in_active = false;
+    flat_valid_ = false;
+  }
+  if (k.in_modified)
+    mod_erase(c);
+}
+
+void System::mod_push_back(Id c) {
+  CnstRec& k = cnsts_[c];
+  k.in_modified = true;
+  k.mod_next = kNone;
+  k.mod_prev = mod_tail_;
+  if (mod_tail_ != kNone)
+    cnsts_[mod_tail_].mod_next = c;
+  else
+    mod_head_ = c;
+  mod_tail_ = c;
+}
+void System::mod_erase(Id c) {
+  CnstRec& k = cnsts_[c];
+  if (k.mod_prev != kNone)
+    cnsts_[k.mod_prev].mod_next = k.mod_next;
+  else
+    mod_head_ = k.mod_next;
+  if (k.mod_next != kNone)
+    cnsts_[k.mod_next].mod_prev = k.mod_prev;
+  else
+    mod_tail_ = k.mod_prev;
+  k.mod_prev = k.mod_next = kNone;
+  k.in_modified = false;
+}
+
+// ------------------------------------------------------------------------------------------
+// concurrency (maxmin.cpp:42-58, 730-743)
+// ------------------------------------------------------------------------------------------
+void System::inc_conc(Id e) {
+  CnstRec& k = cnsts_[elems_[e].cnst];
+  k.conc_current += elems_[e].concurrency();
+  if (k.conc_current > k.conc_maximum)
+    k.conc_maximum = k.conc_current;
+  check(k.conc_limit < 0 || k.conc_current <= k.conc_limit, "Concurrency limit overflow!");
+}
+void System::dec_conc(Id e) {
+  CnstRec& k = cnsts_[elems_[e].cnst];
+  check(k.conc_current >= elems_[e].concurrency(), "concurrency underflow");
+  k.conc_current -= elems_[e].concurrency();
+}
+int System::min_slack(Id v) const {
+  int best = std::numeric_limits<int>::max();
+  const VarRec& r = vars_[v];
+  for (int i = 0; i < r.n_elems; i++) {
+    int s = cnsts_[elems_[r.ebase + i].cnst].slack();
+    if (s < best) {
+      if (s == 0)
+        return 0;
+      best = s;
+    }
+  }
+  return best;
+}
+
+void System::set_concurrency_limit(Id c, int limit) {
+  check(limit < 0 || cnsts_[c].conc_maximum <= limit,
+        "New concurrency limit should be larger than observed concurrency maximum");
+  cnsts_[c].conc_limit = limit;
+}
+
+// ------------------------------------------------------------------------------------------
+// creation / destruction
+// ------------------------------------------------------------------------------------------
+Id System::constraint_new(void* id, double bound) {
+  check(cnsts_.size() < size_t(std::numeric_limits<Id>::max()), "too many constraints");
+  CnstRec k;
+  k.bound = bound;
+  k.id = id;
+  k.rank = next_cnst_rank_++;
+  k.conc_limit = concurrency_limit;
+  cnsts_.push_back(k);
+  flat_valid_ = false;
+  return Id(cnsts_.size() - 1);
+}
+
+Id System::variable_new(void* id, double penalty, double bound, size_t n_cnst) {
+  Id v;
+  if (!free_var_ids_.empty()) {
+    v = free_var_ids_.back();
+    free_var_ids_.pop_back();
+  } else {
+    check(vars_.size() < size_t(std::numeric_limits<Id>::max()), "too many variables");
+    vars_.emplace_back();
+    v = Id(vars_.size() - 1);
+  }
+  VarRec& r = vars_[v];
+  r = VarRec();
+  r.id = id;
+  r.rank = next_var_rank_++;
+  r.penalty = penalty;
+  r.bound = bound;
+  r.visited = visited_counter_ - 1;
+  r.live = true;
+  r.cap = int32_t(n_cnst);
+  if (n_cnst < free_slabs_.size() && !free_slabs_[n_cnst].empty()) {
+    r.ebase = free_slabs_[n_cnst].back();
+    free_slabs_[n_cnst].pop_back();
+  } else {
+    r.ebase = int64_t(elems_.size());
+    check(elems_.size() + n_cnst < size_t(std::numeric_limits<Id>::max()), "too many elements");
+    elems_.resize(elems_.size() + n_cnst);
+  }
+  if (penalty > 0)
+    vset_push_front(v);
+  else
+    vset_push_back(v);
+  n_live_vars_++;
+  flat_valid_ = false;
+  return v;
+}
+
+// maxmin.cpp:106-138
+void System::var_free(Id v) {
+  modified_ = true;
+  flat_valid_ = false;
+  VarRec& r = vars_[v];
+  if (r.n_elems)
+    update_modified_set(elems_[r.ebase].cnst);
+  for (int i = 0; i < r.n_elems; i++) {
+    Id e = Id(r.ebase + i);
+    Id c = elems_[e].cnst;
+    if (vars_[v].penalty > 0)
+      dec_conc(e);
+    elem_unlink(e);
+    if (cnsts_[c].n_en + cnsts_[c].n_dis == 0)
+      make_cnst_inactive(c);
+    else
+      on_disabled_var(c);
+  }
+  VarRec& rr = vars_[v];
+  for (int i = 0; i < rr.cap; i++)
+    elems_[rr.ebase + i] = ElemRec();
+  if (size_t(rr.cap) < 64) {
+    if (free_slabs_.size() <= size_t(rr.cap))
+      free_slabs_.resize(rr.cap + 1);
+    free_slabs_[rr.cap].push_back(rr.ebase);
+  }
+  rr.n_elems = 0;
+  rr.live = false;
+  free_var_ids_.push_back(v);
+  n_live_vars_--;
+}
+
+void System::variable_free(Id v) {
+  check(v >= 0 && size_t(v) < vars_.size() && vars_[v].live, "variable_free on a dead variable");
+  vset_erase(v);
+  var_free(v);
+}
+
+void System::variable_free_all() {
+  while (vset_head_ != kNone)
+    variable_free(vset_head_);
+}
+
+// ------------------------------------------------------------------------------------------
+// expand / expand_add (maxmin.cpp:234-323)
+// ------------------------------------------------------------------------------------------
+void System::expand(Id c, Id v, double w) {
+  modified_ = true;
+  flat_valid_ = false;
+  VarRec* r = &vars_[v];
+  int current_share = 0;
+  if (r->share > 1)
+    for (int i = 0; i < r->n_elems; i++) {
+      const ElemRec& e = elems_[r->ebase + i];
+      if (e.cnst == c && e.where == 1)
+        current_share += e.concurrency();
+    }
+  if (r->penalty > 0 && r->share - current_share > cnsts_[c].slack()) {
+    double pen = r->penalty;
+    disable_var(v);
+    r = &vars_[v];
+    for (int i = 0; i < r->n_elems; i++)
+      on_disabled_var(elems_[r->ebase + i].cnst);
+    w = 0;
+    r = &vars_[v];
+    r->staged = pen;
+  }
+  check(r->n_elems < r->cap, "Too much constraints");
+  Id e = Id(r->ebase + r->n_elems);
+  r->n_elems++;
+  ElemRec& x = elems_[e];
+  x.weight = w;
+  x.cnst = c;
+  x.var = v;
+  if (r->penalty != 0) {
+    en_push_front(c, e);
+    inc_conc(e);
+  } else {
+    dis_push_back(c, e);
+  }
+  if (!selective_) {
+    make_cnst_active(c);
+  } else if (w > 0 || vars_[v].penalty > 0) {
+    make_cnst_active(c);
+    update_modified_set(c);
+    if (vars_[v].n_elems > 1)
+      update_modified_set(elems_[vars_[v].ebase].cnst);
+  }
+}
+
+void System::expand_add(Id c, Id v, double w) {
+  modified_ = true;
+  flat_valid_ = false;
+  VarRec& r = vars_[v];
+  Id found = kNone;
+  for (int i = 0; i < r.n_elems; i++)  // "first matching element" rule, maxmin.cpp:293-296
+    if (elems_[r.ebase + i].cnst == c) {
+      found = Id(r.ebase + i);
+      break;
+    }
+  if (found == kNone) {
+    expand(c, v, w);
+    return;
+  }
+  if (vars_[v].penalty != 0)
+    dec_conc(found);
+  if (cnsts_[c].policy != SharingPolicy::FATPIPE)
+    elems_[found].weight += w;
+  else
+    elems_[found].weight = std::max(elems_[found].weight, w);
+  if (vars_[v].penalty != 0) {
+    if (cnsts_[c].slack() < elems_[found].concurrency()) {
+      double pen = vars_[v].penalty;
+      disable_var(v);
+      for (int i = 0; i < vars_[v].n_elems; i++)
+        on_disabled_var(elems_[vars_[v].ebase + i].cnst);
+      vars_[v].staged = pen;
+    }
+    inc_conc(found);
+  }
+  update_modified_set(c);
+}
+
+// ------------------------------------------------------------------------------------------
+// staging (maxmin.cpp:749-881)
+// ------------------------------------------------------------------------------------------
+void System::enable_var(Id v) {
+  VarRec& r = vars_[v];
+  r.penalty = r.staged;
+  r.staged = 0;
+  vset_erase(v);
+  vset_push_front(v);
+  for (int i = 0; i < r.n_elems; i++) {
+    Id e = Id(r.ebase + i);
+    elem_unlink(e);
+    en_push_front(elems_[e].cnst, e);
+    inc_conc(e);
+  }
+  if (r.n_elems)
+    update_modified_set(elems_[r.ebase].cnst);
+  flat_valid_ = false;
+}
+
+void System::disable_var(Id v) {
+  VarRec& r = vars_[v];
+  check(r.staged == 0, "Staged penalty should have been cleared");
+  vset_erase(v);
+  vset_push_back(v);
+  if (r.n_elems)
+    update_modified_set(elems_[r.ebase].cnst);
+  for (int i = 0; i < r.n_elems; i++) {
+    Id e = Id(r.ebase + i);
+    elem_unlink(e);
+    dis_push_back(elems_[e].cnst, e);
+    dec_conc(e);
+  }
+  r.penalty = 0.0;
+  r.staged = 0.0;
+  r.value = 0.0;
+  flat_valid_ = false;
+}
+
+void System::on_disabled_var(Id c) {
+  if (cnsts_[c].conc_limit < 0)
+    return;
+  int budget = cnsts_[c].n_dis;
+  if (!budget)
+    return;
+  Id e = cnsts_[c].dis_head;
+  while (budget-- && e != kNone) {
+    Id nxt = elems_[e].where == 2 ? elems_[e].next : kNone;
+    Id v = elems_[e].var;
+    if (vars_[v].staged > 0 && can_enable(v))
+      enable_var(v);
+    check(cnsts_[c].conc_current <= cnsts_[c].conc_limit, "Concurrency overflow!");
+    if (cnsts_[c].conc_current == cnsts_[c].conc_limit)
+      break;
+    e = nxt;
+  }
+}
+
+void System::update_variable_bound(Id v, double bound) {
+  modified_ = true;
+  flat_valid_ = false;
+  vars_[v].bound = bound;
+  if (vars_[v].n_elems)
+    update_modified_set(elems_[vars_[v].ebase].cnst);
+}
+
+void System::update_variable_penalty(Id v, double penalty) {
+  check(penalty >= 0, "Variable penalty should not be negative!");
+  VarRec& r = vars_[v];
+  if (penalty == r.penalty)
+    return;
+  bool enabling = penalty > 0 && r.penalty <= 0;
+  bool disabling = penalty <= 0 && r.penalty > 0;
+  modified_ = true;
+  flat_valid_ = false;
+  if (enabling) {
+    r.staged = penalty;
+    if (min_slack(v) < r.share)
+      return;  // staged instead of enabled
+    enable_var(v);
+  } else if (disabling) {
+    disable_var(v);
+  } else {
+    r.penalty = penalty;
+  }
+}
+
+void System::update_constraint_bound(Id c, double bound) {
+  modified_ = true;
+  flat_valid_ = false;
+  update_modified_set(c);
+  cnsts_[c].bound = bound;
+}
+
+// ------------------------------------------------------------------------------------------
+// selective update closure (maxmin.cpp:898-937)
+// ------------------------------------------------------------------------------------------
+void System::update_modified_set(Id c) {
+  if (selective_ && !cnsts_[c].in_modified) {
+    mod_push_back(c);
+    update_modified_set_rec(c);
+  }
+}
+
+void System::update_modified_set_rec(Id c0) {
+  // Same closure as the recursive reference (every constraint reachable through enabled elements
+  // of unvisited variables), with an explicit stack.
+  std::vector<Id> stack{c0};
+  while (!stack.empty()) {
+    Id c = stack.back();
+    stack.pop_back();
+    for (Id e = cnsts_[c].en_head; e != kNone; e = elems_[e].next) {
+      Id v = elems_[e].var;
+      VarRec& r = vars_[v];
+      if (r.visited == visited_counter_)
+        continue;
+      for (int i = 0; i < r.n_elems; i++) {
+        Id c2 = elems_[r.ebase + i].cnst;
+        if (c2 != c && !cnsts_[c2].in_modified) {
+          mod_push_back(c2);
+          stack.push_back(c2);
+        }
+      }
+      r.visited = visited_counter_;
+    }
+  }
+}
+
+void System::remove_all_modified_set() {
+  if (++visited_counter_ == 1)
+    for (Id v = vset_head_; v != kNone; v = vars_[v].next)
+      vars_[v].visited = 0;
+  while (mod_head_ != kNone)
+    mod_erase(mod_head_);
+}
+
+void System::clear_modified_actions() {
+  for (Id v : modified_actions_)
+    if (size_t(v) < vars_.size())
+      vars_[v].in_modified_set = false;
+  modified_actions_.clear();
+}
+
+// ------------------------------------------------------------------------------------------
+// read API
+// ------------------------------------------------------------------------------------------
+Id System::get_constraint(Id v, int i) const {
+  return i < vars_[v].n_elems ? elems_[vars_[v].ebase + i].cnst : kNone;
+}
+double System::get_constraint_weight(Id v, int i) const {
+  return i < vars_[v].n_elems ? elems_[vars_[v].ebase + i].weight : 0.0;
+}
+double System::get_usage(Id c) const {
+  double r = 0.0;
+  const bool fat = cnsts_[c].policy == SharingPolicy::FATPIPE;
+  for (Id e = cnsts_[c].en_head; e != kNone; e = elems_[e].next) {
+    const ElemRec& x = elems_[e];
+    if (x.weight <= 0)
+      continue;
+    double u = x.weight * vars_[x.var].value;
+    r = fat ? std::max(r, u) : r + u;
+  }
+  return r;
+}
+int System::get_variable_amount(Id c) const {
+  int n = 0;
+  for (Id e = cnsts_[c].en_head; e != kNone; e = elems_[e].next)
+    n += elems_[e].weight > 0;
+  return n;
+}
+std::vector<Id> System::constraint_elements(Id c) const {
+  std::vector<Id> out;
+  for (Id e = cnsts_[c].en_head; e != kNone; e = elems_[e].next)
+    out.push_back(e);
+  for (Id e = cnsts_[c].dis_head; e != kNone; e = elems_[e].next)
+    out.push_back(e);
+  return out;
+}
+std::vector<Id> System::variables_in_order() const {
+  std::vector<Id> out;
+  for (Id v = vset_head_; v != kNone; v = vars_[v].next)
+    out.push_back(v);
+  return out;
+}
+std::vector<Id> System::active_constraints_in_order() const {
+  std::vector<Id> out;
+  for (Id c = act_head_; c != kNone; c = cnsts_[c].act_next)
+    out.push_back(c);
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------
+// flattening
+// ------------------------------------------------------------------------------------------
+std::vector<Id> System::solve_constraint_list() const {
+  std::vector<Id> list;
+  if (kind_ == SolverKind::MAXMIN && selective_) {
+    for (Id c = mod_head_; c != kNone; c = cnsts_[c].mod_next)
+      list.push_back(c);
+  } else {
+    for (Id c = act_head_; c != kNone; c = cnsts_[c].act_next)
+      list.push_back(c);
+  }
+  return list;
+}
+
+// Active part of lmm_solve's init (maxmin.cpp:509-540): enabled elements with w > 0 on listed
+// constraints with bound > bound*prec.  Values of every variable seen through an enabled element
+// of a listed constraint are reset to 0 (maxmin.cpp:509-514).
+void System::flatten_maxmin(Flat& f, const std::vector<Id>& list) {
+  const double prec = maxmin_precision;
+  const int32_t coff = int32_t(f.cbound.size());
+  std::vector<int32_t> dense_c(cnsts_.size(), -1);
+  std::vector<uint8_t> vmark(vars_.size(), 0);
+  int32_t nc = 0;
+  for (Id c : list) {
+    const CnstRec& k = cnsts_[c];
+    const bool part = k.bound > k.bound * prec;
+    bool any = false;
+    for (Id e = k.en_head; e != kNone; e = elems_[e].next) {
+      const ElemRec& x = elems_[e];
+      vars_[x.var].value = 0.0;
+      if (part && x.weight > 0) {
+        any = true;
+        vmark[x.var] = 1;
+        if (selective_ && !vars_[x.var].in_modified_set) {  // maxmin.cpp:536-538
+          vars_[x.var].in_modified_set = true;
+          modified_actions_.push_back(x.var);
+        }
+      }
+    }
+    if (any) {
+      dense_c[c] = coff + nc++;
+      f.cbound.push_back(k.bound);
+      f.cflags.push_back(k.policy == SharingPolicy::FATPIPE ? 1 : 0);
+    }
+  }
+  for (Id v = 0; v < Id(vars_.size()); v++) {
+    if (!vmark[v])
+      continue;
+    const VarRec& r = vars_[v];
+    for (int i = 0; i < r.n_elems; i++) {
+      const ElemRec& x = elems_[r.ebase + i];
+      const int32_t dc = dense_c[x.cnst];
+      if (dc >= 0 && x.weight > 0) {
+        f.cnst_idx.push_back(dc);
+        f.weight.push_back(x.weight);
+      }
+    }
+    f.var_ptr.push_back(int64_t(f.cnst_idx.size()));
+    f.penalty.push_back(r.penalty);
+    f.vbound.push_back(r.bound);
+    f.dense_vars.push_back(v);
+  }
+}
+
+// fair_bottleneck.cpp:29-50: every variable is reset; enabled variables with a non-zero weight are
+// listed, enabled ones without get 1.0; all active constraints are listed.
+void System::flatten_fair(Flat& f) {
+  const int32_t coff = int32_t(f.cbound.size());
+  std::vector<int32_t> dense_c(cnsts_.size(), -1);
+  for (Id v = vset_head_; v != kNone; v = vars_[v].next) {
+    VarRec& r = vars_[v];
+    r.value = 0.0;
+    if (r.penalty > 0.0) {
+      bool any_nz = false, any_pos = false;
+      for (int i = 0; i < r.n_elems; i++) {
+        any_nz |= elems_[r.ebase + i].weight != 0.0;
+        any_pos |= elems_[r.ebase + i].weight > 0.0;
+      }
+      if (!any_nz)
+        r.value = 1.0;
+      else
+        check(any_pos, "FairBottleneck: negative consumption weights are not supported");
+    }
+  }
+  int32_t nc = 0;
+  for (Id c = act_head_; c != kNone; c = cnsts_[c].act_next) {
+    const CnstRec& k = cnsts_[c];
+    bool any = false, zero_w = false;
+    for (Id e = k.en_head; e != kNone; e = elems_[e].next) {
+      any |= elems_[e].weight > 0;
+      zero_w |= elems_[e].weight == 0.0;
+    }
+    if (any) {
+      dense_c[c] = coff + nc++;
+      f.cbound.push_back(k.bound);
+      f.cflags.push_back(uint8_t((k.policy == SharingPolicy::FATPIPE ? 1 : 0) | (zero_w ? 2 : 0)));
+    }
+  }
+  for (Id v = 0; v < Id(vars_.size()); v++) {
+    const VarRec& r = vars_[v];
+    if (!r.live || !(r.penalty > 0))
+      continue;
+    bool listed = false;
+    for (int i = 0; i < r.n_elems; i++)
+      listed |= elems_[r.ebase + i].weight > 0 && dense_c[elems_[r.ebase + i].cnst] >= 0;
+    if (!listed)
+      continue;
+    for (int i = 0; i < r.n_elems; i++) {
+      const ElemRec& x = elems_[r.ebase + i];
+      if (x.weight > 0 && dense_c[x.cnst] >= 0) {
+        f.cnst_idx.push_back(dense_c[x.cnst]);
+        f.weight.push_back(x.weight);
+      }
+    }
+    f.var_ptr.push_back(int64_t(f.cnst_idx.size()));
+    f.penalty.push_back(r.penalty);
+    f.vbound.push_back(r.bound);
+    f.dense_vars.push_back(v);
+  }
+}
+
+void System::flatten_into(Flat& f) {
+  if (kind_ == SolverKind::FAIR_BOTTLENECK)
+    flatten_fair(f);
+  else
+    flatten_maxmin(f, solve_constraint_list());
+}
+
+void System::scatter_values(const double* x) {
+  for (size_t i = 0; i < flat_.dense_vars.size(); i++)
+    vars_[flat_.dense_vars[i]].value = x[i];
+}
+
+void System::finish_solve() {
+  if (kind_ == SolverKind::FAIR_BOTTLENECK) {
+    modified_ = true;  // fair_bottleneck.cpp:148
+  } else {
+    modified_ = false;
+    if (selective_)
+      remove_all_modified_set();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// solve
+// ------------------------------------------------------------------------------------------
+void System::prepare() {
+  auto t0 = std::chrono::steady_clock::now();
+  flat_ = Flat();
+  flatten_into(flat_);
+  stats_.flatten_ms = ms_since(t0);
+  const int64_t nV = int64_t(flat_.dense_vars.size());
+  const int64_t nC = int64_t(flat_.cbound.size());
+  const int64_t nnz = int64_t(flat_.cnst_idx.size());
+  auto t1 = std::chrono::steady_clock::now();
+  int rc = lmmhip_upload(ctx(), nV, nC, nnz, flat_.var_ptr.data(), flat_.cnst_idx.data(), flat_.weight.data(),
+                         flat_.penalty.data(), flat_.vbound.data(), flat_.cbound.data(), flat_.cflags.data());
+  if (rc)
+    fatal(std::string("upload failed: ") + lmmhip_last_error());
+  stats_.upload_ms = ms_since(t1);
+  stats_.n_var = nV;
+  stats_.n_cnst = nC;
+  stats_.nnz = nnz;
+  flat_valid_ = true;
+}
+
+void System::device_solve() {
+  int kind = kind_ == SolverKind::FAIR_BOTTLENECK ? LMMHIP_KIND_FAIR_BOTTLENECK : LMMHIP_KIND_MAXMIN;
+  int rc = lmmhip_solve(ctx(), kind, maxmin_precision);
+  if (rc)
+    fatal(std::string("device solve failed: ") + lmmhip_last_error());
+  lmmhip_stats st{};
+  lmmhip_get_stats(ctx(), &st);
+  stats_.rounds = st.rounds;
+  stats_.device_ms = st.device_ms;
+}
+
+void System::fetch() {
+  auto t0 = std::chrono::steady_clock::now();
+  xbuf_.resize(flat_.dense_vars.size());
+  int rc = lmmhip_get_values(ctx(), xbuf_.data());
+  if (rc)
+    fatal(std::string("fetch failed: ") + lmmhip_last_error());
+  scatter_values(xbuf_.data());
+  stats_.fetch_ms = ms_since(t0);
+  finish_solve();
+}
+
+void System::lmm_solve() {
+  if (!modified_)
+    return;
+  SolverKind saved = kind_;
+  kind_ = SolverKind::MAXMIN;  // lmm_solve() is the max-min solver even on a FairBottleneck
+  try {
+    prepare();
+    device_solve();
+    fetch();
+  } catch (...) {
+    kind_ = saved;
+    throw;
+  }
+  kind_ = saved;
+}
+
+void System::solve() {
+  if (kind_ == SolverKind::MAXMIN) {
+    lmm_solve();
+    return;
+  }
+  if (!modified_)  // fair_bottleneck.cpp:25
+    return;
+  prepare();
+  device_solve();
+  fetch();
+}
+
+// ------------------------------------------------------------------------------------------
+// batched solve: disjoint union of independent systems in one device solve
+// ------------------------------------------------------------------------------------------
+void solve_batch(System** systems, int n) {
+  if (n <= 0)
+    return;
+  const SolverKind kind = systems[0]->kind();
+  System::Flat f;
+  std::vector<size_t> var_begin(size_t(n) + 1, 0);
+  std::vector<std::vector<Id>> dense(n);
+  for (int i = 0; i < n; i++) {
+    check(systems[i]->kind() == kind, "solve_batch: mixed solver kinds");
+    size_t before = f.dense_vars.size();
+    systems[i]->flatten_into(f);
+    var_begin[i] = before;
+    var_begin[i + 1] = f.dense_vars.size();
+  }
+  System* s0 = systems[0];
+  int rc = lmmhip_upload(s0->ctx(), int64_t(f.dense_vars.size()), int64_t(f.cbound.size()),
+                         int64_t(f.cnst_idx.size()), f.var_ptr.data(), f.cnst_idx.data(), f.weight.data(),
+                         f.penalty.data(), f.vbound.data(), f.cbound.data(), f.cflags.data());
+  if (rc)
+    fatal(std::string("batch upload failed: ") + lmmhip_last_error());
+  rc = lmmhip_solve(s0->ctx(), kind == SolverKind::FAIR_BOTTLENECK ? 1 : 0, maxmin_precision);
+  if (rc)
+    fatal(std::string("batch solve failed: ") + lmmhip_last_error());
+  std::vector<double> x(f.dense_vars.size());
+  rc = lmmhip_get_values(s0->ctx(), x.data());
+  if (rc)
+    fatal(std::string("batch fetch failed: ") + lmmhip_last_error());
+  for (int i = 0; i < n; i++) {
+    System* s = systems[i];
+    // values of the dense block of system i
+    for (size_t j = var_begin[i]; j < var_begin[i + 1]; j++)
+      s->set_value(f.dense_vars[j], x[j]);
+    s->finish_solve();
+  }
+}
+
+}  // namespace lmm
+}  // namespace simgrid_amd

@@ -1,0 +1,372 @@
+"""Python mirror of the reference lmm::System API over the MI355X solver (liblmm_amd.so).
+
+Same class and method names as src/kernel/lmm/maxmin.hpp (System, Constraint, Variable,
+constraint_new / variable_new / expand / expand_add / update_* / solve / get_value ...), so tests
+read like the reference's own maxmin_test.cpp.  Every call goes through the C ABI of
+include/lmm/lmm_system.h; solving runs the HIP kernels (no CPU fallback: without a GPU, solve()
+raises LmmError).
+"""
+import ctypes as ct
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "liblmm_amd.so")
+
+P, D, I, I64, U64 = ct.c_void_p, ct.c_double, ct.c_int, ct.c_int64, ct.c_uint64
+PI, PD, PI64 = ct.POINTER(I), ct.POINTER(D), ct.POINTER(I64)
+
+SIGNATURES = {
+    # include/lmm/lmm_system.h
+    "lmm_set_precision": (None, [D]),
+    "lmm_get_precision": (D, []),
+    "lmm_set_default_concurrency_limit": (None, [I]),
+    "lmm_system_new": (P, [I, I]),
+    "lmm_system_free": (None, [P]),
+    "lmm_constraint_new": (I64, [P, D]),
+    "lmm_constraint_unshare": (I, [P, I64]),
+    "lmm_constraint_is_shared": (I, [P, I64]),
+    "lmm_constraint_set_concurrency_limit": (I, [P, I64, I]),
+    "lmm_constraint_concurrency": (I, [P, I64, PI, PI, PI]),
+    "lmm_constraint_reset_concurrency_maximum": (I, [P, I64]),
+    "lmm_constraint_get_usage": (D, [P, I64]),
+    "lmm_constraint_get_variable_amount": (I, [P, I64]),
+    "lmm_constraint_get_bound": (D, [P, I64]),
+    "lmm_constraint_rank": (I, [P, I64]),
+    "lmm_constraint_used": (I, [P, I64]),
+    "lmm_constraint_elements": (I, [P, I64, PI, PD, PD, PI, I]),
+    "lmm_variable_new": (I64, [P, D, D, I64]),
+    "lmm_variable_free": (I, [P, I64]),
+    "lmm_variable_free_all": (I, [P]),
+    "lmm_variable_set_concurrency_share": (I, [P, I64, I]),
+    "lmm_variable_get_value": (D, [P, I64]),
+    "lmm_variable_get_bound": (D, [P, I64]),
+    "lmm_variable_get_penalty": (D, [P, I64]),
+    "lmm_variable_rank": (I, [P, I64]),
+    "lmm_variable_number_of_constraints": (I, [P, I64]),
+    "lmm_get_values": (I, [P, PI64, I64, PD]),
+    "lmm_system_variables": (I, [P, PI64, I]),
+    "lmm_system_active_constraints": (I, [P, PI64, I]),
+    "lmm_modified_actions": (I, [P, PI64, I]),
+    "lmm_clear_modified_actions": (I, [P]),
+    "lmm_expand": (I, [P, I64, I64, D]),
+    "lmm_expand_add": (I, [P, I64, I64, D]),
+    "lmm_update_variable_bound": (I, [P, I64, D]),
+    "lmm_update_variable_penalty": (I, [P, I64, D]),
+    "lmm_update_constraint_bound": (I, [P, I64, D]),
+    "lmm_solve": (I, [P]),
+    "lmm_lmm_solve": (I, [P]),
+    "lmm_is_modified": (I, [P]),
+    "lmm_prepare": (I, [P]),
+    "lmm_device_solve": (I, [P]),
+    "lmm_fetch": (I, [P]),
+    "lmm_last_stats": (I, [P, PI64, PD]),
+    "lmm_solve_batch": (I, [ct.POINTER(P), I]),
+    "lmm_system_device_ctx": (P, [P]),
+    "lmm_gen_maxmin_bench": (I, [P, I, I, PI64, PI64, PI, PI]),
+    "lmm_gen_synthetic": (I64, [P, I64, I64, I, U64, I, I, I, I, PI64]),
+    "lmm_device_count": (I, []),
+    "lmm_last_error": (ct.c_char_p, []),
+    # include/lmm/lmm_hip.h
+    "lmmhip_ctx_create": (I, [I, ct.POINTER(P)]),
+    "lmmhip_ctx_destroy": (I, [P]),
+    "lmmhip_upload": (I, [P, I64, I64, I64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_update_vars": (I, [P, PD, PD]),
+    "lmmhip_update_cnsts": (I, [P, PD]),
+    "lmmhip_solve": (I, [P, I, D]),
+    "lmmhip_get_values": (I, [P, PD]),
+    "lmmhip_values_device_ptr": (I, [P, ct.POINTER(P)]),
+    "lmmhip_get_stats": (I, [P, P]),
+    "lmmhip_set_profiling": (I, [P, I]),
+    "lmmhip_launch_profile": (I, [P, PI, PI, ct.POINTER(ct.c_float), I]),
+    "lmmhip_round_profile": (I, [P, PI64, PI64, I]),
+    "lmmhip_device_count": (I, []),
+    "lmmhip_last_error": (ct.c_char_p, []),
+}
+
+_lib = None
+
+
+class LmmError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load liblmm_amd.so (built by __graft_entry__.build() / `make -C simgrid_amd/csrc`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LmmError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        l = ct.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise LmmError(lib().lmm_last_error().decode())
+    return rc
+
+
+def set_precision(p):
+    lib().lmm_set_precision(p)
+
+
+def get_precision():
+    return lib().lmm_get_precision()
+
+
+def device_count():
+    return lib().lmm_device_count()
+
+
+class Constraint:
+    __slots__ = ("sys", "h")
+
+    def __init__(self, sys, h):
+        self.sys, self.h = sys, h
+
+    def unshare(self):
+        _check(lib().lmm_constraint_unshare(self.sys.h, self.h))
+
+    def is_shared(self):
+        return bool(lib().lmm_constraint_is_shared(self.sys.h, self.h))
+
+    def set_concurrency_limit(self, l):
+        _check(lib().lmm_constraint_set_concurrency_limit(self.sys.h, self.h, l))
+
+    def concurrency(self):
+        a, b, c = I(), I(), I()
+        _check(lib().lmm_constraint_concurrency(self.sys.h, self.h, ct.byref(a), ct.byref(b), ct.byref(c)))
+        return a.value, b.value, c.value
+
+    def get_concurrency_limit(self):
+        return self.concurrency()[2]
+
+    def get_concurrency_maximum(self):
+        return self.concurrency()[1]
+
+    def reset_concurrency_maximum(self):
+        _check(lib().lmm_constraint_reset_concurrency_maximum(self.sys.h, self.h))
+
+    def get_usage(self):
+        return lib().lmm_constraint_get_usage(self.sys.h, self.h)
+
+    def get_variable_amount(self):
+        return lib().lmm_constraint_get_variable_amount(self.sys.h, self.h)
+
+    def get_bound(self):
+        return lib().lmm_constraint_get_bound(self.sys.h, self.h)
+
+    @property
+    def rank(self):
+        return lib().lmm_constraint_rank(self.sys.h, self.h)
+
+    def elements(self):
+        """[(var_rank, weight, value, enabled)] in System::print() order."""
+        n = lib().lmm_constraint_elements(self.sys.h, self.h, None, None, None, None, 0)
+        rk, w, x, en = (I * n)(), (D * n)(), (D * n)(), (I * n)()
+        lib().lmm_constraint_elements(self.sys.h, self.h, rk, w, x, en, n)
+        return [(rk[i], w[i], x[i], bool(en[i])) for i in range(n)]
+
+
+class Variable:
+    __slots__ = ("sys", "h")
+
+    def __init__(self, sys, h):
+        self.sys, self.h = sys, h
+
+    def get_value(self):
+        return lib().lmm_variable_get_value(self.sys.h, self.h)
+
+    def get_bound(self):
+        return lib().lmm_variable_get_bound(self.sys.h, self.h)
+
+    def get_penalty(self):
+        return lib().lmm_variable_get_penalty(self.sys.h, self.h)
+
+    def set_concurrency_share(self, s):
+        _check(lib().lmm_variable_set_concurrency_share(self.sys.h, self.h, s))
+
+    def get_number_of_constraint(self):
+        return lib().lmm_variable_number_of_constraints(self.sys.h, self.h)
+
+    @property
+    def rank(self):
+        return lib().lmm_variable_rank(self.sys.h, self.h)
+
+
+class System:
+    """lmm::System (maxmin.hpp:380) — FairBottleneck (maxmin.hpp:547) with kind=FAIR_BOTTLENECK."""
+
+    MAXMIN, FAIR_BOTTLENECK = 0, 1
+
+    def __init__(self, selective_update=False, kind=0):
+        self.h = lib().lmm_system_new(int(selective_update), kind)
+        if not self.h:
+            raise LmmError(lib().lmm_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.lmm_system_free(self.h)
+            self.h = None
+
+    def constraint_new(self, id_, bound):
+        h = lib().lmm_constraint_new(self.h, bound)
+        if h < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return Constraint(self, h)
+
+    def variable_new(self, id_, penalty, bound=-1.0, number_of_constraints=1):
+        h = lib().lmm_variable_new(self.h, penalty, bound, number_of_constraints)
+        if h < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return Variable(self, h)
+
+    def variable_free(self, v):
+        _check(lib().lmm_variable_free(self.h, v.h))
+
+    def variable_free_all(self):
+        _check(lib().lmm_variable_free_all(self.h))
+
+    def expand(self, c, v, w):
+        _check(lib().lmm_expand(self.h, c.h, v.h, w))
+
+    def expand_add(self, c, v, w):
+        _check(lib().lmm_expand_add(self.h, c.h, v.h, w))
+
+    def update_variable_bound(self, v, b):
+        _check(lib().lmm_update_variable_bound(self.h, v.h, b))
+
+    def update_variable_penalty(self, v, p):
+        _check(lib().lmm_update_variable_penalty(self.h, v.h, p))
+
+    def update_constraint_bound(self, c, b):
+        _check(lib().lmm_update_constraint_bound(self.h, c.h, b))
+
+    def constraint_used(self, c):
+        return bool(lib().lmm_constraint_used(self.h, c.h))
+
+    def solve(self):
+        _check(lib().lmm_solve(self.h))
+
+    def lmm_solve(self):
+        _check(lib().lmm_lmm_solve(self.h))
+
+    # split solve (bench): construction / device-resident solve / results
+    def prepare(self):
+        _check(lib().lmm_prepare(self.h))
+
+    def device_solve(self):
+        _check(lib().lmm_device_solve(self.h))
+
+    def fetch(self):
+        _check(lib().lmm_fetch(self.h))
+
+    def last_stats(self):
+        c, m = (I64 * 4)(), (D * 4)()
+        lib().lmm_last_stats(self.h, c, m)
+        return dict(rounds=c[0], n_var=c[1], n_cnst=c[2], nnz=c[3], device_ms=m[0], flatten_ms=m[1],
+                    upload_ms=m[2], fetch_ms=m[3])
+
+    # ---- device-side measurement (lmmhip_* on this system's context) ----
+    def device_ctx(self):
+        c = lib().lmm_system_device_ctx(self.h)
+        if not c:
+            raise LmmError(lib().lmm_last_error().decode())
+        return c
+
+    def set_profiling(self, on):
+        if lib().lmmhip_set_profiling(self.device_ctx(), int(on)) != 0:
+            raise LmmError(lib().lmmhip_last_error().decode())
+
+    def launch_profile(self):
+        """(slot, round, ms) arrays of every launch of the last profiled solve."""
+        c = self.device_ctx()
+        n = lib().lmmhip_launch_profile(c, None, None, None, 0)
+        if n < 0:
+            raise LmmError(lib().lmmhip_last_error().decode())
+        slot, rnd = np.empty(n, np.int32), np.empty(n, np.int32)
+        ms = np.empty(n, np.float32)
+        lib().lmmhip_launch_profile(c, slot.ctypes.data_as(PI), rnd.ctypes.data_as(PI),
+                                    ms.ctypes.data_as(ct.POINTER(ct.c_float)), n)
+        return slot, rnd, ms
+
+    def round_profile(self):
+        """Alive variables / elements at the start of every round of the last solve."""
+        c = self.device_ctx()
+        cap = 1 << 20
+        av, ae = np.zeros(cap, np.int64), np.zeros(cap, np.int64)
+        r = lib().lmmhip_round_profile(c, av.ctypes.data_as(PI64), ae.ctypes.data_as(PI64), cap)
+        if r < 0:
+            raise LmmError(lib().lmmhip_last_error().decode())
+        return av[:r], ae[:r]
+
+    @property
+    def modified(self):
+        return bool(lib().lmm_is_modified(self.h))
+
+    def variables(self):
+        n = lib().lmm_system_variables(self.h, None, 0)
+        arr = (I64 * n)()
+        lib().lmm_system_variables(self.h, arr, n)
+        return [Variable(self, arr[i]) for i in range(n)]
+
+    def active_constraints(self):
+        n = lib().lmm_system_active_constraints(self.h, None, 0)
+        arr = (I64 * n)()
+        lib().lmm_system_active_constraints(self.h, arr, n)
+        return [Constraint(self, arr[i]) for i in range(n)]
+
+    def modified_actions(self):
+        n = lib().lmm_modified_actions(self.h, None, 0)
+        arr = (I64 * n)()
+        lib().lmm_modified_actions(self.h, arr, n)
+        return [Variable(self, arr[i]) for i in range(n)]
+
+    def clear_modified_actions(self):
+        _check(lib().lmm_clear_modified_actions(self.h))
+
+    # ---- generators ----
+    def gen_maxmin_bench(self, klass, run):
+        C, V = {0: (10, 10), 1: (100, 100), 2: (2000, 2000), 3: (20000, 20000)}[klass]
+        cs, vs = (I64 * C)(), (I64 * V)()
+        a, b = I(), I()
+        if lib().lmm_gen_maxmin_bench(self.h, klass, run, cs, vs, ct.byref(a), ct.byref(b)) < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return ([Constraint(self, cs[i]) for i in range(C)], [Variable(self, vs[i]) for i in range(V)],
+                a.value, b.value)
+
+    def gen_synthetic(self, nb_cnst, nb_var, k=8, seed=1, max_share=2, penalty_mix=0, bounded_permille=0,
+                      fatpipe_permille=0, want_vars=True):
+        vs = np.empty(nb_var, dtype=np.int64) if want_vars else None
+        r = lib().lmm_gen_synthetic(self.h, nb_cnst, nb_var, k, seed, max_share, penalty_mix, bounded_permille,
+                                    fatpipe_permille, vs.ctypes.data_as(PI64) if want_vars else None)
+        if r < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return vs
+
+    def values_of(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        out = np.empty(len(ids), dtype=np.float64)
+        lib().lmm_get_values(self.h, ids.ctypes.data_as(PI64), len(ids), out.ctypes.data_as(PD))
+        return out
+
+
+def solve_batch(systems):
+    """Solve independent systems as one device launch sequence (disjoint union)."""
+    arr = (P * len(systems))(*[s.h for s in systems])
+    _check(lib().lmm_solve_batch(arr, len(systems)))
+
+
+def make_new_maxmin_system(selective_update=False):
+    return System(selective_update, System.MAXMIN)
+
+
+def make_new_fair_bottleneck_system(selective_update=False):
+    return System(selective_update, System.FAIR_BOTTLENECK)

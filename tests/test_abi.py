@@ -1,0 +1,46 @@
+"""The C-ABI library loads and exports every symbol include/lmm/*.h declares (CPU only)."""
+import ctypes as ct
+import os
+import re
+
+import pytest
+
+from simgrid_amd import lmm as L
+
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "lmm")
+
+
+def declared_functions():
+    names = set()
+    for h in ("lmm_hip.h", "lmm_system.h"):
+        text = open(os.path.join(INCLUDE, h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(lmm\w*)\s*\(", text):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_headers_declare_something():
+    names = declared_functions()
+    assert "lmmhip_solve" in names and "lmm_solve" in names and len(names) > 50
+
+
+@pytest.mark.parametrize("name", declared_functions())
+def test_symbol_exported(name):
+    lib = ct.CDLL(L.LIB_PATH)
+    assert hasattr(lib, name), name
+
+
+def test_python_binding_covers_every_symbol():
+    assert set(declared_functions()) <= set(L.SIGNATURES)
+
+
+def test_solve_without_gpu_fails_loudly():
+    if L.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    s = L.System(False)
+    c = s.constraint_new(None, 1.0)
+    v = s.variable_new(None, 1.0)
+    s.expand(c, v, 1.0)
+    with pytest.raises(L.LmmError, match="no HIP device"):
+        s.solve()
