@@ -127,6 +127,10 @@ void System::set_concurrency_limit(Constraint* c, int limit) {
 // maxmin.cpp:106-138
 void System::var_free(Variable* v) {
   modified = true;
+  // A staged variable with two elements on one constraint could be re-enabled by its own
+  // on_disabled_var() below and then erased from variable_set a second time: undefined behaviour
+  // in the reference (crash).  Defined here as "a variable being freed is never re-enabled".
+  v->staged_penalty = 0.0;
   if (!v->elems.empty())
     update_modified_set(v->elems[0].cnst);
   for (Element& e : v->elems) {

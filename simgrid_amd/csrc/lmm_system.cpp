@@ -290,6 +290,10 @@ void System::var_free(Id v) {
   modified_ = true;
   flat_valid_ = false;
   VarRec& r = vars_[v];
+  // The reference can re-enable a staged variable from inside its own free (two elements on one
+  // constraint) and then double-erases it (undefined behaviour); a freed variable is never
+  // re-enabled here (same definition as the oracle).
+  r.staged = 0.0;
   if (r.n_elems)
     update_modified_set(elems_[r.ebase].cnst);
   for (int i = 0; i < r.n_elems; i++) {

@@ -52,6 +52,36 @@ def test_selective_mode_bookkeeping(seed):
     assert ps.modified and os_.modified
 
 
+@pytest.mark.parametrize("M", [L, O], ids=["product", "oracle"])
+def test_free_staged_variable_with_duplicate_elements(M):
+    # The reference re-enables such a variable inside its own free and double-erases it (UB).
+    # Both implementations define it as "a freed variable is never re-enabled".
+    s = M.System(False)
+    c = s.constraint_new(None, 5.0)
+    c.set_concurrency_limit(2)
+    a = s.variable_new(None, 1.0, -1.0, 2)
+    s.expand(c, a, 1.0)
+    s.expand(c, a, 1.0)  # a holds the two slots
+    b = s.variable_new(None, 1.0, -1.0, 2)
+    b.set_concurrency_share(2)
+    s.expand(c, b, 1.0)  # no slack: b is staged (weight 0)
+    s.expand(c, b, 1.0)  # second element of b on c, b disabled
+    assert b.get_penalty() == 0.0
+    s.variable_free(b)  # must not re-enable b while freeing it
+    assert c.concurrency()[0] == 2
+    s.variable_free(a)
+    assert c.concurrency()[0] == 0 and c.elements() == []
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_dense_frees_and_duplicates(seed):
+    ops = K.random_script(seed, conc_limits=(seed % 2 == 0), frees=3 + seed % 7, penalty_updates=4, bound_updates=4,
+                          dup_p=0.4)
+    a = K.replay(L, ops)
+    b = K.replay(O, ops)
+    same_structure(a[0], b[0], a[1], b[1], a[2], b[2])
+
+
 def test_variable_free_all_empties_system():
     ops = K.random_script(7, conc_limits=True)
     ps, pcs, _ = K.replay(L, ops)
