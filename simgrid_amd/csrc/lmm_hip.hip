@@ -475,8 +475,11 @@ const char* lmmhip_last_error(void) { return g_err.c_str(); }
 
 int lmmhip_device_count(void) {
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess)
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    g_err = std::string("hipGetDeviceCount: ") + hipGetErrorString(e);
     return 0;
+  }
   return n;
 }
 

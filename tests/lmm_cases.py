@@ -194,7 +194,8 @@ def lmm_usage_test3(M):  # :96-160 (11 flows on 10 links + 5 fictitious single-f
 # Random operation scripts (replayed identically on both implementations)
 # ---------------------------------------------------------------------------------------------
 def random_script(seed, n_cnst=30, n_var=60, max_el=6, fatpipe_p=0.1, bounded_p=0.2, penalty_mix=True,
-                  conc_limits=False, zero_bound_p=0.05, dup_p=0.2, frees=0, penalty_updates=0, bound_updates=0):
+                  conc_limits=False, zero_bound_p=0.05, dup_p=0.2, frees=0, penalty_updates=0, bound_updates=0,
+                  zero_w_p=0.05):
     """A deterministic list of API operations covering penalties, bounds, FATPIPE, duplicate
     elements, zero-bound constraints, concurrency limits/staging, frees and updates."""
     rng = random.Random(seed)
@@ -217,7 +218,7 @@ def random_script(seed, n_cnst=30, n_var=60, max_el=6, fatpipe_p=0.1, bounded_p=
             ops.append(("share", v, 2))
         cs = rng.sample(range(n_cnst), min(k, n_cnst))
         for c in cs:
-            ops.append(("expand", c, v, round(rng.uniform(0.0, 2.0), 4) if rng.random() > 0.05 else 0.0))
+            ops.append(("expand", c, v, round(rng.uniform(0.0, 2.0), 4) if rng.random() >= zero_w_p else 0.0))
             if rng.random() < 0.3:
                 ops.append(("expand_add", c, v, round(rng.uniform(0.0, 1.0), 4)))
         if rng.random() < dup_p:

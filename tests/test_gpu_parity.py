@@ -103,15 +103,37 @@ def test_random_maxmin_vs_oracle(seed):
     assert K.saturated(ps, pcs, 1e-5) == K.saturated(os_, ocs, 1e-5)
 
 
+# The reference's bottleneck_solve does not terminate on some inputs: a variable dropped from the
+# list keeps its last mu_ (possibly 0, e.g. after sitting on a zero-bound constraint) and FATPIPE
+# constraints take min(usage, w*mu) over ALL enabled elements (fair_bottleneck.cpp:118-125), so their
+# remaining never decreases again and their other variables grow forever.  The oracle hangs there
+# too, so the random FairBottleneck systems avoid {zero-bound + FATPIPE} and zero weights; the
+# product reports LMMHIP_E_NOCONVERGE instead of hanging (test below).
 @pytest.mark.parametrize("seed", range(20))
-def test_random_fair_bottleneck_vs_oracle(seed):
-    ops = K.random_script(1000 + seed, conc_limits=(seed % 3 == 0), frees=2, bound_updates=3)
+@pytest.mark.parametrize("variant", ["fatpipe", "zero_bounds"])
+def test_random_fair_bottleneck_vs_oracle(seed, variant):
+    kw = dict(zero_bound_p=0.0, fatpipe_p=0.1) if variant == "fatpipe" else dict(zero_bound_p=0.05, fatpipe_p=0.0)
+    ops = K.random_script(1000 + seed, conc_limits=(seed % 3 == 0), frees=2, bound_updates=3, zero_w_p=0.0, **kw)
     ps, pcs, pvs = K.replay(L, ops, kind=L.System.FAIR_BOTTLENECK)
     os_, ocs, ovs = K.replay(O, ops, kind=O.System.FAIR_BOTTLENECK)
     ps.solve()
     os_.solve()
     worst, bad = K.compare_values(pvs, ovs)
     assert not bad, bad[:5]
+
+
+def test_fair_bottleneck_nonterminating_input_is_reported():
+    s = L.System(False, L.System.FAIR_BOTTLENECK)
+    z = s.constraint_new(None, 0.0)  # zero-bound: its variable leaves the list with mu = 0
+    f = s.constraint_new(None, 5.0)
+    f.unshare()
+    a = s.variable_new(None, 1.0, -1.0, 2)
+    b = s.variable_new(None, 1.0, -1.0, 1)
+    s.expand(z, a, 1.0)
+    s.expand(f, a, 1.0)
+    s.expand(f, b, 1.0)
+    with pytest.raises(L.LmmError, match="round guard"):
+        s.solve()
 
 
 def test_resolve_after_mutations():
