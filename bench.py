@@ -24,22 +24,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
-SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_scan_vars", 3: "mm_fix_vars", 4: "mm_update_cnsts"}
+SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_fix", 4: "mm_update", 5: "compaction"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def kernel_bytes(slot, nV, nC, av, ae):
-    """Algorithmic bytes one launch must move, given alive variables `av` and their elements `ae`
-    at the start of the round (DESIGN.md §5 derives each term)."""
-    if slot == 2:  # mm_scan_vars: vst(1/var) ; alive: var_ptr 8 + vtmp 8 ; per elem: cnst idx 4 + ratio 8
-        return nV * 1 + av * 16 + ae * 12
-    if slot == 3:  # mm_fix_vars: vst ; alive: vtmp, var_ptr, pen, vbound 32 ; per elem idx 4 + ratio 8 + bad 1
-        return nV * 1 + av * 32 + ae * 13
-    if slot == 4:  # mm_update_cnsts: ratio 8 per constraint
-        return nC * 8
+def kernel_bytes(slot, nV, nC, av, ae, fv, fe):
+    """Algorithmic bytes one launch must move, given the alive variables `av` / elements `ae` at the
+    start of the round and the variables `fv` / elements `fe` fixed in it."""
+    if slot == 2:  # mm_vote: per alive row crow 4 + cvar 4 + valive 1 + vbound 8 + vinfo 4; per element ccol 4 + key 2
+        return av * 21 + ae * 6
+    if slot == 3:  # mm_fix: per alive row valive 1 + vinfo 4 + cvar 4 + pen 8 + votes/acnt 8;
+        #            per fixed row x 8 + ratio 8 + row ptr 8; per fixed element idx 4 + w 8 + key 2 + atomics 20
+        return av * 25 + fv * 24 + fe * 34
+    if slot == 4:  # mm_update: key 2 per constraint
+        return nC * 2
+    if slot == 0:  # mm_init_cnsts: CSC idx 4 + w 8 + pen gather 8 per element; bound 8 + state writes 40 per constraint
+        return 20 * ae + 48 * nC
+    if slot == 1:
+        return nV * 13
     return 0
 
 
@@ -118,10 +123,12 @@ def main():
         sel = slot == k
         byts = 0
         for r in rnd[sel]:
-            if r >= 0 and r < len(av):
-                byts += kernel_bytes(int(k), nV, nC, int(av[r]), int(ae[r]))
+            if 0 <= r < len(av):
+                nxt_v = int(av[r + 1]) if r + 1 < len(av) else 0
+                nxt_e = int(ae[r + 1]) if r + 1 < len(ae) else 0
+                byts += kernel_bytes(int(k), nV, nC, int(av[r]), int(ae[r]), int(av[r]) - nxt_v, int(ae[r]) - nxt_e)
             elif r < 0:
-                byts += kernel_bytes(int(k), nV, nC, nV, nnz)
+                byts += kernel_bytes(int(k), nV, nC, nV, nnz, 0, 0)
         per_kernel[SLOT_NAMES[int(k)]] = dict(launches=int(sel.sum()), total_ms=float(ms[sel].sum()),
                                               avg_us=float(1000 * ms[sel].mean()), alg_bytes=int(byts))
     dom = max(per_kernel, key=lambda n: per_kernel[n]["total_ms"])

@@ -80,6 +80,13 @@ struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s);
 /* Solve n independent systems as one device launch sequence (disjoint union). */
 int lmm_solve_batch(lmm_sys** systems, int n);
 
+/* Max-min certificate of the current values (validation utility, CPU): worst relative constraint
+ * excess, number of infeasible constraints (the assertion of System::print(), maxmin.cpp:470), and
+ * number of enabled variables with x > 0 below their bound that have no saturated constraint on
+ * which their level x*penalty is maximal.  Size-independent parity property for large systems. */
+int lmm_check_certificate(lmm_sys* s, double precision, double* max_excess, int64_t* n_infeasible,
+                          int64_t* n_unbottlenecked);
+
 /* generators (input construction through the API above): maxmin_bench class 0..3, run index */
 int lmm_gen_maxmin_bench(lmm_sys* s, int klass, int run, int64_t* cnst_out, int64_t* var_out, int* check_start,
                          int* check_solve);

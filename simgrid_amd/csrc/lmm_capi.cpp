@@ -196,6 +196,11 @@ int lmm_solve_batch(lmm_sys** systems, int n) {
   }
 }
 
+int lmm_check_certificate(lmm_sys* s, double prec, double* max_excess, int64_t* n_infeasible,
+                          int64_t* n_unbottlenecked) {
+  GUARD(s->sys.check_certificate(prec, max_excess, n_infeasible, n_unbottlenecked))
+}
+
 int lmm_gen_maxmin_bench(lmm_sys* s, int klass, int run, int64_t* cnst_out, int64_t* var_out, int* check_start,
                          int* check_solve) {
   if (klass < 0 || klass > 3)

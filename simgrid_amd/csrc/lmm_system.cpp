@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <limits>
 #include <stdexcept>
@@ -601,6 +602,54 @@ std::vector<Id> System::active_constraints_in_order() const {
   for (Id c = act_head_; c != kNone; c = cnsts_[c].act_next)
     out.push_back(c);
   return out;
+}
+
+void System::check_certificate(double prec, double* max_excess, int64_t* n_infeasible,
+                               int64_t* n_unbottlenecked) const {
+  // usage / max level per constraint over enabled elements with w > 0
+  std::vector<double> usage(cnsts_.size(), 0.0), top(cnsts_.size(), 0.0);
+  for (size_t c = 0; c < cnsts_.size(); c++) {
+    const bool fat = cnsts_[c].policy == SharingPolicy::FATPIPE;
+    for (Id e = cnsts_[c].en_head; e != kNone; e = elems_[e].next) {
+      const ElemRec& x = elems_[e];
+      if (x.weight <= 0)
+        continue;
+      const VarRec& r = vars_[x.var];
+      const double u = x.weight * r.value;
+      usage[c] = fat ? std::max(usage[c], u) : usage[c] + u;
+      top[c] = std::max(top[c], r.value * r.penalty);
+    }
+  }
+  double worst = -1e300;
+  int64_t infeasible = 0, unb = 0;
+  std::vector<uint8_t> sat(cnsts_.size(), 0);
+  for (size_t c = 0; c < cnsts_.size(); c++) {
+    const double b = cnsts_[c].bound;
+    if (!(b > b * prec))  // ignored by lmm_solve (maxmin.cpp:524)
+      continue;
+    const double ex = (usage[c] - b) / b;
+    worst = std::max(worst, ex);
+    if (usage[c] - b > b * prec)
+      infeasible++;
+    sat[c] = !(b - usage[c] > b * prec);
+  }
+  for (Id v = 0; v < Id(vars_.size()); v++) {
+    const VarRec& r = vars_[v];
+    if (!r.live || !(r.penalty > 0) || !(r.value > 0))
+      continue;
+    if (r.bound > 0 && std::fabs(r.value - r.bound) <= std::max(prec, 1e-9 * r.bound))
+      continue;  // at its bound
+    const double lvl = r.value * r.penalty;
+    bool ok = false;
+    for (int i = 0; i < r.n_elems && !ok; i++) {
+      const ElemRec& x = elems_[r.ebase + i];
+      ok = x.weight > 0 && sat[x.cnst] && lvl >= top[x.cnst] * (1 - 1e-9);
+    }
+    unb += !ok;
+  }
+  *max_excess = worst;
+  *n_infeasible = infeasible;
+  *n_unbottlenecked = unb;
 }
 
 // ------------------------------------------------------------------------------------------

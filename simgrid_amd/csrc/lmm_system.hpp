@@ -123,6 +123,12 @@ public:
   std::vector<Id> variables_in_order() const;
   std::vector<Id> active_constraints_in_order() const;
 
+  // Max-min certificate of the current values (the checks System::print() asserts, maxmin.cpp:470-480,
+  // plus the bottleneck property): returns the worst constraint excess (usage - bound)/bound, the
+  // number of infeasible constraints, and the number of enabled variables with x > 0 that are below
+  // their bound and have no saturated constraint on which their level x*penalty is maximal.
+  void check_certificate(double prec, double* max_excess, int64_t* n_infeasible, int64_t* n_unbottlenecked) const;
+
   bool modified() const { return modified_; }
   bool selective() const { return selective_; }
   SolverKind kind() const { return kind_; }

@@ -64,6 +64,7 @@ SIGNATURES = {
     "lmm_last_stats": (I, [P, PI64, PD]),
     "lmm_solve_batch": (I, [ct.POINTER(P), I]),
     "lmm_system_device_ctx": (P, [P]),
+    "lmm_check_certificate": (I, [P, D, PD, PI64, PI64]),
     "lmm_gen_maxmin_bench": (I, [P, I, I, PI64, PI64, PI, PI]),
     "lmm_gen_synthetic": (I64, [P, I64, I64, I, U64, I, I, I, I, PI64]),
     "lmm_device_count": (I, []),
@@ -96,6 +97,14 @@ def lib():
     """Load liblmm_amd.so (built by __graft_entry__.build() / `make -C simgrid_amd/csrc`)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 and loads it by path;
+        # if ours (/opt/rocm) were loaded first, the two runtimes would race for the device and the
+        # second one sees "no ROCm-capable device".  Loading torch first makes this library bind to
+        # the already-loaded runtime (same soname).
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
         if not os.path.exists(LIB_PATH):
             raise LmmError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
         l = ct.CDLL(LIB_PATH)
@@ -273,6 +282,13 @@ class System:
         lib().lmm_last_stats(self.h, c, m)
         return dict(rounds=c[0], n_var=c[1], n_cnst=c[2], nnz=c[3], device_ms=m[0], flatten_ms=m[1],
                     upload_ms=m[2], fetch_ms=m[3])
+
+    def check_certificate(self, precision=None):
+        """(max relative excess, #infeasible constraints, #variables without a bottleneck)."""
+        ex, ni, nu = D(), I64(), I64()
+        p = get_precision() if precision is None else precision
+        _check(lib().lmm_check_certificate(self.h, p, ct.byref(ex), ct.byref(ni), ct.byref(nu)))
+        return ex.value, ni.value, nu.value
 
     # ---- device-side measurement (lmmhip_* on this system's context) ----
     def device_ctx(self):
