@@ -24,27 +24,32 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
-SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_fix", 4: "mm_update", 5: "compaction"}
+SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_ready", 4: "mm_saturate",
+              5: "mm_update", 6: "compaction"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def kernel_bytes(slot, nV, nC, av, ae, fv, fe):
-    """Algorithmic bytes one launch must move, given the alive variables `av` / elements `ae` at the
-    start of the round and the variables `fv` / elements `fe` fixed in it."""
-    if slot == 2:  # mm_vote: per alive row crow 4 + cvar 4 + valive 1 + vbound 8 + vinfo 4; per element ccol 4 + key 2
-        return av * 21 + ae * 6
-    if slot == 3:  # mm_fix: per alive row valive 1 + vinfo 4 + cvar 4 + pen 8 + votes/acnt 8;
-        #            per fixed row x 8 + ratio 8 + row ptr 8; per fixed element idx 4 + w 8 + key 2 + atomics 20
-        return av * 25 + fv * 24 + fe * 34
-    if slot == 4:  # mm_update: key 2 per constraint
-        return nC * 2
-    if slot == 0:  # mm_init_cnsts: CSC idx 4 + w 8 + pen gather 8 per element; bound 8 + state writes 40 per constraint
-        return 20 * ae + 48 * nC
+def kernel_bytes(slot, nV, nC, av, ae, fv, fe, rv, re_):
+    """Algorithmic bytes one launch must move: `av`/`ae` alive variables / elements at
+    the start of the round, `fv`/`fe` variables / elements fixed in it, `rv`/`re_` variables /
+    elements re-evaluated by the vote phase."""
+    if slot == 2:  # mm_vote: per alive row cvar 4 + vstate 4 + tgt 4 + chg 4;
+        #            per re-evaluated row crow 8 + vbound 8 + pen 8 + tgt 4; per element ccol 4 + key 2
+        return av * 16 + rv * 28 + re_ * 6
+    if slot == 3:  # mm_ready: key 2 + votes 4 + acnt 4 per constraint
+        return nC * 10
+    if slot == 4:  # mm_saturate: per fixed var csc idx 4 + vstate 4 + pen 8 + x 8 + row ptr 8;
+        #            per fixed element csr idx 4 + w 8 + key 2 + cflags 1 + atomics dcnt 4, drem 8, duse 8
+        return fv * 32 + fe * 35
+    if slot == 5:  # mm_update: key 2 + dcnt 4 per constraint; per touched constraint ~56 B of state
+        return nC * 6 + min(fe, nC) * 56
+    if slot == 0:  # mm_init_cnsts: CSC idx 4 + w 8 + pen gather 8 per element; bound 8 + state writes 48 per constraint
+        return 20 * ae + 56 * nC
     if slot == 1:
-        return nV * 13
+        return nV * 25
     return 0
 
 
@@ -117,6 +122,7 @@ def main():
     s.set_profiling(False)
     slot, rnd, ms = s.launch_profile()
     av, ae = s.round_profile()
+    rv, re_ = s.vote_profile()
     nV, nC, nnz, rounds = st["n_var"], st["n_cnst"], st["nnz"], st["rounds"]
     per_kernel = {}
     for k in sorted(set(slot.tolist())):
@@ -126,9 +132,11 @@ def main():
             if 0 <= r < len(av):
                 nxt_v = int(av[r + 1]) if r + 1 < len(av) else 0
                 nxt_e = int(ae[r + 1]) if r + 1 < len(ae) else 0
-                byts += kernel_bytes(int(k), nV, nC, int(av[r]), int(ae[r]), int(av[r]) - nxt_v, int(ae[r]) - nxt_e)
+                rr = (int(rv[r]), int(re_[r])) if r < len(rv) else (0, 0)
+                byts += kernel_bytes(int(k), nV, nC, int(av[r]), int(ae[r]), int(av[r]) - nxt_v,
+                                     int(ae[r]) - nxt_e, *rr)
             elif r < 0:
-                byts += kernel_bytes(int(k), nV, nC, nV, nnz, 0, 0)
+                byts += kernel_bytes(int(k), nV, nC, nV, nnz, 0, 0, 0, 0)
         per_kernel[SLOT_NAMES[int(k)]] = dict(launches=int(sel.sum()), total_ms=float(ms[sel].sum()),
                                               avg_us=float(1000 * ms[sel].mean()), alg_bytes=int(byts))
     dom = max(per_kernel, key=lambda n: per_kernel[n]["total_ms"])
@@ -150,6 +158,7 @@ def main():
     if args.profile_json and rank == 0:
         with open(args.profile_json, "w") as f:
             json.dump(dict(per_kernel=per_kernel, rounds=rounds, alive_vars=av.tolist(), alive_elems=ae.tolist(),
+                           reeval_vars=rv.tolist(), reeval_elems=re_.tolist(),
                            device_ms=st["device_ms"]), f)
 
     # ---- CPU baseline: the oracle (single-threaded restatement), bounded sample, rank 0, N=1 ----

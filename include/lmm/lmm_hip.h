@@ -88,6 +88,9 @@ int lmmhip_launch_profile(lmmhip_ctx* ctx, int* slot, int* round, float* ms, int
 /* Work profile of the last solve: alive variables / their elements at the start of each round
  * (from the per-variable exit round).  Returns the number of rounds. */
 int lmmhip_round_profile(lmmhip_ctx* ctx, int64_t* alive_vars, int64_t* alive_elems, int cap);
+/* Per round of the last profiled maxmin solve: variables re-evaluated by the vote phase and their
+ * elements.  Returns the number of rounds. */
+int lmmhip_vote_profile(lmmhip_ctx* ctx, int64_t* reeval_vars, int64_t* reeval_elems, int cap);
 
 /* Number of visible HIP devices (0 when none; never initialises a context). */
 int lmmhip_device_count(void);

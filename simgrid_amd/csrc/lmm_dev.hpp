@@ -1,0 +1,154 @@
+// lmm_dev.hpp — device-side layout and helpers shared by the LMM kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+#include <cstdint>
+
+namespace lmmdev {
+
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kMaxBlocks = 2048;       // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond
+constexpr int kRowsPerThread = 8;      // compaction chunking
+constexpr int kCompactRows = kBlock * kRowsPerThread;
+constexpr unsigned kDeadKey = 0xFFFFu;  // > every key of a finite positive ratio (<= 0x7F80)
+
+// control block words (int32, zeroed at the start of every solve)
+enum : int {
+  CTL_DONE = 0,
+  CTL_ROUNDS = 1,
+  CTL_ANY0 = 2,      // fair bottleneck: "some variable still listed", per round parity (2 words)
+  CTL_NROWS = 4,     // alive-row buffer sizes (3 buffers)
+  CTL_NELEM = 7,     // alive-row buffer element counts (3 buffers)
+  CTL_ALIVE_C = 10,  // maxmin: constraints still in the light table
+  CTL_NREADY = 11,   // maxmin: ready-list length of the current round
+  CTL_NTOUCH0 = 12,  // maxmin: touched-list lengths, per round parity (2 words)
+  CTL_REEVAL = 14,   // maxmin: variables re-evaluated (statistics)
+  CTL_WORDS = 16
+};
+
+struct Dev {
+  int32_t nV, nC;
+  int64_t nnz;
+  // structure (uploaded once)
+  const uint32_t* var_ptr;   // [nV+1] CSR row offsets (variable-major)
+  const int32_t* csr_c;      // [nnz]
+  const double* csr_w;       // [nnz]
+  const uint32_t* cnst_ptr;  // [nC+1] CSC offsets (constraint-major)
+  const int32_t* csc_v;      // [nnz]
+  const double* csc_w;       // [nnz]
+  const double* pen;         // [nV]
+  const double* vbound;      // [nV]
+  const double* cbound;      // [nC]
+  const uint8_t* cflags;     // [nC] bit0 FATPIPE, bit1 zero-weight enabled element
+  // per-variable state
+  double* x;        // [nV] values (output)
+  int32_t* fixr;    // [nV] round in which the variable left the alive set (measurement only)
+  int32_t* vstate;  // [nV] maxmin: 0 alive, 1 fixed or dropped (claimed with atomicCAS)
+  int32_t* tgt;     // [nV] maxmin: constraint the variable currently votes for (-1: none)
+  double* vtmp;     // [nV] fair bottleneck: mu
+  uint8_t* vst;     // [nV] fair bottleneck: 1 listed / 0 not
+  // per-constraint state
+  double* ratio;    // [nC] remaining/usage, +inf when out of the light table
+  uint16_t* key;    // [nC] round-down 16-bit key of ratio, kDeadKey when out
+  double* rem;      // [nC]
+  double* use;      // [nC]
+  double* drem;     // [nC] atomic accumulators (SHARED constraints)
+  double* duse;     // [nC]
+  int32_t* acnt;    // [nC] alive (unfixed) elements
+  int32_t* dcnt;    // [nC] atomic accumulator of fixed elements
+  int32_t* votes;   // [nC] persistent: alive elements whose variable votes for this constraint
+  int32_t* chg;     // [nC] last round in which ratio / liveness changed
+  int32_t* ready;   // [nC] ready list (constraints that are local minima this round)
+  int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
+  // alive-row buffers: 0 = the original CSR (identity ids), 1/2 = compaction targets
+  const int32_t* cvar[3];
+  const uint32_t* crow[3];
+  const int32_t* ccol[3];
+  int32_t* bsum;    // compaction scratch: per-block rows / elems (2 x blocks)
+  int32_t* ctl;     // control words
+  int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
+};
+
+constexpr int kStatRounds = 4096;  // rounds covered by the profiling counters
+
+__device__ __forceinline__ double dinf() { return __builtin_huge_val(); }
+
+// 16-bit monotone key: round the ratio down to f32, keep the upper 16 bits (sign, exponent, 7 bits
+// of mantissa).  Monotone non-decreasing, so key(a) < key(b) => a < b; equal keys need the exact
+// fp64 comparison.
+__device__ __forceinline__ uint16_t ratio_key(double r) {
+  float f = __double2float_rd(r);
+  return uint16_t(__float_as_uint(f) >> 16);
+}
+
+template <int W> __device__ __forceinline__ double grp_min(double v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1)
+    v = fmin(v, __shfl_xor(v, o, W));
+  return v;
+}
+template <int W> __device__ __forceinline__ unsigned grp_umin(unsigned v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1)
+    v = min(v, (unsigned)__shfl_xor((int)v, o, W));
+  return v;
+}
+template <int W> __device__ __forceinline__ int grp_imin(int v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1)
+    v = min(v, __shfl_xor(v, o, W));
+  return v;
+}
+template <int W> __device__ __forceinline__ int grp_isum(int v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1)
+    v += __shfl_xor(v, o, W);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v = fmax(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v = fmin(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Append `pred` items to a global list with one atomic per wave (ballot + popcount).
+__device__ __forceinline__ int wave_append(bool pred, int32_t* counter) {
+  const unsigned long long m = __ballot(pred);
+  if (!m)
+    return -1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader)
+    base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader, kWave);
+  return pred ? base + __popcll(m & ((1ull << lane) - 1)) : -1;
+}
+
+inline int grid_for(int64_t n, int per_block) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g < 1)
+    g = 1;
+  if (g > kMaxBlocks)
+    g = kMaxBlocks;
+  return int(g);
+}
+
+}  // namespace lmmdev

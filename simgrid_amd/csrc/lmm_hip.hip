@@ -1,45 +1,21 @@
-// lmm_hip.hip — MI355X (gfx950, CDNA4) kernels of the LMM solver + the C ABI of include/lmm/lmm_hip.h.
+// lmm_hip.hip — device context + C ABI of include/lmm/lmm_hip.h for the MI355X (gfx950) LMM solver.
 //
-// The reference solves with two sequential CPU algorithms over boost::intrusive lists:
-//   * System::lmm_solve (src/kernel/lmm/maxmin.cpp:502-693): progressive filling — repeatedly find
-//     the constraint(s) with the globally smallest remaining/usage ratio (exact == ties,
-//     maxmin.cpp:397-409), fix their active variables at that level (or at their bound,
-//     maxmin.cpp:563-595), and update every constraint those variables touch (maxmin.cpp:601-659).
-//   * FairBottleneck::bottleneck_solve (fair_bottleneck.cpp:23-153): Jacobi rounds of three sweeps.
-//
-// maxmin on the device — "local-minimum parallel progressive filling" (DESIGN.md §3).  Ratios never
-// decrease, so a constraint whose ratio is <= the ratio of every constraint sharing an unfixed
-// variable with it saturates at exactly its current ratio in the sequential order too.  One round:
-//   mm_vote<G>   G lanes per alive variable (compacted rows): find the constraint(s) of minimal
-//                ratio through 16-bit monotone keys (round-down of the ratio: a 2 MB table per 10^6
-//                constraints that stays in L2), resolve key ties exactly in fp64, and cast one
-//                atomic "vote" for the minimal constraint(s).  A bounded variable whose level
-//                bound*penalty is below that minimum votes for nothing (maxmin.cpp:563-595).
-//   mm_fix       one thread per alive variable: its constraint is a local minimum iff every alive
-//                element voted for it (votes == alive element count); fix the variable at
-//                ratio/penalty (or at its bound) and push w*x, w/p and count decrements with atomics.
-//   mm_update    one thread per constraint: apply the decrements, clamp (surf_interface.hpp:34-44;
-//                clamping a sum of non-negative decrements == clamping after each one), drop
-//                saturated constraints (maxmin.cpp:608-623), refresh ratio and key; FATPIPE usage is
-//                recomputed as the max over still-unfixed elements (maxmin.cpp:625-658).
-// Every 16 rounds the alive rows are compacted (order preserving) so later rounds stream only live data.
-//
-// fair bottleneck — the reference's rounds are already bulk-synchronous; one round = three launches
-// mirroring fair_bottleneck.cpp:65-87, :89-105 and :107-144.
-//
+// Kernels: lmm_maxmin_kernels.hpp (System::lmm_solve, maxmin.cpp:487-693) and lmm_fb_kernels.hpp
+// (FairBottleneck::bottleneck_solve, fair_bottleneck.cpp:23-153); layout in lmm_dev.hpp.
 // All arithmetic is fp64; device code is compiled with -ffp-contract=off so every a*b+c rounds like the
 // reference (the FairBottleneck `value == bound` test is exact).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cfloat>
-#include <climits>
-#include <cstdio>
-#include <cstring>
 #include <string>
 #include <vector>
 
 #include "../../include/lmm/lmm_hip.h"
+#include "lmm_dev.hpp"
+#include "lmm_fb_kernels.hpp"
+#include "lmm_maxmin_kernels.hpp"
+
+using namespace lmmdev;
 
 namespace {
 
@@ -57,606 +33,6 @@ int fail(int code, const std::string& msg) {
       return fail(LMMHIP_E_HIP, std::string(#expr " -> ") + hipGetErrorString(e_) + " @" + __FILE__ + \
                                     ":" + std::to_string(__LINE__));                                    \
   } while (0)
-
-constexpr int kBlock = 256;
-constexpr int kWave = 64;
-constexpr int kMaxBlocks = 2048;       // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond
-constexpr int kRowsPerThread = 8;      // compaction chunking
-constexpr int kCompactRows = kBlock * kRowsPerThread;
-constexpr unsigned kDeadKey = 0xFFFFu;  // > every key of a finite positive ratio (<= 0x7F80)
-constexpr int kDrop = -1, kBound = -2;
-constexpr int kTieBit = 1 << 30;
-
-// control block words
-enum : int {
-  CTL_DONE = 0,
-  CTL_ROUNDS = 1,
-  CTL_ANY0 = 2,  // + parity
-  CTL_NROWS = 4, // + buffer (3 buffers)
-  CTL_NELEM = 8, // + buffer
-  CTL_WORDS = 16
-};
-
-struct Dev {
-  int32_t nV, nC;
-  int64_t nnz;
-  // structure (uploaded once)
-  const uint32_t* var_ptr;   // [nV+1] CSR row offsets (variable-major)
-  const int32_t* csr_c;      // [nnz]
-  const double* csr_w;       // [nnz]
-  const uint32_t* cnst_ptr;  // [nC+1] CSC offsets (constraint-major)
-  const int32_t* csc_v;      // [nnz]
-  const double* csc_w;       // [nnz]
-  const double* pen;         // [nV]
-  const double* vbound;      // [nV]
-  const double* cbound;      // [nC]
-  const uint8_t* cflags;     // [nC] bit0 FATPIPE, bit1 zero-weight enabled element
-  // per-variable state
-  double* x;       // [nV] values (output)
-  int32_t* fixr;   // [nV] round in which the variable left the alive set (measurement only)
-  double* vtmp;    // [nV] fair bottleneck: mu
-  uint8_t* vst;    // [nV] fair bottleneck: 1 listed / 0 not
-  // per-constraint state
-  double* ratio;   // [nC] remaining/usage, +inf when out of the light table
-  uint16_t* key;   // [nC] round-down 16-bit key of ratio, kDeadKey when out
-  double* rem;     // [nC]
-  double* use;     // [nC]
-  double* drem;    // [nC] atomic accumulators (SHARED constraints)
-  double* duse;    // [nC]
-  int32_t* acnt;   // [nC] alive (unfixed) elements
-  int32_t* dcnt;   // [nC] atomic accumulator of fixed elements
-  int32_t* votes;  // [nC]
-  // alive-row buffers: 0 = the original CSR (identity ids), 1/2 = compaction targets
-  const int32_t* cvar[3];
-  const uint32_t* crow[3];
-  const int32_t* ccol[3];
-  uint8_t* valive[3];
-  int32_t* vinfo;  // [nV] per-row result of mm_vote
-  int32_t* bsum;   // compaction scratch: per-block rows / elems (2 x blocks)
-  int32_t* ctl;    // control words
-};
-
-__device__ __forceinline__ double dinf() { return __builtin_huge_val(); }
-
-// 16-bit monotone key: round the ratio down to f32, keep the upper 16 bits (sign, exponent, 7 bits
-// of mantissa).  Monotone non-decreasing, so key(a) < key(b) => a < b; equal keys need the exact
-// fp64 comparison.
-__device__ __forceinline__ uint16_t ratio_key(double r) {
-  float f = __double2float_rd(r);
-  return uint16_t(__float_as_uint(f) >> 16);
-}
-
-template <int W> __device__ __forceinline__ double grp_min(double v) {
-#pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1)
-    v = fmin(v, __shfl_xor(v, o, W));
-  return v;
-}
-template <int W> __device__ __forceinline__ unsigned grp_umin(unsigned v) {
-#pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1)
-    v = min(v, (unsigned)__shfl_xor((int)v, o, W));
-  return v;
-}
-template <int W> __device__ __forceinline__ int grp_imax(int v) {
-#pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1)
-    v = max(v, __shfl_xor(v, o, W));
-  return v;
-}
-template <int W> __device__ __forceinline__ int grp_isum(int v) {
-#pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1)
-    v += __shfl_xor(v, o, W);
-  return v;
-}
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    v += __shfl_xor(v, o, kWave);
-  return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    v = fmax(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-    v = fmin(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-
-// =============================================================================================
-// maxmin (System::lmm_solve)
-// =============================================================================================
-
-// Init, one wave per constraint: maxmin.cpp:520-555.  remaining = bound; skipped when
-// bound <= bound*prec; usage = sum (SHARED) or max (FATPIPE) of w/p over the active elements.
-__global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wpb = kBlock / kWave;
-  int any = 0;
-  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
-    const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
-    const bool fat = s.cflags[c] & 1;
-    double acc = 0.0;
-    for (uint32_t j = b + lane; j < e; j += kWave) {
-      double u = s.csc_w[j] / s.pen[s.csc_v[j]];
-      acc = fat ? fmax(acc, u) : acc + u;
-    }
-    acc = fat ? wave_max(acc) : wave_sum(acc);
-    if (lane == 0) {
-      const double bound = s.cbound[c];
-      const bool part = bound > bound * prec;
-      const double usage = part ? acc : 0.0;
-      s.rem[c] = bound;
-      s.use[c] = usage;
-      s.drem[c] = 0.0;
-      s.duse[c] = 0.0;
-      s.acnt[c] = int32_t(e - b);
-      s.dcnt[c] = 0;
-      s.votes[c] = 0;
-      const bool alive = part && usage > 0;
-      const double r = bound / usage;
-      s.ratio[c] = alive ? r : dinf();
-      s.key[c] = alive ? ratio_key(r) : uint16_t(kDeadKey);
-      any |= alive;
-    }
-  }
-  if (any)
-    s.ctl[CTL_ANY0] = 1;
-}
-
-__global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
-    s.x[v] = 0.0;
-    s.fixr[v] = -1;
-    s.valive[0][v] = 1;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    s.ctl[CTL_NROWS + 0] = s.nV;
-    s.ctl[CTL_NELEM + 0] = int32_t(s.nnz);
-  }
-}
-
-// Round phase 1 — vote.  G lanes per alive row; all loops are wave-uniform so the group shuffles
-// always see their whole group.
-template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int buf, int par) {
-  if (s.ctl[CTL_DONE])
-    return;
-  if (!s.ctl[CTL_ANY0 + par]) {  // no constraint left in the light table: maxmin.cpp:680
-    s.ctl[CTL_DONE] = 1;
-    return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
-  const int64_t nrows = s.ctl[CTL_NROWS + buf];
-  const int32_t* __restrict__ cvar = s.cvar[buf];
-  const uint32_t* __restrict__ crow = s.crow[buf];
-  const int32_t* __restrict__ ccol = s.ccol[buf];
-  const uint8_t* __restrict__ valive = s.valive[buf];
-  const uint16_t* __restrict__ key = s.key;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane & (G - 1);
-  constexpr int kGpw = kWave / G;
-  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  for (int64_t base = wave * kGpw; base < nrows; base += nwaves * kGpw) {
-    const int64_t row = base + lane / G;
-    const bool valid = row < nrows && valive[row];
-    uint32_t b = 0, e = 0;
-    if (valid) {
-      b = crow[row];
-      e = crow[row + 1];
-    }
-    // pass 1: minimal key over the row
-    unsigned mk = kDeadKey;
-    for (uint32_t j = b + g; j < e; j += G)
-      mk = min(mk, (unsigned)key[ccol[j]]);
-    mk = grp_umin<G>(mk);
-    // pass 2: how many elements share it
-    int nmin = 0;
-    for (uint32_t j = b + g; j < e; j += G)
-      nmin += key[ccol[j]] == mk;
-    nmin = grp_isum<G>(nmin);
-    int v = valid ? cvar[row] : 0;
-    const double vb = valid ? s.vbound[v] : -1.0;
-    const bool live = valid && mk != kDeadKey;
-    // exact minimum only when the key is ambiguous or a bound has to be compared
-    double minr = dinf();
-    if (live && (nmin > 1 || vb > 0))
-      for (uint32_t j = b + g; j < e; j += G) {
-        const int32_t c = ccol[j];
-        if (key[c] == mk)
-          minr = fmin(minr, s.ratio[c]);
-      }
-    minr = grp_min<G>(minr);
-    const double lb = vb > 0 ? vb * s.pen[v] : dinf();
-    const bool bounded = live && vb > 0 && lb < minr;
-    int first = INT_MAX, last = -1;
-    if (live && !bounded)
-      for (uint32_t j = b + g; j < e; j += G) {
-        const int32_t c = ccol[j];
-        if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr)) {
-          atomicAdd(&s.votes[c], 1);
-          first = min(first, c);
-          last = max(last, c);
-        }
-      }
-    first = -grp_imax<G>(-first);
-    last = grp_imax<G>(last);
-    if (valid && g == 0) {
-      int code;
-      if (!live)
-        code = kDrop;
-      else if (bounded)
-        code = kBound;
-      else
-        code = first | (last != first ? kTieBit : 0);
-      s.vinfo[row] = code;
-    }
-  }
-}
-
-// Round phase 2 — fix.  maxmin.cpp:580-595 (value) and :601-606 (decrements).
-__global__ void __launch_bounds__(kBlock) mm_fix(Dev s, int buf, int round) {
-  if (s.ctl[CTL_DONE])
-    return;
-  const int64_t nrows = s.ctl[CTL_NROWS + buf];
-  const int32_t* __restrict__ cvar = s.cvar[buf];
-  uint8_t* valive = s.valive[buf];
-  for (int64_t row = int64_t(blockIdx.x) * kBlock + threadIdx.x; row < nrows; row += int64_t(gridDim.x) * kBlock) {
-    if (!valive[row])
-      continue;
-    const int code = s.vinfo[row];
-    const int v = cvar[row];
-    if (code == kDrop) {  // every constraint of v left the light table: v stays at 0
-      valive[row] = 0;
-      s.fixr[v] = round;
-      continue;
-    }
-    const double p = s.pen[v];
-    double xv = 0.0;
-    bool fix = false;
-    if (code == kBound) {
-      xv = s.vbound[v];
-      fix = true;
-    } else {
-      const int c = code & (kTieBit - 1);
-      if (s.votes[c] == s.acnt[c]) {
-        fix = true;
-        xv = s.ratio[c] / p;
-      } else if (code & kTieBit) {  // several minimal constraints: any of them saturating fixes v
-        const double r = s.ratio[c];
-        for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1] && !fix; j++) {
-          const int32_t c2 = s.csr_c[j];
-          if (c2 != c && s.ratio[c2] == r && s.votes[c2] == s.acnt[c2]) {
-            fix = true;
-            xv = r / p;
-          }
-        }
-      }
-    }
-    if (!fix)
-      continue;
-    s.x[v] = xv;
-    valive[row] = 0;
-    s.fixr[v] = round;
-    for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++) {
-      const int32_t c = s.csr_c[j];
-      if (s.key[c] == kDeadKey)
-        continue;
-      atomicAdd(&s.dcnt[c], 1);
-      if (!(s.cflags[c] & 1)) {
-        const double w = s.csr_w[j];
-        unsafeAtomicAdd(&s.drem[c], w * xv);
-        unsafeAtomicAdd(&s.duse[c], w / p);
-      }
-    }
-  }
-}
-
-// Round phase 3 — constraint update.  maxmin.cpp:603-658.
-__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int par, double prec) {
-  if (s.ctl[CTL_DONE])
-    return;
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_ROUNDS] += 1;
-  int any = 0;
-  for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < s.nC; c += int64_t(gridDim.x) * kBlock) {
-    if (s.key[c] == kDeadKey)
-      continue;
-    s.votes[c] = 0;
-    const int dc = s.dcnt[c];
-    if (!dc) {  // untouched: ratio unchanged
-      any = 1;
-      continue;
-    }
-    s.dcnt[c] = 0;
-    s.acnt[c] -= dc;
-    const double bound = s.cbound[c];
-    double rem = s.rem[c], use;
-    if (!(s.cflags[c] & 1)) {
-      use = s.use[c] - s.duse[c];
-      rem -= s.drem[c];
-      s.drem[c] = 0.0;
-      s.duse[c] = 0.0;
-      if (rem < bound * prec)
-        rem = 0.0;
-      if (use < prec)
-        use = 0.0;
-    } else {  // FATPIPE: usage = max w/p over enabled elements whose variable is still at 0
-      use = 0.0;
-      for (uint32_t j = s.cnst_ptr[c]; j < s.cnst_ptr[c + 1]; j++) {
-        const int32_t v = s.csc_v[j];
-        if (s.x[v] > 0)
-          continue;
-        use = fmax(use, s.csc_w[j] / s.pen[v]);
-      }
-    }
-    s.rem[c] = rem;
-    s.use[c] = use;
-    if (!(use > prec) || !(rem > bound * prec)) {
-      s.ratio[c] = dinf();
-      s.key[c] = kDeadKey;
-    } else {
-      const double r = rem / use;
-      s.ratio[c] = r;
-      s.key[c] = ratio_key(r);
-      any = 1;
-    }
-  }
-  if (any)
-    s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
-}
-
-// ---- order-preserving compaction of the alive rows: count / scan / write ----
-__device__ __forceinline__ void block_scan2(int& a, int& b, int* sh) {  // exclusive, kBlock threads
-  const int t = threadIdx.x;
-  sh[t] = a;
-  sh[kBlock + t] = b;
-  __syncthreads();
-  for (int o = 1; o < kBlock; o <<= 1) {
-    int xa = t >= o ? sh[t - o] : 0, xb = t >= o ? sh[kBlock + t - o] : 0;
-    __syncthreads();
-    sh[t] += xa;
-    sh[kBlock + t] += xb;
-    __syncthreads();
-  }
-  a = sh[t] - a;  // exclusive
-  b = sh[kBlock + t] - b;
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(kBlock) cmp_count(Dev s, int in) {
-  __shared__ int sh[2 * kBlock];
-  const int64_t nrows = s.ctl[CTL_NROWS + in];
-  const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
-  int nr = 0, ne = 0;
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t row = r0 + k;
-    if (row < nrows && s.valive[in][row]) {
-      nr++;
-      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
-    }
-  }
-  int a = nr, b = ne;
-  block_scan2(a, b, sh);
-  if (threadIdx.x == kBlock - 1) {
-    s.bsum[2 * blockIdx.x] = a + nr;
-    s.bsum[2 * blockIdx.x + 1] = b + ne;
-  }
-}
-
-__global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int out) {
-  __shared__ int sa[1024], sb[1024];
-  const int t = threadIdx.x;
-  const int per = (nblk + 1023) / 1024;
-  int a = 0, b = 0;
-  for (int i = t * per; i < (t + 1) * per && i < nblk; i++) {
-    a += s.bsum[2 * i];
-    b += s.bsum[2 * i + 1];
-  }
-  sa[t] = a;
-  sb[t] = b;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    int xa = t >= o ? sa[t - o] : 0, xb = t >= o ? sb[t - o] : 0;
-    __syncthreads();
-    sa[t] += xa;
-    sb[t] += xb;
-    __syncthreads();
-  }
-  int ra = sa[t] - a, rb = sb[t] - b;  // exclusive base of this thread's segment
-  for (int i = t * per; i < (t + 1) * per && i < nblk; i++) {
-    const int ca = s.bsum[2 * i], cb = s.bsum[2 * i + 1];
-    s.bsum[2 * i] = ra;
-    s.bsum[2 * i + 1] = rb;
-    ra += ca;
-    rb += cb;
-  }
-  if (t == 1023) {
-    s.ctl[CTL_NROWS + out] = sa[t];
-    s.ctl[CTL_NELEM + out] = sb[t];
-    const_cast<uint32_t*>(s.crow[out])[sa[t]] = uint32_t(sb[t]);
-  }
-}
-
-__global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
-  __shared__ int sh[2 * kBlock];
-  const int64_t nrows = s.ctl[CTL_NROWS + in];
-  const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
-  int nr = 0, ne = 0;
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t row = r0 + k;
-    if (row < nrows && s.valive[in][row]) {
-      nr++;
-      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
-    }
-  }
-  int pr = nr, pe = ne;
-  block_scan2(pr, pe, sh);
-  pr += s.bsum[2 * blockIdx.x];
-  pe += s.bsum[2 * blockIdx.x + 1];
-  int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
-  uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
-  int32_t* ocol = const_cast<int32_t*>(s.ccol[out]);
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t row = r0 + k;
-    if (row < nrows && s.valive[in][row]) {
-      const uint32_t b = s.crow[in][row], e = s.crow[in][row + 1];
-      ovar[pr] = s.cvar[in][row];
-      orow[pr] = uint32_t(pe);
-      s.valive[out][pr] = 1;
-      for (uint32_t j = b; j < e; j++)
-        ocol[pe++] = s.ccol[in][j];
-      pr++;
-    }
-  }
-}
-
-// =============================================================================================
-// FairBottleneck::bottleneck_solve
-// =============================================================================================
-
-__global__ void __launch_bounds__(kBlock) fb_init(Dev s) {
-  const int64_t n = s.nV > s.nC ? s.nV : s.nC;
-  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-    if (i < s.nV) {  // fair_bottleneck.cpp:29-41 (only listed variables are flattened)
-      s.x[i] = 0.0;
-      s.vtmp[i] = 0.0;
-      s.vst[i] = 1;
-      s.fixr[i] = -1;
-    }
-    if (i < s.nC) {  // :44-50
-      s.rem[i] = s.cbound[i];
-      s.use[i] = 0.0;
-      s.ratio[i] = 0.0;  // 0 = in the constraint list, +inf = erased
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_ANY0] = s.nV > 0;
-}
-
-// :65-87 — usage = remaining / (number of listed variables with w > 0), FATPIPE -> 1.
-__global__ void __launch_bounds__(kBlock) fb_cnst_share(Dev s, int par) {
-  if (s.ctl[CTL_DONE])
-    return;
-  if (!s.ctl[CTL_ANY0 + par]) {
-    s.ctl[CTL_DONE] = 1;
-    return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
-    s.ctl[CTL_ROUNDS] += 1;
-  }
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wpb = kBlock / kWave;
-  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
-    if (s.ratio[c] != 0.0)
-      continue;
-    int nb = 0;
-    for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave)
-      nb += s.vst[s.csc_v[j]];
-    nb = grp_isum<kWave>(nb);
-    if (lane == 0) {
-      if (nb > 0 && (s.cflags[c] & 1))
-        nb = 1;
-      if (nb == 0) {
-        s.rem[c] = 0.0;
-        s.use[c] = 0.0;
-        s.ratio[c] = dinf();
-      } else {
-        s.use[c] = s.rem[c] / nb;
-      }
-    }
-  }
-}
-
-// :89-105 — per listed variable: mu = min(usage/w, bound - value); value += mu; exact
-// `value == bound` drops it from the list.
-__global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) {
-  if (s.ctl[CTL_DONE])
-    return;
-  int any = 0;
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
-    if (!s.vst[v])
-      continue;
-    double inc = DBL_MAX;
-    for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
-      inc = fmin(inc, s.use[s.csr_c[j]] / s.csr_w[j]);
-    const double vb = s.vbound[v];
-    double x = s.x[v];
-    if (vb > 0)
-      inc = fmin(inc, vb - x);
-    s.vtmp[v] = inc;
-    x += inc;
-    s.x[v] = x;
-    if (x == vb)
-      s.vst[v] = 0;
-    else
-      any = 1;
-    s.fixr[v] = round;  // last round in which v was listed
-  }
-  if (any)
-    s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
-}
-
-// :107-144 — remaining -= sum w*mu over ALL enabled elements (stale mu of variables that already
-// left the list included), FATPIPE: remaining -= min(usage, min w*mu); remaining <= 0 erases the
-// constraint and every listed variable on it.
-__global__ void __launch_bounds__(kBlock) fb_cnst_update(Dev s, double prec) {
-  if (s.ctl[CTL_DONE])
-    return;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wpb = kBlock / kWave;
-  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
-    if (s.ratio[c] != 0.0)
-      continue;
-    const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
-    const bool fat = s.cflags[c] & 1;
-    double acc = fat ? dinf() : 0.0;
-    for (uint32_t j = b + lane; j < e; j += kWave) {
-      const double d = s.csc_w[j] * s.vtmp[s.csc_v[j]];
-      acc = fat ? fmin(acc, d) : acc + d;
-    }
-    acc = fat ? wave_min(acc) : wave_sum(acc);
-    double rem = s.rem[c];
-    if (!fat) {
-      rem -= acc;
-    } else {
-      double u = s.use[c];
-      if (s.cflags[c] & 2)
-        u = fmin(u, 0.0);
-      u = fmin(u, acc);
-      s.use[c] = u;
-      rem -= u;
-    }
-    if (rem < prec)
-      rem = 0.0;
-    const bool erase = rem <= 0.0;
-    if (lane == 0) {
-      s.rem[c] = rem;
-      if (erase)
-        s.ratio[c] = dinf();
-    }
-    if (erase)
-      for (uint32_t j = b + lane; j < e; j += kWave)
-        s.vst[s.csc_v[j]] = 0;
-  }
-}
-
-int grid_for(int64_t n, int per_block) {
-  int64_t g = (n + per_block - 1) / per_block;
-  if (g < 1)
-    g = 1;
-  if (g > kMaxBlocks)
-    g = kMaxBlocks;
-  return int(g);
-}
 
 }  // namespace
 
@@ -680,6 +56,7 @@ struct lmmhip_ctx {
   std::vector<int> launch_slot, launch_round;
   std::vector<float> launch_ms;
   lmmhip_stats stats{};
+  int32_t* vstat = nullptr;  // profiling counters of mm_vote ([round][block] x 2)
 };
 
 static void free_all(lmmhip_ctx* c) {
@@ -751,6 +128,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   free_all(c);
   if (c->h_ctl)
     (void)hipHostFree(c->h_ctl);
+  if (c->vstat)
+    (void)hipFree(c->vstat);
   if (c->ev0)
     (void)hipEventDestroy(c->ev0);
   if (c->ev1)
@@ -856,9 +235,10 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &crow2, nV + 1);
   rc |= dalloc(c, &ccol1, nnz);
   rc |= dalloc(c, &ccol2, nnz);
-  for (int b = 0; b < 3; b++)
-    rc |= dalloc(c, &d.valive[b], nV);
-  rc |= dalloc(c, &d.vinfo, nV);
+  rc |= dalloc(c, &d.vstate, nV);
+  rc |= dalloc(c, &d.tgt, nV);
+  rc |= dalloc(c, &d.chg, nC);
+  rc |= dalloc(c, &d.ready, nC);
   rc |= dalloc(c, &d.bsum, 2 * nblk);
   rc |= dalloc(c, &d.ctl, CTL_WORDS);
   if (rc) {
@@ -962,6 +342,12 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   c->launch_round.clear();
   c->launch_ms.clear();
   HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+  const size_t stat_bytes = sizeof(int32_t) * 2 * size_t(kStatRounds) * kMaxBlocks;
+  if (c->profiling && !c->vstat)
+    HIPCHK(hipMalloc(&c->vstat, stat_bytes));
+  c->d.vstat = c->profiling ? c->vstat : nullptr;
+  if (c->profiling)
+    HIPCHK(hipMemsetAsync(c->vstat, 0, stat_bytes, c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   int rc = kind == LMMHIP_KIND_MAXMIN ? solve_maxmin(c, precision) : solve_fair(c, precision);
   if (rc)
@@ -1026,31 +412,32 @@ static int poll_ctl(lmmhip_ctx* c) {
   return 0;
 }
 
-static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf, int par) {
+static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   const Dev& d = c->d;
   const int G = c->group;
   const int grid = grid_for(nrows * G, kBlock);
   switch (G) {
   case 4:
-    LAUNCH(2, r, mm_vote<4>, grid, kBlock, d, buf, par);
+    LAUNCH(2, r, mm_vote<4>, grid, kBlock, d, buf, int(r));
     break;
   case 8:
-    LAUNCH(2, r, mm_vote<8>, grid, kBlock, d, buf, par);
+    LAUNCH(2, r, mm_vote<8>, grid, kBlock, d, buf, int(r));
     break;
   case 16:
-    LAUNCH(2, r, mm_vote<16>, grid, kBlock, d, buf, par);
+    LAUNCH(2, r, mm_vote<16>, grid, kBlock, d, buf, int(r));
     break;
   case 32:
-    LAUNCH(2, r, mm_vote<32>, grid, kBlock, d, buf, par);
+    LAUNCH(2, r, mm_vote<32>, grid, kBlock, d, buf, int(r));
     break;
   default:
-    LAUNCH(2, r, mm_vote<64>, grid, kBlock, d, buf, par);
+    LAUNCH(2, r, mm_vote<64>, grid, kBlock, d, buf, int(r));
     break;
   }
   return 0;
 }
 
-// Slots: 0 mm_init_cnsts, 1 mm_init_vars, 2 mm_vote, 3 mm_fix, 4 mm_update, 5 compaction.
+// Slots: 0 mm_init_cnsts, 1 mm_init_vars, 2 mm_vote, 3 mm_ready, 4 mm_saturate, 5 mm_update,
+// 6 compaction.
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
@@ -1062,13 +449,12 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   int64_t r = 0, last_compact = 0, nrows = d.nV;
   int buf = 0, chunk = 2;
   for (;;) {
-    const int gR = grid_for(nrows, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
-      const int par = int(r & 1);
-      if (int rc = launch_vote(c, r, nrows, buf, par))
+      if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
-      LAUNCH(3, r, mm_fix, gR, kBlock, d, buf, int(r));
-      LAUNCH(4, r, mm_update, gC, kBlock, d, par, prec);
+      LAUNCH(3, r, mm_ready, gC, kBlock, d);
+      LAUNCH(4, r, mm_saturate, kMaxBlocks, kBlock, d, int(r));
+      LAUNCH(5, r, mm_update, gC, kBlock, d, int(r), prec);
     }
     if (int rc = poll_ctl(c))
       return rc;
@@ -1079,13 +465,16 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     if (r - last_compact >= 16 && nrows > 4096) {  // order-preserving compaction of the alive rows
       const int out = buf == 1 ? 2 : 1;
       const int nblk = int((nrows + kCompactRows - 1) / kCompactRows);
-      LAUNCH(5, r, cmp_count, nblk, kBlock, d, buf);
-      LAUNCH(5, r, cmp_scan, 1, 1024, d, nblk, out);
-      LAUNCH(5, r, cmp_write, nblk, kBlock, d, buf, out);
+      LAUNCH(6, r, cmp_count, nblk, kBlock, d, buf);
+      LAUNCH(6, r, cmp_scan, 1, 1024, d, nblk, out);
       if (int rc = poll_ctl(c))
         return rc;
-      nrows = c->h_ctl[CTL_NROWS + out];
-      buf = out;
+      const int64_t alive_rows = c->h_ctl[CTL_NROWS + out];
+      if (alive_rows < nrows * 3 / 4) {  // worth rewriting
+        LAUNCH(6, r, cmp_write, nblk, kBlock, d, buf, out);
+        nrows = alive_rows;
+        buf = out;
+      }
       last_compact = r;
     }
     if (chunk < 16)
@@ -1168,6 +557,25 @@ int lmmhip_round_profile(lmmhip_ctx* c, int64_t* alive_vars, int64_t* alive_elem
       alive_vars[r] = av;
       alive_elems[r] = ae;
     }
+  }
+  return R;
+}
+
+int lmmhip_vote_profile(lmmhip_ctx* c, int64_t* rows, int64_t* elems, int cap) {
+  if (!c || !c->vstat)
+    return fail(LMMHIP_E_STATE, "no profiled maxmin solve");
+  const int R = int(std::min<int64_t>(c->stats.rounds, kStatRounds));
+  std::vector<int32_t> h(size_t(2) * kStatRounds * kMaxBlocks);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(h.data(), c->vstat, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost));
+  for (int r = 0; r < R && r < cap; r++) {
+    int64_t a = 0, b = 0;
+    for (int k = 0; k < kMaxBlocks; k++) {
+      a += h[2 * (size_t(r) * kMaxBlocks + k)];
+      b += h[2 * (size_t(r) * kMaxBlocks + k) + 1];
+    }
+    rows[r] = a;
+    elems[r] = b;
   }
   return R;
 }

@@ -1,0 +1,406 @@
+// lmm_maxmin_kernels.hpp — System::lmm_solve on gfx950 (included by lmm_hip.hip).
+//
+// Local-minimum parallel progressive filling with persistent votes:
+//   every alive variable votes for ONE constraint of minimal ratio among its constraints (ties:
+//   smallest id — the smallest-id constraint of the global-minimum set then always collects every
+//   vote, so each round makes progress).  Ratios never decrease, so a vote stays valid until the
+//   voted constraint's ratio changes: only variables whose target changed in the previous round are
+//   re-evaluated.  A constraint is a local minimum ("ready") iff every alive element votes for it.
+//
+// Round r (4 launches):
+//   mm_vote<G>   re-evaluate the variables whose target changed in round r-1 (G lanes per row):
+//                minimal 16-bit key over the row, exact fp64 only on key ties / bound checks; move
+//                the vote; a variable whose level bound*penalty is below its minimum is fixed at its
+//                bound right here (maxmin.cpp:563-595); a variable with no alive constraint drops.
+//   mm_ready     one thread per constraint: votes == alive elements -> ready list.
+//   mm_saturate  one wave per ready constraint: claim its alive variables (atomicCAS), fix them at
+//                ratio/penalty (maxmin.cpp:583), push w*x, w/p and count decrements (maxmin.cpp:601-606).
+//   mm_update    one thread per constraint: apply decrements, clamp (surf_interface.hpp:34-44 —
+//                clamping a sum of non-negative decrements == clamping after each one), drop
+//                saturated constraints (maxmin.cpp:608-623), refresh ratio, key and change stamp;
+//                FATPIPE usage is recomputed over the still-unfixed elements (maxmin.cpp:625-658).
+#pragma once
+#include "lmm_dev.hpp"
+
+namespace lmmdev {
+
+// Init, one wave per constraint: maxmin.cpp:520-555.  remaining = bound; skipped when
+// bound <= bound*prec; usage = sum (SHARED) or max (FATPIPE) of w/p over the active elements.
+__global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wpb = kBlock / kWave;
+  int alive_cnt = 0;
+  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
+    const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
+    const bool fat = s.cflags[c] & 1;
+    double acc = 0.0;
+    for (uint32_t j = b + lane; j < e; j += kWave) {
+      double u = s.csc_w[j] / s.pen[s.csc_v[j]];
+      acc = fat ? fmax(acc, u) : acc + u;
+    }
+    acc = fat ? wave_max(acc) : wave_sum(acc);
+    if (lane == 0) {
+      const double bound = s.cbound[c];
+      const bool part = bound > bound * prec;
+      const double usage = part ? acc : 0.0;
+      s.rem[c] = bound;
+      s.use[c] = usage;
+      s.drem[c] = 0.0;
+      s.duse[c] = 0.0;
+      s.acnt[c] = int32_t(e - b);
+      s.dcnt[c] = 0;
+      s.votes[c] = 0;
+      s.chg[c] = -1;
+      const bool alive = part && usage > 0;
+      const double r = bound / usage;
+      s.ratio[c] = alive ? r : dinf();
+      s.key[c] = alive ? ratio_key(r) : uint16_t(kDeadKey);
+      alive_cnt += alive;
+    }
+  }
+  if (lane == 0 && alive_cnt)
+    atomicAdd(&s.ctl[CTL_ALIVE_C], alive_cnt);
+}
+
+__global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
+    s.x[v] = 0.0;
+    s.fixr[v] = -1;
+    s.vstate[v] = 0;
+    s.tgt[v] = -1;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    s.ctl[CTL_NROWS + 0] = s.nV;
+    s.ctl[CTL_NELEM + 0] = int32_t(s.nnz);
+  }
+}
+
+// Decrements of a fixed variable's element j (maxmin.cpp:601-606); FATPIPE constraints only count.
+__device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double xv, double p) {
+  const int32_t c = s.csr_c[j];
+  if (s.key[c] == kDeadKey)
+    return;
+  atomicAdd(&s.dcnt[c], 1);
+  if (!(s.cflags[c] & 1)) {
+    const double w = s.csr_w[j];
+    unsafeAtomicAdd(&s.drem[c], w * xv);
+    unsafeAtomicAdd(&s.duse[c], w / p);
+  }
+}
+
+// Round phase 1 — (re-)vote.  G lanes per alive row; loops are wave-uniform so the group shuffles
+// always see their whole group.
+template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int buf, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (s.ctl[CTL_ALIVE_C] <= 0) {  // light table empty: maxmin.cpp:680
+    s.ctl[CTL_DONE] = 1;
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_NREADY] = 0;
+  __shared__ int st_rows, st_elems;  // profiling counters (LDS, one store per block)
+  if (s.vstat && threadIdx.x == 0)
+    st_rows = st_elems = 0;
+  if (s.vstat)
+    __syncthreads();
+  const int64_t nrows = s.ctl[CTL_NROWS + buf];
+  const int32_t* __restrict__ cvar = s.cvar[buf];
+  const uint32_t* __restrict__ crow = s.crow[buf];
+  const int32_t* __restrict__ ccol = s.ccol[buf];
+  const uint16_t* __restrict__ key = s.key;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane & (G - 1);
+  constexpr int kGpw = kWave / G;
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+  for (int64_t base = wave * kGpw; base < nrows; base += nwaves * kGpw) {
+    const int64_t row = base + lane / G;
+    bool valid = row < nrows;
+    const int v = valid ? cvar[row] : 0;
+    valid = valid && s.vstate[v] == 0;
+    const int t = valid ? s.tgt[v] : -1;
+    const bool need = valid && (t < 0 || s.chg[t] == round - 1);
+    uint32_t b = 0, e = 0;
+    if (need) {
+      b = crow[row];
+      e = crow[row + 1];
+      if (s.vstat && g == 0) {
+        atomicAdd(&st_rows, 1);
+        atomicAdd(&st_elems, int(e - b));
+      }
+    }
+    unsigned mk = kDeadKey;
+    for (uint32_t j = b + g; j < e; j += G)
+      mk = min(mk, (unsigned)key[ccol[j]]);
+    mk = grp_umin<G>(mk);
+    int nmin = 0;
+    for (uint32_t j = b + g; j < e; j += G)
+      nmin += key[ccol[j]] == mk;
+    nmin = grp_isum<G>(nmin);
+    const double vb = need ? s.vbound[v] : -1.0;
+    const bool live = need && mk != kDeadKey;
+    double minr = dinf();
+    if (live && (nmin > 1 || vb > 0))
+      for (uint32_t j = b + g; j < e; j += G) {
+        const int32_t c = ccol[j];
+        if (key[c] == mk)
+          minr = fmin(minr, s.ratio[c]);
+      }
+    minr = grp_min<G>(minr);
+    const double p = need ? s.pen[v] : 1.0;
+    const bool bounded = live && vb > 0 && vb * p < minr;
+    int newt = INT_MAX;
+    if (live && !bounded)
+      for (uint32_t j = b + g; j < e; j += G) {
+        const int32_t c = ccol[j];
+        if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
+          newt = min(newt, c);
+      }
+    newt = grp_imin<G>(newt);
+    int mult_new = 0, mult_old = 0;
+    for (uint32_t j = b + g; j < e; j += G) {
+      const int32_t c = ccol[j];
+      mult_new += c == newt;
+      mult_old += c == t;
+    }
+    mult_new = grp_isum<G>(mult_new);
+    mult_old = grp_isum<G>(mult_old);
+    if (need && !live) {  // every constraint of v left the light table: v stays at 0
+      if (g == 0) {
+        s.vstate[v] = 1;
+        s.fixr[v] = round;
+      }
+    } else if (bounded) {  // fixed at its bound (maxmin.cpp:587-589)
+      if (g == 0) {
+        s.vstate[v] = 1;
+        s.fixr[v] = round;
+        s.x[v] = vb;
+        if (t >= 0 && key[t] != kDeadKey)
+          atomicSub(&s.votes[t], mult_old);
+      }
+      for (uint32_t j = s.var_ptr[v] + g; j < s.var_ptr[v + 1]; j += G)
+        push_decrement(s, j, vb, p);
+    } else if (live && newt != t && g == 0) {
+      if (t >= 0 && key[t] != kDeadKey)
+        atomicSub(&s.votes[t], mult_old);
+      atomicAdd(&s.votes[newt], mult_new);
+      s.tgt[v] = newt;
+    }
+  }
+  if (s.vstat) {
+    __syncthreads();
+    if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
+      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x)] = st_rows;
+      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x) + 1] = st_elems;
+    }
+  }
+}
+
+// Round phase 2 — ready list: constraints every alive element votes for.
+__global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int64_t n = s.nC;
+  for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
+    const int64_t c = base + threadIdx.x;
+    const bool rdy = c < n && s.key[c] != kDeadKey && s.votes[c] == s.acnt[c];
+    const int pos = wave_append(rdy, &s.ctl[CTL_NREADY]);
+    if (rdy)
+      s.ready[pos] = int32_t(c);
+  }
+}
+
+// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.
+__global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int nready = s.ctl[CTL_NREADY];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+  for (int64_t i = wave; i < nready; i += nwaves) {
+    const int32_t c = s.ready[i];
+    const double r = s.ratio[c];
+    for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave) {
+      const int32_t v = s.csc_v[j];
+      if (s.vstate[v] != 0 || atomicCAS(&s.vstate[v], 0, 1) != 0)
+        continue;
+      const double p = s.pen[v];
+      const double xv = r / p;
+      s.x[v] = xv;
+      s.fixr[v] = round;
+      int mult = 0;
+      for (uint32_t k = s.var_ptr[v]; k < s.var_ptr[v + 1]; k++) {
+        mult += s.csr_c[k] == c;
+        push_decrement(s, k, xv, p);
+      }
+      atomicSub(&s.votes[c], mult);
+    }
+  }
+}
+
+// Round phase 4 — constraint update: maxmin.cpp:603-658.
+__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_ROUNDS] += 1;
+  int died = 0;
+  for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < s.nC; c += int64_t(gridDim.x) * kBlock) {
+    if (s.key[c] == kDeadKey)
+      continue;
+    const int dc = s.dcnt[c];
+    if (!dc)  // untouched: ratio unchanged
+      continue;
+    s.dcnt[c] = 0;
+    s.acnt[c] -= dc;
+    s.chg[c] = round;
+    const double bound = s.cbound[c];
+    double rem = s.rem[c], use;
+    if (!(s.cflags[c] & 1)) {
+      use = s.use[c] - s.duse[c];
+      rem -= s.drem[c];
+      s.drem[c] = 0.0;
+      s.duse[c] = 0.0;
+      if (rem < bound * prec)
+        rem = 0.0;
+      if (use < prec)
+        use = 0.0;
+    } else {  // FATPIPE: usage = max w/p over enabled elements whose variable is still at 0
+      use = 0.0;
+      for (uint32_t j = s.cnst_ptr[c]; j < s.cnst_ptr[c + 1]; j++) {
+        const int32_t v = s.csc_v[j];
+        if (s.x[v] > 0)
+          continue;
+        use = fmax(use, s.csc_w[j] / s.pen[v]);
+      }
+    }
+    s.rem[c] = rem;
+    s.use[c] = use;
+    if (!(use > prec) || !(rem > bound * prec)) {
+      s.ratio[c] = dinf();
+      s.key[c] = kDeadKey;
+      died++;
+    } else {
+      const double r = rem / use;
+      s.ratio[c] = r;
+      s.key[c] = ratio_key(r);
+    }
+  }
+  // one atomic per wave for the light-table size
+  for (int o = 32; o > 0; o >>= 1)
+    died += __shfl_xor(died, o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0 && died)
+    atomicSub(&s.ctl[CTL_ALIVE_C], died);
+}
+
+// ---- order-preserving compaction of the alive rows: count / scan / write ----
+__device__ __forceinline__ void block_scan2(int& a, int& b, int* sh) {  // exclusive, kBlock threads
+  const int t = threadIdx.x;
+  sh[t] = a;
+  sh[kBlock + t] = b;
+  __syncthreads();
+  for (int o = 1; o < kBlock; o <<= 1) {
+    int xa = t >= o ? sh[t - o] : 0, xb = t >= o ? sh[kBlock + t - o] : 0;
+    __syncthreads();
+    sh[t] += xa;
+    sh[kBlock + t] += xb;
+    __syncthreads();
+  }
+  a = sh[t] - a;
+  b = sh[kBlock + t] - b;
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool row_alive(const Dev& s, int in, int64_t row) {
+  return s.vstate[s.cvar[in][row]] == 0;
+}
+
+__global__ void __launch_bounds__(kBlock) cmp_count(Dev s, int in) {
+  __shared__ int sh[2 * kBlock];
+  const int64_t nrows = s.ctl[CTL_NROWS + in];
+  const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
+  int nr = 0, ne = 0;
+  for (int k = 0; k < kRowsPerThread; k++) {
+    const int64_t row = r0 + k;
+    if (row < nrows && row_alive(s, in, row)) {
+      nr++;
+      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
+    }
+  }
+  int a = nr, b = ne;
+  block_scan2(a, b, sh);
+  if (threadIdx.x == kBlock - 1) {
+    s.bsum[2 * blockIdx.x] = a + nr;
+    s.bsum[2 * blockIdx.x + 1] = b + ne;
+  }
+}
+
+__global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int out) {
+  __shared__ int sa[1024], sb[1024];
+  const int t = threadIdx.x;
+  const int per = (nblk + 1023) / 1024;
+  int a = 0, b = 0;
+  for (int i = t * per; i < (t + 1) * per && i < nblk; i++) {
+    a += s.bsum[2 * i];
+    b += s.bsum[2 * i + 1];
+  }
+  sa[t] = a;
+  sb[t] = b;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    int xa = t >= o ? sa[t - o] : 0, xb = t >= o ? sb[t - o] : 0;
+    __syncthreads();
+    sa[t] += xa;
+    sb[t] += xb;
+    __syncthreads();
+  }
+  int ra = sa[t] - a, rb = sb[t] - b;  // exclusive base of this thread's segment
+  for (int i = t * per; i < (t + 1) * per && i < nblk; i++) {
+    const int ca = s.bsum[2 * i], cb = s.bsum[2 * i + 1];
+    s.bsum[2 * i] = ra;
+    s.bsum[2 * i + 1] = rb;
+    ra += ca;
+    rb += cb;
+  }
+  if (t == 1023) {
+    s.ctl[CTL_NROWS + out] = sa[t];
+    s.ctl[CTL_NELEM + out] = sb[t];
+    const_cast<uint32_t*>(s.crow[out])[sa[t]] = uint32_t(sb[t]);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
+  __shared__ int sh[2 * kBlock];
+  const int64_t nrows = s.ctl[CTL_NROWS + in];
+  const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
+  int nr = 0, ne = 0;
+  for (int k = 0; k < kRowsPerThread; k++) {
+    const int64_t row = r0 + k;
+    if (row < nrows && row_alive(s, in, row)) {
+      nr++;
+      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
+    }
+  }
+  int pr = nr, pe = ne;
+  block_scan2(pr, pe, sh);
+  pr += s.bsum[2 * blockIdx.x];
+  pe += s.bsum[2 * blockIdx.x + 1];
+  int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
+  uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
+  int32_t* ocol = const_cast<int32_t*>(s.ccol[out]);
+  for (int k = 0; k < kRowsPerThread; k++) {
+    const int64_t row = r0 + k;
+    if (row < nrows && row_alive(s, in, row)) {
+      const uint32_t b = s.crow[in][row], e = s.crow[in][row + 1];
+      ovar[pr] = s.cvar[in][row];
+      orow[pr] = uint32_t(pe);
+      for (uint32_t j = b; j < e; j++)
+        ocol[pe++] = s.ccol[in][j];
+      pr++;
+    }
+  }
+}
+
+}  // namespace lmmdev

@@ -82,6 +82,7 @@ SIGNATURES = {
     "lmmhip_set_profiling": (I, [P, I]),
     "lmmhip_launch_profile": (I, [P, PI, PI, ct.POINTER(ct.c_float), I]),
     "lmmhip_round_profile": (I, [P, PI64, PI64, I]),
+    "lmmhip_vote_profile": (I, [P, PI64, PI64, I]),
     "lmmhip_device_count": (I, []),
     "lmmhip_last_error": (ct.c_char_p, []),
 }
@@ -322,6 +323,16 @@ class System:
         if r < 0:
             raise LmmError(lib().lmmhip_last_error().decode())
         return av[:r], ae[:r]
+
+    def vote_profile(self):
+        """Re-evaluated variables / elements per round of the last profiled maxmin solve."""
+        c = self.device_ctx()
+        cap = 1 << 16
+        rv, re_ = np.zeros(cap, np.int64), np.zeros(cap, np.int64)
+        r = lib().lmmhip_vote_profile(c, rv.ctypes.data_as(PI64), re_.ctypes.data_as(PI64), cap)
+        if r < 0:
+            raise LmmError(lib().lmmhip_last_error().decode())
+        return rv[:r], re_[:r]
 
     @property
     def modified(self):
