@@ -415,7 +415,7 @@ static int poll_ctl(lmmhip_ctx* c) {
 static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   const Dev& d = c->d;
   const int G = c->group;
-  const int grid = grid_for(nrows * G, kBlock);
+  const int grid = grid_for(nrows, kBlock);  // one lane per row in the work-queue scan
   switch (G) {
   case 4:
     LAUNCH(2, r, mm_vote<4>, grid, kBlock, d, buf, int(r));

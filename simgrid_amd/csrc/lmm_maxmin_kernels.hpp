@@ -114,58 +114,85 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
   constexpr int kGpw = kWave / G;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  for (int64_t base = wave * kGpw; base < nrows; base += nwaves * kGpw) {
-    const int64_t row = base + lane / G;
-    bool valid = row < nrows;
-    const int v = valid ? cvar[row] : 0;
-    valid = valid && s.vstate[v] == 0;
-    const int t = valid ? s.tgt[v] : -1;
-    const bool need = valid && (t < 0 || s.chg[t] == round - 1);
-    uint32_t b = 0, e = 0;
-    if (need) {
-      b = crow[row];
-      e = crow[row + 1];
-      if (s.vstat && g == 0) {
-        atomicAdd(&st_rows, 1);
-        atomicAdd(&st_elems, int(e - b));
+  // One lane per row decides whether the row needs work (its target changed last round); the rows
+  // that do are then processed kGpw at a time (one G-lane group each), so a wave only pays for the
+  // rows that need it.
+  for (int64_t base = wave * kWave; base < nrows; base += nwaves * kWave) {
+    const int64_t lrow = base + lane;
+    bool lvalid = lrow < nrows;
+    const int lv = lvalid ? cvar[lrow] : 0;
+    lvalid = lvalid && s.vstate[lv] == 0;
+    const int lt = lvalid ? s.tgt[lv] : -1;
+    const bool lneed = lvalid && (lt < 0 || s.chg[lt] == round - 1);
+    unsigned long long mask = __ballot(lneed);
+    while (mask) {  // wave-uniform
+      unsigned long long m = mask;
+      for (int i = 0; i < lane / G; i++)
+        m &= m - 1;
+      const int pos = m ? __ffsll((long long)m) - 1 : -1;
+      for (int i = 0; i < kGpw; i++)
+        mask &= mask - 1;
+      const int src = pos < 0 ? 0 : pos;
+      const int v = __shfl(lv, src, kWave);
+      const int t = __shfl(lt, src, kWave);
+      const bool need = pos >= 0;
+      const int64_t row = base + src;
+      uint32_t b = 0, e = 0;
+      if (need) {
+        b = crow[row];
+        e = crow[row + 1];
+        if (s.vstat && g == 0) {
+          atomicAdd(&st_rows, 1);
+          atomicAdd(&st_elems, int(e - b));
+        }
       }
-    }
-    unsigned mk = kDeadKey;
-    for (uint32_t j = b + g; j < e; j += G)
-      mk = min(mk, (unsigned)key[ccol[j]]);
-    mk = grp_umin<G>(mk);
-    int nmin = 0;
-    for (uint32_t j = b + g; j < e; j += G)
-      nmin += key[ccol[j]] == mk;
-    nmin = grp_isum<G>(nmin);
-    const double vb = need ? s.vbound[v] : -1.0;
-    const bool live = need && mk != kDeadKey;
-    double minr = dinf();
-    if (live && (nmin > 1 || vb > 0))
-      for (uint32_t j = b + g; j < e; j += G) {
+      // the lane's first element stays in registers; rows longer than G loop over the rest
+      const uint32_t j0 = b + g;
+      const bool h0 = j0 < e;
+      const int32_t c0 = h0 ? ccol[j0] : -1;
+      const unsigned k0 = h0 ? key[c0] : kDeadKey;
+      unsigned mk = k0;
+      for (uint32_t j = j0 + G; j < e; j += G)
+        mk = min(mk, (unsigned)key[ccol[j]]);
+      mk = grp_umin<G>(mk);
+      int nmin = h0 && k0 == mk;
+      for (uint32_t j = j0 + G; j < e; j += G)
+        nmin += key[ccol[j]] == mk;
+      nmin = grp_isum<G>(nmin);
+      const double vb = need ? s.vbound[v] : -1.0;
+      const bool live = need && mk != kDeadKey;
+      double minr = dinf();
+      if (live && (nmin > 1 || vb > 0)) {
+        if (h0 && k0 == mk)
+          minr = s.ratio[c0];
+        for (uint32_t j = j0 + G; j < e; j += G) {
+          const int32_t c = ccol[j];
+          if (key[c] == mk)
+            minr = fmin(minr, s.ratio[c]);
+        }
+      }
+      minr = grp_min<G>(minr);
+      const double p = need ? s.pen[v] : 1.0;
+      const bool bounded = live && vb > 0 && vb * p < minr;
+      int newt = INT_MAX;
+      if (live && !bounded) {
+        if (h0 && k0 == mk && (nmin == 1 || s.ratio[c0] == minr))
+          newt = c0;
+        for (uint32_t j = j0 + G; j < e; j += G) {
+          const int32_t c = ccol[j];
+          if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
+            newt = min(newt, c);
+        }
+      }
+      newt = grp_imin<G>(newt);
+      int mult_new = h0 && c0 == newt, mult_old = h0 && c0 == t;
+      for (uint32_t j = j0 + G; j < e; j += G) {
         const int32_t c = ccol[j];
-        if (key[c] == mk)
-          minr = fmin(minr, s.ratio[c]);
+        mult_new += c == newt;
+        mult_old += c == t;
       }
-    minr = grp_min<G>(minr);
-    const double p = need ? s.pen[v] : 1.0;
-    const bool bounded = live && vb > 0 && vb * p < minr;
-    int newt = INT_MAX;
-    if (live && !bounded)
-      for (uint32_t j = b + g; j < e; j += G) {
-        const int32_t c = ccol[j];
-        if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
-          newt = min(newt, c);
-      }
-    newt = grp_imin<G>(newt);
-    int mult_new = 0, mult_old = 0;
-    for (uint32_t j = b + g; j < e; j += G) {
-      const int32_t c = ccol[j];
-      mult_new += c == newt;
-      mult_old += c == t;
-    }
-    mult_new = grp_isum<G>(mult_new);
-    mult_old = grp_isum<G>(mult_old);
+      mult_new = grp_isum<G>(mult_new);
+      mult_old = grp_isum<G>(mult_old);
     if (need && !live) {  // every constraint of v left the light table: v stays at 0
       if (g == 0) {
         s.vstate[v] = 1;
@@ -186,6 +213,7 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
         atomicSub(&s.votes[t], mult_old);
       atomicAdd(&s.votes[newt], mult_new);
       s.tgt[v] = newt;
+    }
     }
   }
   if (s.vstat) {
