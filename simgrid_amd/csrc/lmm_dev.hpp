@@ -26,8 +26,8 @@ enum : int {
   CTL_ALIVE_C = 10,  // maxmin: constraints still in the light table
   CTL_NREADY = 11,   // maxmin: ready-list length of the current round
   CTL_NTOUCH0 = 12,  // maxmin: touched-list lengths, per round parity (2 words)
-  CTL_REEVAL = 14,   // maxmin: variables re-evaluated (statistics)
-  CTL_WORDS = 16
+  CTL_NCL0 = 14,     // maxmin: alive-constraint list lengths (2 buffers)
+  CTL_WORDS = 32
 };
 
 struct Dev {
@@ -64,6 +64,7 @@ struct Dev {
   int32_t* chg;     // [nC] last round in which ratio / liveness changed
   int32_t* ready;   // [nC] ready list (constraints that are local minima this round)
   int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
+  int32_t* clist[2];  // [nC] alive-constraint lists (periodically compacted)
   // alive-row buffers: 0 = the original CSR (identity ids), 1/2 = compaction targets
   const int32_t* cvar[3];
   const uint32_t* crow[3];
@@ -140,6 +141,30 @@ __device__ __forceinline__ int wave_append(bool pred, int32_t* counter) {
     base = atomicAdd(counter, __popcll(m));
   base = __shfl(base, leader, kWave);
   return pred ? base + __popcll(m & ((1ull << lane) - 1)) : -1;
+}
+
+// Append `pred` items to a global list with ONE atomic per block (all kBlock threads must call).
+__device__ __forceinline__ int block_append(bool pred, int32_t* counter) {
+  __shared__ int wcnt[kBlock / kWave];
+  __shared__ int bbase;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const unsigned long long m = __ballot(pred);
+  if (lane == 0)
+    wcnt[w] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int i = 0; i < kBlock / kWave; i++) {
+      const int c = wcnt[i];
+      wcnt[i] = tot;
+      tot += c;
+    }
+    bbase = tot ? atomicAdd(counter, tot) : 0;
+  }
+  __syncthreads();
+  const int pos = bbase + wcnt[w] + __popcll(m & ((1ull << lane) - 1));
+  __syncthreads();
+  return pred ? pos : -1;
 }
 
 inline int grid_for(int64_t n, int per_block) {

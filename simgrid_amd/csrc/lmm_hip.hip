@@ -239,6 +239,8 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &d.tgt, nV);
   rc |= dalloc(c, &d.chg, nC);
   rc |= dalloc(c, &d.ready, nC);
+  rc |= dalloc(c, &d.clist[0], nC);
+  rc |= dalloc(c, &d.clist[1], nC);
   rc |= dalloc(c, &d.bsum, 2 * nblk);
   rc |= dalloc(c, &d.ctl, CTL_WORDS);
   if (rc) {
@@ -444,17 +446,19 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int gC = grid_for(d.nC, kBlock);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, mm_init_vars, grid_for(d.nV, kBlock), kBlock, d);
+  LAUNCH(1, -1, mm_clist, gC, kBlock, d, 0, 0, 1);
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
-  int64_t r = 0, last_compact = 0, nrows = d.nV;
-  int buf = 0, chunk = 2;
+  int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
+  int buf = 0, cb = 0, chunk = 2;
   for (;;) {
+    const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
-      LAUNCH(3, r, mm_ready, gC, kBlock, d);
+      LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
       LAUNCH(4, r, mm_saturate, kMaxBlocks, kBlock, d, int(r));
-      LAUNCH(5, r, mm_update, gC, kBlock, d, int(r), prec);
+      LAUNCH(5, r, mm_update, gL, kBlock, d, int(r), prec, cb);
     }
     if (int rc = poll_ctl(c))
       return rc;
@@ -462,6 +466,16 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       break;
     if (r > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
+    if (r - last_clist >= 8 && ncl > 4096) {  // alive-constraint list (order not preserved)
+      const int out = cb ^ 1;
+      HIPCHK(hipMemsetAsync(d.ctl + CTL_NCL0 + out, 0, sizeof(int32_t), c->stream));
+      LAUNCH(6, r, mm_clist, gL, kBlock, d, cb, out, 0);
+      cb = out;
+      last_clist = r;
+      if (int rc = poll_ctl(c))
+        return rc;
+      ncl = c->h_ctl[CTL_NCL0 + cb];
+    }
     if (r - last_compact >= 16 && nrows > 4096) {  // order-preserving compaction of the alive rows
       const int out = buf == 1 ? 2 : 1;
       const int nblk = int((nrows + kCompactRows - 1) / kCompactRows);

@@ -225,17 +225,33 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
   }
 }
 
-// Round phase 2 — ready list: constraints every alive element votes for.
-__global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
+// Alive-constraint list: built at init, re-compacted with the rows (order not preserved).
+__global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int from_all) {
+  const int64_t n = from_all ? s.nC : s.ctl[CTL_NCL0 + in];
+  for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
+    const int64_t i = base + threadIdx.x;
+    int32_t c = -1;
+    if (i < n)
+      c = from_all ? int32_t(i) : s.clist[in][i];
+    const bool alive = c >= 0 && s.key[c] != kDeadKey;
+    const int pos = block_append(alive, &s.ctl[CTL_NCL0 + out]);
+    if (alive)
+      s.clist[out][pos] = c;
+  }
+}
+
+// Round phase 2 — ready list: alive constraints every alive element votes for.
+__global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
   if (s.ctl[CTL_DONE])
     return;
-  const int64_t n = s.nC;
+  const int64_t n = s.ctl[CTL_NCL0 + cb];
   for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
-    const int64_t c = base + threadIdx.x;
-    const bool rdy = c < n && s.key[c] != kDeadKey && s.votes[c] == s.acnt[c];
+    const int64_t i = base + threadIdx.x;
+    const int32_t c = i < n ? s.clist[cb][i] : 0;
+    const bool rdy = i < n && s.key[c] != kDeadKey && s.votes[c] == s.acnt[c];
     const int pos = wave_append(rdy, &s.ctl[CTL_NREADY]);
     if (rdy)
-      s.ready[pos] = int32_t(c);
+      s.ready[pos] = c;
   }
 }
 
@@ -269,13 +285,15 @@ __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round) {
 }
 
 // Round phase 4 — constraint update: maxmin.cpp:603-658.
-__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec, int cb) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_ROUNDS] += 1;
   int died = 0;
-  for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < s.nC; c += int64_t(gridDim.x) * kBlock) {
+  const int64_t n = s.ctl[CTL_NCL0 + cb];
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const int32_t c = s.clist[cb][i];
     if (s.key[c] == kDeadKey)
       continue;
     const int dc = s.dcnt[c];
