@@ -62,7 +62,9 @@ struct Dev {
   int32_t* dcnt;    // [nC] atomic accumulator of fixed elements
   int32_t* votes;   // [nC] persistent: alive elements whose variable votes for this constraint
   int32_t* chg;     // [nC] last round in which ratio / liveness changed
-  int32_t* ready;   // [nC] ready list (constraints that are local minima this round)
+  int32_t* ready;   // [nC + slack] ready constraints, one segment per mm_ready block
+  int32_t* bready;  // [kMaxBlocks] ready count of each segment
+  int32_t* balive;  // [kMaxBlocks] constraints still alive after mm_update, per block
   int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
   int32_t* clist[2];  // [nC] alive-constraint lists (periodically compacted)
   // alive-row buffers: 0 = the original CSR (identity ids), 1/2 = compaction targets

@@ -238,7 +238,9 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &d.vstate, nV);
   rc |= dalloc(c, &d.tgt, nV);
   rc |= dalloc(c, &d.chg, nC);
-  rc |= dalloc(c, &d.ready, nC);
+  rc |= dalloc(c, &d.ready, nC + kMaxBlocks);
+  rc |= dalloc(c, &d.bready, kMaxBlocks);
+  rc |= dalloc(c, &d.balive, kMaxBlocks);
   rc |= dalloc(c, &d.clist[0], nC);
   rc |= dalloc(c, &d.clist[1], nC);
   rc |= dalloc(c, &d.bsum, 2 * nblk);
@@ -457,9 +459,10 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
-      LAUNCH(4, r, mm_saturate, kMaxBlocks, kBlock, d, int(r));
+      LAUNCH(4, r, mm_saturate, grid_for(gL, kBlock / kWave), kBlock, d, int(r), cb, gL);
       LAUNCH(5, r, mm_update, gL, kBlock, d, int(r), prec, cb);
     }
+    LAUNCH(6, r, mm_done, 1, kBlock, d, gL);
     if (int rc = poll_ctl(c))
       return rc;
     if (c->h_ctl[CTL_DONE])

@@ -91,14 +91,8 @@ __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double 
 // Round phase 1 — (re-)vote.  G lanes per alive row; loops are wave-uniform so the group shuffles
 // always see their whole group.
 template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int buf, int round) {
-  if (s.ctl[CTL_DONE])
+  if (s.ctl[CTL_DONE])  // light table empty (maxmin.cpp:680), detected by mm_done
     return;
-  if (s.ctl[CTL_ALIVE_C] <= 0) {  // light table empty: maxmin.cpp:680
-    s.ctl[CTL_DONE] = 1;
-    return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_NREADY] = 0;
   __shared__ int st_rows, st_elems;  // profiling counters (LDS, one store per block)
   if (s.vstat && threadIdx.x == 0)
     st_rows = st_elems = 0;
@@ -240,65 +234,90 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int f
   }
 }
 
-// Round phase 2 — ready list: alive constraints every alive element votes for.
+// Round phase 2 — ready list: alive constraints every alive element votes for.  Block b scans one
+// contiguous chunk of the alive-constraint list and writes its ready constraints into its own segment
+// of `ready` (LDS counter, no global atomic); bready[b] = segment length.
+__device__ __forceinline__ int64_t chunk_of(int64_t n, int nblocks) { return (n + nblocks - 1) / nblocks; }
+
 __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
   if (s.ctl[CTL_DONE])
     return;
+  __shared__ int cnt;
+  if (threadIdx.x == 0)
+    cnt = 0;
+  __syncthreads();
   const int64_t n = s.ctl[CTL_NCL0 + cb];
-  for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
-    const int64_t i = base + threadIdx.x;
-    const int32_t c = i < n ? s.clist[cb][i] : 0;
-    const bool rdy = i < n && s.key[c] != kDeadKey && s.votes[c] == s.acnt[c];
-    const int pos = wave_append(rdy, &s.ctl[CTL_NREADY]);
-    if (rdy)
-      s.ready[pos] = c;
+  const int64_t chunk = chunk_of(n, gridDim.x);
+  const int64_t lo = int64_t(blockIdx.x) * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+    const int32_t c = s.clist[cb][i];
+    if (s.key[c] != kDeadKey && s.votes[c] == s.acnt[c])
+      s.ready[lo + atomicAdd(&cnt, 1)] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s.bready[blockIdx.x] = cnt;
+}
+
+// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.  One wave per constraint;
+// every alive variable on it is claimed once (atomicCAS: duplicates / shared variables), fixed at
+// ratio/penalty and pushes its decrements.  Wave w handles segments w, w + nwaves, ... whole.
+__device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane) {
+  const double r = s.ratio[c];
+  for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave) {
+    const int32_t v = s.csc_v[j];
+    if (s.vstate[v] != 0 || atomicCAS(&s.vstate[v], 0, 1) != 0)
+      continue;
+    const double p = s.pen[v];
+    const double xv = r / p;
+    s.x[v] = xv;
+    s.fixr[v] = round;
+    int mult = 0;
+    for (uint32_t k = s.var_ptr[v]; k < s.var_ptr[v + 1]; k++) {
+      mult += s.csr_c[k] == c;
+      push_decrement(s, k, xv, p);
+    }
+    atomicSub(&s.votes[c], mult);
   }
 }
 
-// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.
-__global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round) {
+__global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, int ready_blocks) {
   if (s.ctl[CTL_DONE])
     return;
-  const int nready = s.ctl[CTL_NREADY];
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  for (int64_t i = wave; i < nready; i += nwaves) {
-    const int32_t c = s.ready[i];
-    const double r = s.ratio[c];
-    for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave) {
-      const int32_t v = s.csc_v[j];
-      if (s.vstate[v] != 0 || atomicCAS(&s.vstate[v], 0, 1) != 0)
-        continue;
-      const double p = s.pen[v];
-      const double xv = r / p;
-      s.x[v] = xv;
-      s.fixr[v] = round;
-      int mult = 0;
-      for (uint32_t k = s.var_ptr[v]; k < s.var_ptr[v + 1]; k++) {
-        mult += s.csr_c[k] == c;
-        push_decrement(s, k, xv, p);
-      }
-      atomicSub(&s.votes[c], mult);
-    }
+  const int64_t chunk = chunk_of(s.ctl[CTL_NCL0 + cb], ready_blocks);
+  for (int64_t seg = wave; seg < ready_blocks; seg += nwaves) {
+    const int nseg = s.bready[seg];
+    for (int i = 0; i < nseg; i++)
+      saturate_one(s, s.ready[seg * chunk + i], round, lane);
   }
 }
 
-// Round phase 4 — constraint update: maxmin.cpp:603-658.
+// Round phase 4 — constraint update: maxmin.cpp:603-658.  balive[block] = constraints of the
+// block's range still in the light table (read by mm_done; plain stores, no global atomic).
 __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec, int cb) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_ROUNDS] += 1;
-  int died = 0;
+  __shared__ int alive_cnt;
+  if (threadIdx.x == 0)
+    alive_cnt = 0;
+  __syncthreads();
+  int alive = 0;
   const int64_t n = s.ctl[CTL_NCL0 + cb];
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
     const int32_t c = s.clist[cb][i];
     if (s.key[c] == kDeadKey)
       continue;
     const int dc = s.dcnt[c];
-    if (!dc)  // untouched: ratio unchanged
+    if (!dc) {  // untouched: ratio unchanged
+      alive++;
       continue;
+    }
     s.dcnt[c] = 0;
     s.acnt[c] -= dc;
     s.chg[c] = round;
@@ -327,19 +346,34 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
     if (!(use > prec) || !(rem > bound * prec)) {
       s.ratio[c] = dinf();
       s.key[c] = kDeadKey;
-      died++;
     } else {
       const double r = rem / use;
       s.ratio[c] = r;
       s.key[c] = ratio_key(r);
+      alive++;
     }
   }
-  // one atomic per wave for the light-table size
-  for (int o = 32; o > 0; o >>= 1)
-    died += __shfl_xor(died, o, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0 && died)
-    atomicSub(&s.ctl[CTL_ALIVE_C], died);
+  if (alive)
+    atomicAdd(&alive_cnt, alive);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s.balive[blockIdx.x] = alive_cnt;
 }
+
+// Termination (maxmin.cpp:680): no constraint left in the light table after the last update.
+__global__ void __launch_bounds__(kBlock) mm_done(Dev s, int update_blocks) {
+  int a = 0;
+  for (int b = threadIdx.x; b < update_blocks; b += kBlock)
+    a += s.balive[b];
+  a = grp_isum<kWave>(a);
+  __shared__ int w[kBlock / kWave];
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    w[threadIdx.x / kWave] = a;
+  __syncthreads();
+  if (threadIdx.x == 0 && w[0] + w[1] + w[2] + w[3] == 0)
+    s.ctl[CTL_DONE] = 1;
+}
+
 
 // ---- order-preserving compaction of the alive rows: count / scan / write ----
 __device__ __forceinline__ void block_scan2(int& a, int& b, int* sh) {  // exclusive, kBlock threads
