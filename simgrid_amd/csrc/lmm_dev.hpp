@@ -27,6 +27,7 @@ enum : int {
   CTL_NREADY = 11,   // maxmin: ready-list length of the current round
   CTL_NTOUCH0 = 12,  // maxmin: touched-list lengths, per round parity (2 words)
   CTL_NCL0 = 14,     // maxmin: alive-constraint list lengths (2 buffers)
+  CTL_LASTR = 16,    // maxmin: last round that fixed a variable (+1 = rounds)
   CTL_WORDS = 32
 };
 

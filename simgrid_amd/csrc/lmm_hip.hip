@@ -362,6 +362,8 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->stats.device_ms = ms;
   c->stats.rounds = c->h_ctl[CTL_ROUNDS];
+  if (kind == LMMHIP_KIND_MAXMIN && c->stats.rounds > 0)  // launched rounds include empty tail rounds
+    c->stats.rounds = c->h_ctl[CTL_LASTR] + 1;
   if (c->profiling)
     return resolve_profile(c);
   return 0;
@@ -440,6 +442,30 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   return 0;
 }
 
+static int launch_saturate(lmmhip_ctx* c, int64_t r, int64_t ncl, int cb, int gL) {
+  const Dev& d = c->d;
+  int64_t g = ncl / kBlock;
+  const int grid = int(g < 1 ? 1 : g > kMaxBlocks ? kMaxBlocks : g);
+  switch (c->group) {
+  case 4:
+    LAUNCH(4, r, mm_saturate<4>, grid, kBlock, d, int(r), cb, gL);
+    break;
+  case 8:
+    LAUNCH(4, r, mm_saturate<8>, grid, kBlock, d, int(r), cb, gL);
+    break;
+  case 16:
+    LAUNCH(4, r, mm_saturate<16>, grid, kBlock, d, int(r), cb, gL);
+    break;
+  case 32:
+    LAUNCH(4, r, mm_saturate<32>, grid, kBlock, d, int(r), cb, gL);
+    break;
+  default:
+    LAUNCH(4, r, mm_saturate<64>, grid, kBlock, d, int(r), cb, gL);
+    break;
+  }
+  return 0;
+}
+
 // Slots: 0 mm_init_cnsts, 1 mm_init_vars, 2 mm_vote, 3 mm_ready, 4 mm_saturate, 5 mm_update,
 // 6 compaction.
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
@@ -459,7 +485,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
-      LAUNCH(4, r, mm_saturate, grid_for(gL, kBlock / kWave), kBlock, d, int(r), cb, gL);
+      if (int rc = launch_saturate(c, r, ncl, cb, gL))
+        return rc;
       LAUNCH(5, r, mm_update, gL, kBlock, d, int(r), prec, cb);
     }
     LAUNCH(6, r, mm_done, 1, kBlock, d, gL);

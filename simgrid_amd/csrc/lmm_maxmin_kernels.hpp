@@ -260,39 +260,102 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
     s.bready[blockIdx.x] = cnt;
 }
 
-// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.  One wave per constraint;
-// every alive variable on it is claimed once (atomicCAS: duplicates / shared variables), fixed at
-// ratio/penalty and pushes its decrements.  Wave w handles segments w, w + nwaves, ... whole.
-__device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane) {
+// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.  One wave per ready
+// constraint; its lanes claim the alive variables on it (atomicCAS: duplicates / variables shared by
+// two ready constraints), fix them at ratio/penalty, then G-lane groups push the decrements of the
+// claimed variables' rows in parallel.
+template <int G> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane) {
   const double r = s.ratio[c];
-  for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave) {
-    const int32_t v = s.csc_v[j];
-    if (s.vstate[v] != 0 || atomicCAS(&s.vstate[v], 0, 1) != 0)
-      continue;
-    const double p = s.pen[v];
-    const double xv = r / p;
-    s.x[v] = xv;
-    s.fixr[v] = round;
-    int mult = 0;
-    for (uint32_t k = s.var_ptr[v]; k < s.var_ptr[v + 1]; k++) {
-      mult += s.csr_c[k] == c;
-      push_decrement(s, k, xv, p);
+  const int g = lane & (G - 1);
+  constexpr int kGpw = kWave / G;
+  const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
+  for (uint32_t base = cb; base < ce; base += kWave) {  // wave-uniform
+    const uint32_t j = base + lane;
+    int32_t lv = -1;
+    if (j < ce) {
+      lv = s.csc_v[j];
+      if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, 1) != 0)
+        lv = -1;
     }
-    atomicSub(&s.votes[c], mult);
+    if (lv >= 0) {
+      s.x[lv] = r / s.pen[lv];
+      s.fixr[lv] = round;
+    }
+    unsigned long long mask = __ballot(lv >= 0);
+    while (mask) {
+      unsigned long long m = mask;
+      for (int i = 0; i < lane / G; i++)
+        m &= m - 1;
+      const int pos = m ? __ffsll((long long)m) - 1 : -1;
+      for (int i = 0; i < kGpw; i++)
+        mask &= mask - 1;
+      const int v = __shfl(lv, pos < 0 ? 0 : pos, kWave);
+      int mult = 0;
+      if (pos >= 0) {
+        const double p = s.pen[v];
+        const double xv = r / p;
+        for (uint32_t k = s.var_ptr[v] + g; k < s.var_ptr[v + 1]; k += G) {
+          mult += s.csr_c[k] == c;
+          push_decrement(s, k, xv, p);
+        }
+      }
+      mult = grp_isum<G>(mult);
+      if (pos >= 0 && g == 0)
+        atomicSub(&s.votes[c], mult);
+    }
   }
 }
 
+template <int G>
 __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, int ready_blocks) {
   if (s.ctl[CTL_DONE])
     return;
+  // exclusive prefix of the per-segment ready counts, in LDS
+  __shared__ int pre[kMaxBlocks + 1];
+  __shared__ int part[kBlock + 1];
+  constexpr int kPer = kMaxBlocks / kBlock;
+  int loc[kPer];
+  int sum = 0;
+  for (int k = 0; k < kPer; k++) {
+    const int seg = threadIdx.x * kPer + k;
+    loc[k] = seg < ready_blocks ? s.bready[seg] : 0;
+    sum += loc[k];
+  }
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < kBlock; i++) {
+      const int t = part[i];
+      part[i] = acc;
+      acc += t;
+    }
+    part[kBlock] = acc;
+  }
+  __syncthreads();
+  int acc = part[threadIdx.x];
+  for (int k = 0; k < kPer; k++) {
+    pre[threadIdx.x * kPer + k] = acc;
+    acc += loc[k];
+  }
+  if (threadIdx.x == 0)
+    pre[kMaxBlocks] = part[kBlock];
+  __syncthreads();
+  const int total = pre[kMaxBlocks];
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
   const int64_t chunk = chunk_of(s.ctl[CTL_NCL0 + cb], ready_blocks);
-  for (int64_t seg = wave; seg < ready_blocks; seg += nwaves) {
-    const int nseg = s.bready[seg];
-    for (int i = 0; i < nseg; i++)
-      saturate_one(s, s.ready[seg * chunk + i], round, lane);
+  for (int64_t i = wave; i < total; i += nwaves) {
+    int lo = 0, hi = ready_blocks;  // last segment with pre[seg] <= i
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) / 2;
+      if (pre[mid] <= i)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    saturate_one<G>(s, s.ready[lo * chunk + (i - pre[lo])], round, lane);
   }
 }
 
@@ -307,7 +370,7 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   if (threadIdx.x == 0)
     alive_cnt = 0;
   __syncthreads();
-  int alive = 0;
+  int alive = 0, any_touch = 0;
   const int64_t n = s.ctl[CTL_NCL0 + cb];
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
     const int32_t c = s.clist[cb][i];
@@ -318,6 +381,7 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
       alive++;
       continue;
     }
+    any_touch = 1;
     s.dcnt[c] = 0;
     s.acnt[c] -= dc;
     s.chg[c] = round;
@@ -358,6 +422,8 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   __syncthreads();
   if (threadIdx.x == 0)
     s.balive[blockIdx.x] = alive_cnt;
+  if (__syncthreads_or(any_touch) && threadIdx.x == 0)
+    s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
 }
 
 // Termination (maxmin.cpp:680): no constraint left in the light table after the last update.
