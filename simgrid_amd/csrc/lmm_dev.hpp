@@ -49,7 +49,6 @@ struct Dev {
   double* x;        // [nV] values (output)
   int32_t* fixr;    // [nV] round in which the variable left the alive set (measurement only)
   int32_t* vstate;  // [nV] maxmin: 0 alive, 1 fixed or dropped (claimed with atomicCAS)
-  int32_t* tgt;     // [nV] maxmin: constraint the variable currently votes for (-1: none)
   double* vtmp;     // [nV] fair bottleneck: mu
   uint8_t* vst;     // [nV] fair bottleneck: 1 listed / 0 not
   // per-constraint state
@@ -62,7 +61,7 @@ struct Dev {
   int32_t* acnt;    // [nC] alive (unfixed) elements
   int32_t* dcnt;    // [nC] atomic accumulator of fixed elements
   int32_t* votes;   // [nC] persistent: alive elements whose variable votes for this constraint
-  int32_t* chg;     // [nC] last round in which ratio / liveness changed
+  uint16_t* chg;    // [nC] last round (mod 2^16) in which ratio / liveness changed
   int32_t* ready;   // [nC + slack] ready constraints, one segment per mm_ready block
   int32_t* bready;  // [kMaxBlocks] ready count of each segment
   int32_t* balive;  // [kMaxBlocks] constraints still alive after mm_update, per block
@@ -72,12 +71,15 @@ struct Dev {
   const int32_t* cvar[3];
   const uint32_t* crow[3];
   const int32_t* ccol[3];
+  int32_t* rtgt[3];  // per row: constraint the variable votes for; kUnvoted / kRetired
   int32_t* bsum;    // compaction scratch: per-block rows / elems (2 x blocks)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };
 
 constexpr int kStatRounds = 4096;  // rounds covered by the profiling counters
+constexpr int32_t kUnvoted = -1;   // row target: not evaluated yet
+constexpr int32_t kRetired = -2;   // row target: variable fixed or dropped (skip until compaction)
 
 __device__ __forceinline__ double dinf() { return __builtin_huge_val(); }
 

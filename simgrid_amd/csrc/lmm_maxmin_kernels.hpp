@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
       s.acnt[c] = int32_t(e - b);
       s.dcnt[c] = 0;
       s.votes[c] = 0;
-      s.chg[c] = -1;
+      s.chg[c] = uint16_t(0xFFFF);
       const bool alive = part && usage > 0;
       const double r = bound / usage;
       s.ratio[c] = alive ? r : dinf();
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
     s.x[v] = 0.0;
     s.fixr[v] = -1;
     s.vstate[v] = 0;
-    s.tgt[v] = -1;
+    s.rtgt[0][v] = kUnvoted;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_NROWS + 0] = s.nV;
@@ -111,13 +111,12 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
   // One lane per row decides whether the row needs work (its target changed last round); the rows
   // that do are then processed kGpw at a time (one G-lane group each), so a wave only pays for the
   // rows that need it.
+  int32_t* __restrict__ rtgt = s.rtgt[buf];
+  const uint16_t prev = uint16_t(round - 1);
   for (int64_t base = wave * kWave; base < nrows; base += nwaves * kWave) {
     const int64_t lrow = base + lane;
-    bool lvalid = lrow < nrows;
-    const int lv = lvalid ? cvar[lrow] : 0;
-    lvalid = lvalid && s.vstate[lv] == 0;
-    const int lt = lvalid ? s.tgt[lv] : -1;
-    const bool lneed = lvalid && (lt < 0 || s.chg[lt] == round - 1);
+    const int lt = lrow < nrows ? rtgt[lrow] : kRetired;  // streamed, row-aligned
+    const bool lneed = lt == kUnvoted || (lt >= 0 && s.chg[lt] == prev);
     unsigned long long mask = __ballot(lneed);
     while (mask) {  // wave-uniform
       unsigned long long m = mask;
@@ -127,10 +126,15 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
       for (int i = 0; i < kGpw; i++)
         mask &= mask - 1;
       const int src = pos < 0 ? 0 : pos;
-      const int v = __shfl(lv, src, kWave);
       const int t = __shfl(lt, src, kWave);
-      const bool need = pos >= 0;
       const int64_t row = base + src;
+      const int v = pos >= 0 ? cvar[row] : 0;
+      bool need = pos >= 0;
+      if (need && s.vstate[v] != 0) {  // fixed by mm_saturate since: retire the row
+        if (g == 0)
+          rtgt[row] = kRetired;
+        need = false;
+      }
       uint32_t b = 0, e = 0;
       if (need) {
         b = crow[row];
@@ -187,27 +191,29 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
       }
       mult_new = grp_isum<G>(mult_new);
       mult_old = grp_isum<G>(mult_old);
-    if (need && !live) {  // every constraint of v left the light table: v stays at 0
-      if (g == 0) {
-        s.vstate[v] = 1;
-        s.fixr[v] = round;
-      }
-    } else if (bounded) {  // fixed at its bound (maxmin.cpp:587-589)
-      if (g == 0) {
-        s.vstate[v] = 1;
-        s.fixr[v] = round;
-        s.x[v] = vb;
+      if (need && !live) {  // every constraint of v left the light table: v stays at 0
+        if (g == 0) {
+          s.vstate[v] = 1;
+          s.fixr[v] = round;
+          rtgt[row] = kRetired;
+        }
+      } else if (bounded) {  // fixed at its bound (maxmin.cpp:587-589)
+        if (g == 0) {
+          s.vstate[v] = 1;
+          s.fixr[v] = round;
+          s.x[v] = vb;
+          rtgt[row] = kRetired;
+          if (t >= 0 && key[t] != kDeadKey)
+            atomicSub(&s.votes[t], mult_old);
+        }
+        for (uint32_t j = s.var_ptr[v] + g; j < s.var_ptr[v + 1]; j += G)
+          push_decrement(s, j, vb, p);
+      } else if (live && newt != t && g == 0) {
         if (t >= 0 && key[t] != kDeadKey)
           atomicSub(&s.votes[t], mult_old);
+        atomicAdd(&s.votes[newt], mult_new);
+        rtgt[row] = newt;
       }
-      for (uint32_t j = s.var_ptr[v] + g; j < s.var_ptr[v + 1]; j += G)
-        push_decrement(s, j, vb, p);
-    } else if (live && newt != t && g == 0) {
-      if (t >= 0 && key[t] != kDeadKey)
-        atomicSub(&s.votes[t], mult_old);
-      atomicAdd(&s.votes[newt], mult_new);
-      s.tgt[v] = newt;
-    }
     }
   }
   if (s.vstat) {
@@ -384,7 +390,7 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
     any_touch = 1;
     s.dcnt[c] = 0;
     s.acnt[c] -= dc;
-    s.chg[c] = round;
+    s.chg[c] = uint16_t(round);
     const double bound = s.cbound[c];
     double rem = s.rem[c], use;
     if (!(s.cflags[c] & 1)) {
@@ -541,6 +547,7 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
     if (row < nrows && row_alive(s, in, row)) {
       const uint32_t b = s.crow[in][row], e = s.crow[in][row + 1];
       ovar[pr] = s.cvar[in][row];
+      s.rtgt[out][pr] = s.rtgt[in][row];
       orow[pr] = uint32_t(pe);
       for (uint32_t j = b; j < e; j++)
         ocol[pe++] = s.ccol[in][j];
