@@ -425,10 +425,8 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   const int grid = grid_for(nrows, kBlock);  // one lane per row in the work-queue scan
   switch (G) {
   case 4:
-    LAUNCH(2, r, mm_vote<4>, grid, kBlock, d, buf, int(r));
-    break;
-  case 8:
-    LAUNCH(2, r, mm_vote<8>, grid, kBlock, d, buf, int(r));
+  case 8:  // short rows: one lane per row (more gathers in flight per wave)
+    LAUNCH(2, r, mm_vote_lane, grid, kBlock, d, buf, int(r));
     break;
   case 16:
     LAUNCH(2, r, mm_vote<16>, grid, kBlock, d, buf, int(r));

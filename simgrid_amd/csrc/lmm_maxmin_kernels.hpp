@@ -240,6 +240,128 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int f
   }
 }
 
+// Lane-per-row variant of mm_vote for short rows (mean length <= 8): every lane resolves its own
+// row with up to kReg independent gathers in flight, 8x the memory-level parallelism of a G=8 group.
+constexpr int kReg = 8;
+
+__global__ void __launch_bounds__(kBlock) mm_vote_lane(Dev s, int buf, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ int st_rows, st_elems;
+  if (s.vstat && threadIdx.x == 0)
+    st_rows = st_elems = 0;
+  if (s.vstat)
+    __syncthreads();
+  const int64_t nrows = s.ctl[CTL_NROWS + buf];
+  const int32_t* __restrict__ cvar = s.cvar[buf];
+  const uint32_t* __restrict__ crow = s.crow[buf];
+  const int32_t* __restrict__ ccol = s.ccol[buf];
+  int32_t* __restrict__ rtgt = s.rtgt[buf];
+  const uint16_t* __restrict__ key = s.key;
+  const uint16_t prev = uint16_t(round - 1);
+  for (int64_t row = int64_t(blockIdx.x) * kBlock + threadIdx.x; row < nrows; row += int64_t(gridDim.x) * kBlock) {
+    const int t = rtgt[row];
+    if (!(t == kUnvoted || (t >= 0 && s.chg[t] == prev)))
+      continue;
+    const int v = cvar[row];
+    if (s.vstate[v] != 0) {  // fixed by mm_saturate since: retire the row
+      rtgt[row] = kRetired;
+      continue;
+    }
+    const uint32_t b = crow[row], e = crow[row + 1];
+    if (s.vstat) {
+      atomicAdd(&st_rows, 1);
+      atomicAdd(&st_elems, int(e - b));
+    }
+    int32_t cc[kReg];
+    unsigned kk[kReg];
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      cc[i] = b + i < e ? ccol[b + i] : -1;
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      kk[i] = cc[i] >= 0 ? key[cc[i]] : kDeadKey;
+    unsigned mk = kDeadKey;
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      mk = min(mk, kk[i]);
+    for (uint32_t j = b + kReg; j < e; j++)
+      mk = min(mk, (unsigned)key[ccol[j]]);
+    int nmin = 0;
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      nmin += kk[i] == mk;
+    for (uint32_t j = b + kReg; j < e; j++)
+      nmin += key[ccol[j]] == mk;
+    const double vb = s.vbound[v];
+    if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
+      s.vstate[v] = 1;
+      s.fixr[v] = round;
+      rtgt[row] = kRetired;
+      continue;
+    }
+    double minr = dinf();
+    if (nmin > 1 || vb > 0) {
+#pragma unroll
+      for (int i = 0; i < kReg; i++)
+        if (kk[i] == mk)
+          minr = fmin(minr, s.ratio[cc[i]]);
+      for (uint32_t j = b + kReg; j < e; j++) {
+        const int32_t c = ccol[j];
+        if (key[c] == mk)
+          minr = fmin(minr, s.ratio[c]);
+      }
+    }
+    int mult_old = 0;
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      mult_old += cc[i] == t;
+    for (uint32_t j = b + kReg; j < e; j++)
+      mult_old += ccol[j] == t;
+    const double p = s.pen[v];
+    if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
+      s.vstate[v] = 1;
+      s.fixr[v] = round;
+      s.x[v] = vb;
+      rtgt[row] = kRetired;
+      if (t >= 0 && key[t] != kDeadKey)
+        atomicSub(&s.votes[t], mult_old);
+      for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
+        push_decrement(s, j, vb, p);
+      continue;
+    }
+    int newt = INT_MAX;
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      if (kk[i] == mk && (nmin == 1 || s.ratio[cc[i]] == minr))
+        newt = min(newt, cc[i]);
+    for (uint32_t j = b + kReg; j < e; j++) {
+      const int32_t c = ccol[j];
+      if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
+        newt = min(newt, c);
+    }
+    if (newt == t)
+      continue;
+    int mult_new = 0;
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      mult_new += cc[i] == newt;
+    for (uint32_t j = b + kReg; j < e; j++)
+      mult_new += ccol[j] == newt;
+    if (t >= 0 && key[t] != kDeadKey)
+      atomicSub(&s.votes[t], mult_old);
+    atomicAdd(&s.votes[newt], mult_new);
+    rtgt[row] = newt;
+  }
+  if (s.vstat) {
+    __syncthreads();
+    if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
+      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x)] = st_rows;
+      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x) + 1] = st_elems;
+    }
+  }
+}
+
 // Round phase 2 — ready list: alive constraints every alive element votes for.  Block b scans one
 // contiguous chunk of the alive-constraint list and writes its ready constraints into its own segment
 // of `ready` (LDS counter, no global atomic); bready[b] = segment length.
