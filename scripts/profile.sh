@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py (run on the GPU box via gpurun).  Counter passes are separate from
+# the kernel-trace pass, as MI355X_MICROARCH.md prescribes (FETCH_SIZE and WRITE_SIZE do not fit in
+# one pass).  Output: gpurun_out/rp_*/ (CSV).  usage: scripts/profile.sh [bench args...]
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline $*"
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace -o run \
+  -- python3 $BENCH > gpurun_out/rp_trace.log 2>&1
+rc=$?; echo "trace rc=$rc" >> gpurun_out/rp_trace.log; if fatal $rc; then exit $rc; fi
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_$ctr -o run \
+    -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > gpurun_out/rp_$ctr.log 2>&1
+  rc=$?; echo "$ctr rc=$rc" >> gpurun_out/rp_$ctr.log; if fatal $rc; then exit $rc; fi
+  # calibration on known byte counts (scripts/ubench_gather.hip: 320 MB int32 stream, gathers)
+  timeout -k 10 200 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_cal_$ctr -o run \
+    -- ./scripts/ubench_gather > gpurun_out/rp_cal_$ctr.log 2>&1
+  rc=$?; echo "cal $ctr rc=$rc" >> gpurun_out/rp_cal_$ctr.log; if fatal $rc; then exit $rc; fi
+done
+exit 0
