@@ -26,6 +26,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_ready", 4: "mm_saturate",
               5: "mm_update", 6: "compaction"}
+# rocprofv3 kernel names (profiles/*_traffic.json keys) behind each launch slot
+SLOT_KERNELS = {"mm_vote": ("mm_vote_lane", "mm_vote"), "mm_saturate": ("mm_saturate",),
+                "mm_update": ("mm_update",), "mm_ready": ("mm_ready",), "compaction": ("cmp_write",),
+                "mm_init_cnsts": ("mm_init_cnsts",), "mm_init_vars": ("mm_init_vars",)}
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
 
 
 def log(*a):
@@ -63,7 +68,7 @@ def main():
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-div", type=int, default=10, help="CPU baseline sample = 1/div of the workload")
-    ap.add_argument("--traffic-json", default=None, help="per-kernel HBM bytes from a rocprofv3 --pmc pass")
+    ap.add_argument("--traffic-json", default=TRAFFIC_JSON, help="per-kernel HBM bytes from a rocprofv3 --pmc pass")
     ap.add_argument("--profile-json", default=None, help="write the per-launch profile here")
     args = ap.parse_args()
 
@@ -146,8 +151,10 @@ def main():
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if dom in tj:
-            traffic = tj[dom].get("hbm_bytes_per_launch")
+        for kname in SLOT_KERNELS.get(dom, ()):
+            if kname in tj.get("kernels", {}):
+                traffic = tj["kernels"][kname]["hbm_bytes_per_launch"]
+                break
     solve_alg = 56 * nnz + 24 * nV + 32 * nC
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
