@@ -41,9 +41,10 @@ def kernel_bytes(slot, nV, nC, av, ae, fv, fe, rv, re_):
     """Algorithmic bytes one launch must move: `av`/`ae` alive variables / elements at
     the start of the round, `fv`/`fe` variables / elements fixed in it, `rv`/`re_` variables /
     elements re-evaluated by the vote phase."""
-    if slot == 2:  # mm_vote: per alive row cvar 4 + vstate 4 + tgt 4 + chg 4;
-        #            per re-evaluated row crow 8 + vbound 8 + pen 8 + tgt 4; per element ccol 4 + key 2
-        return av * 16 + rv * 28 + re_ * 6
+    if slot == 2:  # mm_vote: per alive row rtgt 4 + skey 2 + chg[t] 2;
+        #            per re-evaluated row cvar 4 + vstate 4 + crow 8 + vbound 8 + pen 8 + rtgt/skey 6;
+        #            per re-evaluated element ccol 4 + key 2
+        return av * 8 + rv * 38 + re_ * 6
     if slot == 3:  # mm_ready: key 2 + votes 4 + acnt 4 per constraint
         return nC * 10
     if slot == 4:  # mm_saturate: per fixed var csc idx 4 + vstate 4 + pen 8 + x 8 + row ptr 8;

@@ -72,6 +72,7 @@ struct Dev {
   const uint32_t* crow[3];
   const int32_t* ccol[3];
   int32_t* rtgt[3];  // per row: constraint the variable votes for; kUnvoted / kRetired
+  uint16_t* skey[3];  // per row: min key over the row's OTHER constraints at its last vote (0 if bounded)
   int32_t* bsum;    // compaction scratch: per-block rows / elems (2 x blocks)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements

@@ -236,8 +236,10 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &ccol1, nnz);
   rc |= dalloc(c, &ccol2, nnz);
   rc |= dalloc(c, &d.vstate, nV);
-  for (int b = 0; b < 3; b++)
+  for (int b = 0; b < 3; b++) {
     rc |= dalloc(c, &d.rtgt[b], nV);
+    rc |= dalloc(c, &d.skey[b], nV);
+  }
   rc |= dalloc(c, &d.chg, nC);
   rc |= dalloc(c, &d.ready, nC + kMaxBlocks);
   rc |= dalloc(c, &d.bready, kMaxBlocks);

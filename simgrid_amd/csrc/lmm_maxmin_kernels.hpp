@@ -116,7 +116,9 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
   for (int64_t base = wave * kWave; base < nrows; base += nwaves * kWave) {
     const int64_t lrow = base + lane;
     const int lt = lrow < nrows ? rtgt[lrow] : kRetired;  // streamed, row-aligned
-    const bool lneed = lt == kUnvoted || (lt >= 0 && s.chg[lt] == prev);
+    // re-vote when the target changed last round, unless it is still strictly below every other
+    // constraint of the row (their keys only grow): then the vote stands (skey)
+    const bool lneed = lt == kUnvoted || (lt >= 0 && s.chg[lt] == prev && !(key[lt] < s.skey[buf][lrow]));
     unsigned long long mask = __ballot(lneed);
     while (mask) {  // wave-uniform
       unsigned long long m = mask;
@@ -183,6 +185,15 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
         }
       }
       newt = grp_imin<G>(newt);
+      unsigned sk = h0 && c0 != newt ? k0 : kDeadKey;  // min key over the other constraints
+      for (uint32_t j = j0 + G; j < e; j += G) {
+        const int32_t c = ccol[j];
+        if (c != newt)
+          sk = min(sk, (unsigned)key[c]);
+      }
+      sk = grp_umin<G>(sk);
+      if (live && !bounded && g == 0)
+        s.skey[buf][row] = vb > 0 ? 0 : uint16_t(sk);
       int mult_new = h0 && c0 == newt, mult_old = h0 && c0 == t;
       for (uint32_t j = j0 + G; j < e; j += G) {
         const int32_t c = ccol[j];
@@ -240,119 +251,184 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int f
   }
 }
 
-// Lane-per-row variant of mm_vote for short rows (mean length <= 8): every lane resolves its own
-// row with up to kReg independent gathers in flight, 8x the memory-level parallelism of a G=8 group.
+// Lane-per-row variant of mm_vote for short rows (mean length <= 8).  The filter pass streams the
+// row targets (one lane per row, kFilt rows in flight per lane) and queues the rows that need a
+// re-vote in LDS; each full queue of kBlock rows is then resolved one lane per row, with up to kReg
+// independent gathers in flight, so the rare slow rows no longer stall whole waves of fast ones.
 constexpr int kReg = 8;
+constexpr int kFilt = 4;
+
+__device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
+                                         int* st_elems) {
+  const int32_t* __restrict__ cvar = s.cvar[buf];
+  const uint32_t* __restrict__ crow = s.crow[buf];
+  const int32_t* __restrict__ ccol = s.ccol[buf];
+  int32_t* __restrict__ rtgt = s.rtgt[buf];
+  uint16_t* __restrict__ skey = s.skey[buf];
+  const uint16_t* __restrict__ key = s.key;
+  const int t = rtgt[row];
+  const int v = cvar[row];
+  if (s.vstate[v] != 0) {  // fixed by mm_saturate since: retire the row
+    rtgt[row] = kRetired;
+    return;
+  }
+  const uint32_t b = crow[row], e = crow[row + 1];
+  if (s.vstat) {
+    atomicAdd(st_rows, 1);
+    atomicAdd(st_elems, int(e - b));
+  }
+  int32_t cc[kReg];
+  unsigned kk[kReg];
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    cc[i] = b + i < e ? ccol[b + i] : -1;
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    kk[i] = cc[i] >= 0 ? key[cc[i]] : kDeadKey;
+  unsigned mk = kDeadKey;
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    mk = min(mk, kk[i]);
+  for (uint32_t j = b + kReg; j < e; j++)
+    mk = min(mk, (unsigned)key[ccol[j]]);
+  int nmin = 0;
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    nmin += kk[i] == mk;
+  for (uint32_t j = b + kReg; j < e; j++)
+    nmin += key[ccol[j]] == mk;
+  const double vb = s.vbound[v];
+  if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
+    s.vstate[v] = 1;
+    s.fixr[v] = round;
+    rtgt[row] = kRetired;
+    return;
+  }
+  double minr = dinf();
+  if (nmin > 1 || vb > 0) {
+#pragma unroll
+    for (int i = 0; i < kReg; i++)
+      if (kk[i] == mk)
+        minr = fmin(minr, s.ratio[cc[i]]);
+    for (uint32_t j = b + kReg; j < e; j++) {
+      const int32_t c = ccol[j];
+      if (key[c] == mk)
+        minr = fmin(minr, s.ratio[c]);
+    }
+  }
+  int mult_old = 0;
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    mult_old += cc[i] == t;
+  for (uint32_t j = b + kReg; j < e; j++)
+    mult_old += ccol[j] == t;
+  const double p = s.pen[v];
+  if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
+    s.vstate[v] = 1;
+    s.fixr[v] = round;
+    s.x[v] = vb;
+    rtgt[row] = kRetired;
+    if (t >= 0 && key[t] != kDeadKey)
+      atomicSub(&s.votes[t], mult_old);
+    for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
+      push_decrement(s, j, vb, p);
+    return;
+  }
+  int newt = INT_MAX;
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    if (kk[i] == mk && (nmin == 1 || s.ratio[cc[i]] == minr))
+      newt = min(newt, cc[i]);
+  for (uint32_t j = b + kReg; j < e; j++) {
+    const int32_t c = ccol[j];
+    if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
+      newt = min(newt, c);
+  }
+  unsigned sk = kDeadKey;  // min key over the other constraints of the row
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    if (cc[i] != newt)
+      sk = min(sk, kk[i]);
+  for (uint32_t j = b + kReg; j < e; j++) {
+    const int32_t c = ccol[j];
+    if (c != newt)
+      sk = min(sk, (unsigned)key[c]);
+  }
+  skey[row] = vb > 0 ? 0 : uint16_t(sk);
+  if (newt == t)
+    return;
+  int mult_new = 0;
+#pragma unroll
+  for (int i = 0; i < kReg; i++)
+    mult_new += cc[i] == newt;
+  for (uint32_t j = b + kReg; j < e; j++)
+    mult_new += ccol[j] == newt;
+  if (t >= 0 && key[t] != kDeadKey)
+    atomicSub(&s.votes[t], mult_old);
+  atomicAdd(&s.votes[newt], mult_new);
+  rtgt[row] = newt;
+}
 
 __global__ void __launch_bounds__(kBlock) mm_vote_lane(Dev s, int buf, int round) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ int st_rows, st_elems;
-  if (s.vstat && threadIdx.x == 0)
-    st_rows = st_elems = 0;
-  if (s.vstat)
-    __syncthreads();
+  __shared__ int q[kBlock * (kFilt + 1)];  // queued rows (relative to the block's chunk base)
+  __shared__ int qn;
+  if (threadIdx.x == 0)
+    st_rows = st_elems = qn = 0;
+  __syncthreads();
   const int64_t nrows = s.ctl[CTL_NROWS + buf];
-  const int32_t* __restrict__ cvar = s.cvar[buf];
-  const uint32_t* __restrict__ crow = s.crow[buf];
-  const int32_t* __restrict__ ccol = s.ccol[buf];
-  int32_t* __restrict__ rtgt = s.rtgt[buf];
+  const int32_t* __restrict__ rtgt = s.rtgt[buf];
+  const uint16_t* __restrict__ skey = s.skey[buf];
   const uint16_t* __restrict__ key = s.key;
   const uint16_t prev = uint16_t(round - 1);
-  for (int64_t row = int64_t(blockIdx.x) * kBlock + threadIdx.x; row < nrows; row += int64_t(gridDim.x) * kBlock) {
-    const int t = rtgt[row];
-    if (!(t == kUnvoted || (t >= 0 && s.chg[t] == prev)))
-      continue;
-    const int v = cvar[row];
-    if (s.vstate[v] != 0) {  // fixed by mm_saturate since: retire the row
-      rtgt[row] = kRetired;
-      continue;
+  // contiguous chunk per block so queued rows fit in 32-bit offsets from the chunk base
+  constexpr int kStep = kBlock * kFilt;
+  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kStep - 1) / kStep * kStep;
+  const int64_t lo = int64_t(blockIdx.x) * per;
+  const int64_t hi = lo + per < nrows ? lo + per : nrows;
+  for (int64_t base = lo; base < hi; base += kStep) {  // block-uniform
+    int tt[kFilt];
+#pragma unroll
+    for (int u = 0; u < kFilt; u++) {
+      const int64_t row = base + u * kBlock + threadIdx.x;
+      tt[u] = row < hi ? rtgt[row] : kRetired;
     }
-    const uint32_t b = crow[row], e = crow[row + 1];
-    if (s.vstat) {
-      atomicAdd(&st_rows, 1);
-      atomicAdd(&st_elems, int(e - b));
+    unsigned ch[kFilt];
+#pragma unroll
+    for (int u = 0; u < kFilt; u++)
+      ch[u] = tt[u] >= 0 ? s.chg[tt[u]] : 0u;
+#pragma unroll
+    for (int u = 0; u < kFilt; u++) {
+      const int64_t row = base + u * kBlock + threadIdx.x;
+      bool need = tt[u] == kUnvoted;
+      if (tt[u] >= 0 && ch[u] == prev)  // target changed last round: does the vote still stand?
+        need = !(key[tt[u]] < skey[row]);
+      const unsigned long long m = __ballot(need);  // one LDS atomic per wave
+      const int lane = threadIdx.x & (kWave - 1);
+      const int leader = m ? __ffsll((long long)m) - 1 : 0;
+      int at = 0;
+      if (m && lane == leader)
+        at = atomicAdd(&qn, __popcll(m));
+      at = __shfl(at, leader, kWave);
+      if (need)
+        q[at + __popcll(m & ((1ull << lane) - 1))] = int(row - lo);
     }
-    int32_t cc[kReg];
-    unsigned kk[kReg];
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      cc[i] = b + i < e ? ccol[b + i] : -1;
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      kk[i] = cc[i] >= 0 ? key[cc[i]] : kDeadKey;
-    unsigned mk = kDeadKey;
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      mk = min(mk, kk[i]);
-    for (uint32_t j = b + kReg; j < e; j++)
-      mk = min(mk, (unsigned)key[ccol[j]]);
-    int nmin = 0;
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      nmin += kk[i] == mk;
-    for (uint32_t j = b + kReg; j < e; j++)
-      nmin += key[ccol[j]] == mk;
-    const double vb = s.vbound[v];
-    if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
-      s.vstate[v] = 1;
-      s.fixr[v] = round;
-      rtgt[row] = kRetired;
-      continue;
+    __syncthreads();
+    int n = qn;
+    while (n >= kBlock) {  // resolve full queues: the last kBlock entries each time
+      vote_row(s, buf, round, lo + q[n - kBlock + threadIdx.x], &st_rows, &st_elems);
+      n -= kBlock;
     }
-    double minr = dinf();
-    if (nmin > 1 || vb > 0) {
-#pragma unroll
-      for (int i = 0; i < kReg; i++)
-        if (kk[i] == mk)
-          minr = fmin(minr, s.ratio[cc[i]]);
-      for (uint32_t j = b + kReg; j < e; j++) {
-        const int32_t c = ccol[j];
-        if (key[c] == mk)
-          minr = fmin(minr, s.ratio[c]);
-      }
-    }
-    int mult_old = 0;
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      mult_old += cc[i] == t;
-    for (uint32_t j = b + kReg; j < e; j++)
-      mult_old += ccol[j] == t;
-    const double p = s.pen[v];
-    if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
-      s.vstate[v] = 1;
-      s.fixr[v] = round;
-      s.x[v] = vb;
-      rtgt[row] = kRetired;
-      if (t >= 0 && key[t] != kDeadKey)
-        atomicSub(&s.votes[t], mult_old);
-      for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
-        push_decrement(s, j, vb, p);
-      continue;
-    }
-    int newt = INT_MAX;
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      if (kk[i] == mk && (nmin == 1 || s.ratio[cc[i]] == minr))
-        newt = min(newt, cc[i]);
-    for (uint32_t j = b + kReg; j < e; j++) {
-      const int32_t c = ccol[j];
-      if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
-        newt = min(newt, c);
-    }
-    if (newt == t)
-      continue;
-    int mult_new = 0;
-#pragma unroll
-    for (int i = 0; i < kReg; i++)
-      mult_new += cc[i] == newt;
-    for (uint32_t j = b + kReg; j < e; j++)
-      mult_new += ccol[j] == newt;
-    if (t >= 0 && key[t] != kDeadKey)
-      atomicSub(&s.votes[t], mult_old);
-    atomicAdd(&s.votes[newt], mult_new);
-    rtgt[row] = newt;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      qn = n;
+    __syncthreads();
   }
+  const int n = qn;
+  if (threadIdx.x < n)
+    vote_row(s, buf, round, lo + q[threadIdx.x], &st_rows, &st_elems);
   if (s.vstat) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
@@ -645,36 +721,75 @@ __global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int out) {
   }
 }
 
-__global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
-  __shared__ int sh[2 * kBlock];
-  const int64_t nrows = s.ctl[CTL_NROWS + in];
-  const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
-  int nr = 0, ne = 0;
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t row = r0 + k;
-    if (row < nrows && row_alive(s, in, row)) {
-      nr++;
-      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
+// Exclusive block scan of two counters (wave shuffles + one LDS exchange); ta/tb = block totals.
+__device__ __forceinline__ void block_scan_pair(int& a, int& b, int& ta, int& tb) {
+  __shared__ int wa[kBlock / kWave], wb[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int ia = a, ib = b;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int xa = __shfl_up(ia, o, kWave), xb = __shfl_up(ib, o, kWave);
+    if (lane >= o) {
+      ia += xa;
+      ib += xb;
     }
   }
-  int pr = nr, pe = ne;
-  block_scan2(pr, pe, sh);
-  pr += s.bsum[2 * blockIdx.x];
-  pe += s.bsum[2 * blockIdx.x + 1];
+  if (lane == kWave - 1) {
+    wa[w] = ia;
+    wb[w] = ib;
+  }
+  __syncthreads();
+  int oa = 0, ob = 0;
+  ta = tb = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / kWave; i++) {
+    oa += i < w ? wa[i] : 0;
+    ob += i < w ? wb[i] : 0;
+    ta += wa[i];
+    tb += wb[i];
+  }
+  __syncthreads();
+  a = oa + ia - a;
+  b = ob + ib - b;
+}
+
+// Rows of a block are visited k-major (row = base + k * kBlock + thread) so that neighbouring lanes
+// read and write neighbouring rows; the output keeps the input order.
+__global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
+  const int64_t nrows = s.ctl[CTL_NROWS + in];
+  const int64_t base = int64_t(blockIdx.x) * kCompactRows;
+  int pr = s.bsum[2 * blockIdx.x], pe = s.bsum[2 * blockIdx.x + 1];
+  const int32_t* __restrict__ icol = s.ccol[in];
   int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
   uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
-  int32_t* ocol = const_cast<int32_t*>(s.ccol[out]);
+  int32_t* __restrict__ ocol = const_cast<int32_t*>(s.ccol[out]);
   for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t row = r0 + k;
-    if (row < nrows && row_alive(s, in, row)) {
-      const uint32_t b = s.crow[in][row], e = s.crow[in][row + 1];
-      ovar[pr] = s.cvar[in][row];
-      s.rtgt[out][pr] = s.rtgt[in][row];
-      orow[pr] = uint32_t(pe);
-      for (uint32_t j = b; j < e; j++)
-        ocol[pe++] = s.ccol[in][j];
-      pr++;
+    const int64_t row = base + int64_t(k) * kBlock + threadIdx.x;
+    int32_t v = -1;
+    uint32_t b = 0, e = 0;
+    if (row < nrows) {
+      v = s.cvar[in][row];
+      if (s.vstate[v] == 0) {
+        b = s.crow[in][row];
+        e = s.crow[in][row + 1];
+      } else {
+        v = -1;
+      }
     }
+    int xr = v >= 0, xe = int(e - b), tr, te;
+    block_scan_pair(xr, xe, tr, te);
+    if (v >= 0) {
+      const int o = pr + xr;
+      ovar[o] = v;
+      s.rtgt[out][o] = s.rtgt[in][row];
+      s.skey[out][o] = s.skey[in][row];
+      orow[o] = uint32_t(pe + xe);
+      int32_t* dst = ocol + pe + xe;
+      for (uint32_t j = b; j < e; j++)
+        *dst++ = icol[j];
+    }
+    pr += tr;
+    pe += te;
   }
 }
 
