@@ -56,10 +56,12 @@ struct Dev {
   uint16_t* key;    // [nC] round-down 16-bit key of ratio, kDeadKey when out
   double* rem;      // [nC]
   double* use;      // [nC]
-  double* drem;     // [nC] atomic accumulators (SHARED constraints)
-  double* duse;     // [nC]
+  // [4*nC] per-constraint decrement record {remaining, usage, fixed elements, unused}: 32 B per
+  // constraint so the three pushes of one element, issued by the 4 lanes of a quad in ONE wave
+  // instruction, are one memory-side atomic request (scripts/ubench_atomic.hip: 2.9x the rate of
+  // three separate arrays)
+  double* crec;
   int32_t* acnt;    // [nC] alive (unfixed) elements
-  int32_t* dcnt;    // [nC] atomic accumulator of fixed elements
   int32_t* votes;   // [nC] persistent: alive elements whose variable votes for this constraint
   uint16_t* chg;    // [nC] last round (mod 2^16) in which ratio / liveness changed
   int32_t* ready;   // [nC + slack] ready constraints, one segment per mm_ready block

@@ -223,10 +223,8 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &d.key, nC);
   rc |= dalloc(c, &d.rem, nC);
   rc |= dalloc(c, &d.use, nC);
-  rc |= dalloc(c, &d.drem, nC);
-  rc |= dalloc(c, &d.duse, nC);
+  rc |= dalloc(c, &d.crec, 4 * nC);
   rc |= dalloc(c, &d.acnt, nC);
-  rc |= dalloc(c, &d.dcnt, nC);
   rc |= dalloc(c, &d.votes, nC);
   rc |= dalloc(c, &cvar0, nV);
   rc |= dalloc(c, &cvar1, nV);

@@ -45,10 +45,8 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
       const double usage = part ? acc : 0.0;
       s.rem[c] = bound;
       s.use[c] = usage;
-      s.drem[c] = 0.0;
-      s.duse[c] = 0.0;
+      reinterpret_cast<double4*>(s.crec)[c] = make_double4(0.0, 0.0, 0.0, 0.0);
       s.acnt[c] = int32_t(e - b);
-      s.dcnt[c] = 0;
       s.votes[c] = 0;
       s.chg[c] = uint16_t(0xFFFF);
       const bool alive = part && usage > 0;
@@ -75,16 +73,18 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
   }
 }
 
-// Decrements of a fixed variable's element j (maxmin.cpp:601-606); FATPIPE constraints only count.
+// Decrements of a fixed variable's element j (maxmin.cpp:601-606) into the constraint's record;
+// FATPIPE constraints only count.  One lane issues all three (rare paths).
 __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double xv, double p) {
   const int32_t c = s.csr_c[j];
   if (s.key[c] == kDeadKey)
     return;
-  atomicAdd(&s.dcnt[c], 1);
+  double* r = s.crec + 4 * int64_t(c);
+  unsafeAtomicAdd(&r[2], 1.0);
   if (!(s.cflags[c] & 1)) {
     const double w = s.csr_w[j];
-    unsafeAtomicAdd(&s.drem[c], w * xv);
-    unsafeAtomicAdd(&s.duse[c], w / p);
+    unsafeAtomicAdd(&r[0], w * xv);
+    unsafeAtomicAdd(&r[1], w / p);
   }
 }
 
@@ -468,10 +468,17 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
 // constraint; its lanes claim the alive variables on it (atomicCAS: duplicates / variables shared by
 // two ready constraints), fix them at ratio/penalty, then G-lane groups push the decrements of the
 // claimed variables' rows in parallel.
-template <int G> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane) {
+// One wave per ready constraint c.  Per 64-element chunk of c's CSC segment: lanes claim the alive
+// variables (atomicCAS: a duplicate element claims once), fix them at ratio/penalty; then the
+// claimed variables' CSR elements are flattened over the wave (wave prefix of the row lengths, owner
+// found by binary search in LDS), one lane per element loads it, and the element's three pushes are
+// issued by a quad of lanes into the constraint's 32-B record (4 wave instructions per 64 elements,
+// each ONE atomic request per element; scripts/ubench_atomic.hip).  Decrements to c itself are
+// skipped: c leaves the light table (every alive variable on it is fixed, usage -> 0,
+// maxmin.cpp:608-615).
+__device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane, int* pre) {
   const double r = s.ratio[c];
-  const int g = lane & (G - 1);
-  constexpr int kGpw = kWave / G;
+  const int q = lane & 3;
   const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
   for (uint32_t base = cb; base < ce; base += kWave) {  // wave-uniform
     const uint32_t j = base + lane;
@@ -481,32 +488,75 @@ template <int G> __device__ __forceinline__ void saturate_one(const Dev& s, int3
       if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, 1) != 0)
         lv = -1;
     }
+    double lp = 1.0, lx = 0.0;
+    uint32_t rb = 0;
+    int len = 0;
     if (lv >= 0) {
-      s.x[lv] = r / s.pen[lv];
+      lp = s.pen[lv];
+      lx = r / lp;
+      s.x[lv] = lx;
       s.fixr[lv] = round;
+      rb = s.var_ptr[lv];
+      len = int(s.var_ptr[lv + 1] - rb);
     }
-    unsigned long long mask = __ballot(lv >= 0);
-    while (mask) {
-      unsigned long long m = mask;
-      for (int i = 0; i < lane / G; i++)
-        m &= m - 1;
-      const int pos = m ? __ffsll((long long)m) - 1 : -1;
-      for (int i = 0; i < kGpw; i++)
-        mask &= mask - 1;
-      const int v = __shfl(lv, pos < 0 ? 0 : pos, kWave);
-      int mult = 0;
-      if (pos >= 0) {
-        const double p = s.pen[v];
-        const double xv = r / p;
-        for (uint32_t k = s.var_ptr[v] + g; k < s.var_ptr[v + 1]; k += G) {
-          mult += s.csr_c[k] == c;
-          push_decrement(s, k, xv, p);
+    // inclusive wave scan of the row lengths
+    int incl = len;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int t = __shfl_up(incl, o, kWave);
+      if (lane >= o)
+        incl += t;
+    }
+    const int total = __shfl(incl, kWave - 1, kWave);
+    pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
+    __builtin_amdgcn_wave_barrier();
+    for (int f0 = 0; f0 < total; f0 += kWave) {  // wave-uniform
+      const int f = f0 + lane;
+      const bool valid = f < total;
+      int o = 0;  // owner lane: last lane with pre <= f and len > 0 (== last with pre <= f)
+#pragma unroll
+      for (int step = kWave / 2; step > 0; step >>= 1)
+        if (o + step < kWave && pre[o + step] <= f)
+          o += step;
+      const int orb = __shfl(int(rb), o, kWave);
+      const int opre = pre[o];
+      const double ox = __shfl(lx, o, kWave);
+      const double op = __shfl(lp, o, kWave);
+      int32_t cc = -1;
+      double a0 = 0.0, a1 = 0.0;
+      bool fat = false;
+      if (valid) {
+        const uint32_t k = uint32_t(orb) + uint32_t(f - opre);
+        cc = s.csr_c[k];
+        if (cc == c || s.key[cc] == kDeadKey) {
+          cc = -1;
+        } else {
+          fat = s.cflags[cc] & 1;
+          const double w = s.csr_w[k];
+          a0 = w * ox;
+          a1 = w / op;
         }
       }
-      mult = grp_isum<G>(mult);
-      if (pos >= 0 && g == 0)
-        atomicSub(&s.votes[c], mult);
+      const int nel = total - f0 < kWave ? total - f0 : kWave;
+#pragma unroll
+      for (int t = 0; t < kWave / 16; t++) {
+        if (t * 16 >= nel)
+          break;
+        const int e = t * 16 + (lane >> 2);
+        const int ec = __shfl(cc, e, kWave);
+        const int ef = __shfl(int(fat), e, kWave);
+        const double e0 = __shfl(a0, e, kWave);
+        const double e1 = __shfl(a1, e, kWave);
+        if (ec >= 0 && q < 3 && (!ef || q == 2))
+          unsafeAtomicAdd(s.crec + 4 * int64_t(ec) + q, q == 0 ? e0 : q == 1 ? e1 : 1.0);
+      }
     }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0) {
+    s.ratio[c] = dinf();
+    s.key[c] = kDeadKey;
+    s.chg[c] = uint16_t(round);
   }
 }
 
@@ -517,6 +567,7 @@ __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, 
   // exclusive prefix of the per-segment ready counts, in LDS
   __shared__ int pre[kMaxBlocks + 1];
   __shared__ int part[kBlock + 1];
+  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_one)
   constexpr int kPer = kMaxBlocks / kBlock;
   int loc[kPer];
   int sum = 0;
@@ -546,6 +597,8 @@ __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, 
     pre[kMaxBlocks] = part[kBlock];
   __syncthreads();
   const int total = pre[kMaxBlocks];
+  if (total && blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
@@ -559,7 +612,7 @@ __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, 
       else
         hi = mid;
     }
-    saturate_one<G>(s, s.ready[lo * chunk + (i - pre[lo])], round, lane);
+    saturate_one(s, s.ready[lo * chunk + (i - pre[lo])], round, lane, wpre[threadIdx.x / kWave]);
   }
 }
 
@@ -580,22 +633,22 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
     const int32_t c = s.clist[cb][i];
     if (s.key[c] == kDeadKey)
       continue;
-    const int dc = s.dcnt[c];
+    double4* rec = reinterpret_cast<double4*>(s.crec) + c;
+    const double4 d = *rec;
+    const int dc = int(d.z);
     if (!dc) {  // untouched: ratio unchanged
       alive++;
       continue;
     }
     any_touch = 1;
-    s.dcnt[c] = 0;
+    *rec = make_double4(0.0, 0.0, 0.0, 0.0);
     s.acnt[c] -= dc;
     s.chg[c] = uint16_t(round);
     const double bound = s.cbound[c];
     double rem = s.rem[c], use;
     if (!(s.cflags[c] & 1)) {
-      use = s.use[c] - s.duse[c];
-      rem -= s.drem[c];
-      s.drem[c] = 0.0;
-      s.duse[c] = 0.0;
+      use = s.use[c] - d.y;
+      rem -= d.x;
       if (rem < bound * prec)
         rem = 0.0;
       if (use < prec)
