@@ -167,7 +167,8 @@ def main():
         with open(args.profile_json, "w") as f:
             json.dump(dict(per_kernel=per_kernel, rounds=rounds, alive_vars=av.tolist(), alive_elems=ae.tolist(),
                            reeval_vars=rv.tolist(), reeval_elems=re_.tolist(),
-                           device_ms=st["device_ms"]), f)
+                           device_ms=st["device_ms"], launch_slot=slot.tolist(), launch_round=rnd.tolist(),
+                           launch_ms=ms.tolist()), f)
 
     # ---- CPU baseline: the oracle (single-threaded restatement), bounded sample, rank 0, N=1 ----
     cpu = None

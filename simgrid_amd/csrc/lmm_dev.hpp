@@ -31,6 +31,20 @@ enum : int {
   CTL_WORDS = 32
 };
 
+// maxmin per-constraint state, one 64-B line per constraint (array-of-structs): a constraint touched
+// in a round dirties ONE line instead of one line in each of eight arrays (mm_update's write-back
+// at the kernel boundary), and the first three fields are the decrement record: the three pushes of
+// one element, issued by the 4 lanes of a quad in ONE wave instruction, are one memory-side atomic
+// request (scripts/ubench_atomic.hip: 2.9x the rate of three separate arrays).
+struct alignas(64) CstRec {
+  double drem, duse, dcnt;  // decrements pushed this round (atomics; dcnt = fixed elements)
+  int64_t pad;
+  double rem, use;          // remaining, usage (maxmin.cpp:520-535, 603-658)
+  double ratio;             // rem / use; +inf when out of the light table
+  double bound;             // constraint bound
+};
+static_assert(sizeof(CstRec) == 64, "CstRec must be one 64-B line");
+
 struct Dev {
   int32_t nV, nC;
   int64_t nnz;
@@ -47,8 +61,8 @@ struct Dev {
   const uint8_t* cflags;     // [nC] bit0 FATPIPE, bit1 zero-weight enabled element
   // per-variable state
   double* x;        // [nV] values (output)
-  int32_t* fixr;    // [nV] round in which the variable left the alive set (measurement only)
-  int32_t* vstate;  // [nV] maxmin: 0 alive, 1 fixed or dropped (claimed with atomicCAS)
+  int32_t* fixr;    // [nV] fair bottleneck: last round the variable was listed (measurement only)
+  int32_t* vstate;  // [nV] maxmin: 0 alive, r+1 = fixed or dropped in round r (claimed with atomicCAS)
   double* vtmp;     // [nV] fair bottleneck: mu
   uint8_t* vst;     // [nV] fair bottleneck: 1 listed / 0 not
   // per-constraint state
@@ -56,16 +70,16 @@ struct Dev {
   uint16_t* key;    // [nC] round-down 16-bit key of ratio, kDeadKey when out
   double* rem;      // [nC]
   double* use;      // [nC]
-  // [4*nC] per-constraint decrement record {remaining, usage, fixed elements, unused}: 32 B per
-  // constraint so the three pushes of one element, issued by the 4 lanes of a quad in ONE wave
-  // instruction, are one memory-side atomic request (scripts/ubench_atomic.hip: 2.9x the rate of
-  // three separate arrays)
-  double* crec;
-  int32_t* acnt;    // [nC] alive (unfixed) elements
-  int32_t* votes;   // [nC] persistent: alive elements whose variable votes for this constraint
+  CstRec* cst;      // [nC] maxmin: per-constraint record (one 64-B line, see CstRec)
+  // [nC] maxmin: alive elements whose variable votes for ANOTHER constraint (dense: mm_ready reads it
+  // for every alive constraint each round); ready iff 0.  Vote moves add/subtract the moving
+  // variable's multiplicity, fixed elements leave through the record's count in mm_update.
+  int32_t* nvote;
   uint16_t* chg;    // [nC] last round (mod 2^16) in which ratio / liveness changed
+  uint64_t* chgbits;  // [nC/64 + 2] bitmap: constraints changed in the last round (written by mm_update)
   int32_t* ready;   // [nC + slack] ready constraints, one segment per mm_ready block
   int32_t* bready;  // [kMaxBlocks] ready count of each segment
+  uint8_t* touched;  // [nC] 1 = received a decrement this round (set by the pushers, cleared by mm_update)
   int32_t* balive;  // [kMaxBlocks] constraints still alive after mm_update, per block
   int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
   int32_t* clist[2];  // [nC] alive-constraint lists (periodically compacted)

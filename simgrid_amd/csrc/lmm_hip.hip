@@ -48,6 +48,7 @@ struct lmmhip_ctx {
   bool uploaded = false;
   bool profiling = false;
   int group = 8;  // lanes per row in mm_vote (power of two >= mean row length, <= 64)
+  int n_cu = 256;  // compute units (grid of the one-block-per-CU kernels)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // per-launch event pairs (profiling mode): recorded without synchronising, resolved after the
   // solve, so the timed launch sequence is not serialised by the measurement.
@@ -56,6 +57,7 @@ struct lmmhip_ctx {
   std::vector<int> launch_slot, launch_round;
   std::vector<float> launch_ms;
   lmmhip_stats stats{};
+  int last_kind = LMMHIP_KIND_MAXMIN;
   int32_t* vstat = nullptr;  // profiling counters of mm_vote ([round][block] x 2)
 };
 
@@ -103,6 +105,8 @@ int lmmhip_ctx_create(int device, lmmhip_ctx** out) {
   }
   c->device = device;
   hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e == hipSuccess)
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess)
@@ -223,9 +227,8 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &d.key, nC);
   rc |= dalloc(c, &d.rem, nC);
   rc |= dalloc(c, &d.use, nC);
-  rc |= dalloc(c, &d.crec, 4 * nC);
-  rc |= dalloc(c, &d.acnt, nC);
-  rc |= dalloc(c, &d.votes, nC);
+  rc |= dalloc(c, &d.cst, nC);
+  rc |= dalloc(c, &d.nvote, nC);
   rc |= dalloc(c, &cvar0, nV);
   rc |= dalloc(c, &cvar1, nV);
   rc |= dalloc(c, &cvar2, nV);
@@ -239,6 +242,8 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
     rc |= dalloc(c, &d.skey[b], nV);
   }
   rc |= dalloc(c, &d.chg, nC);
+  rc |= dalloc(c, &d.chgbits, (nC + 127) / 128 * 2 + 2);
+  rc |= dalloc(c, &d.touched, nC);
   rc |= dalloc(c, &d.ready, nC + kMaxBlocks);
   rc |= dalloc(c, &d.bready, kMaxBlocks);
   rc |= dalloc(c, &d.balive, kMaxBlocks);
@@ -354,6 +359,7 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   if (c->profiling)
     HIPCHK(hipMemsetAsync(c->vstat, 0, stat_bytes, c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
+  c->last_kind = kind;
   int rc = kind == LMMHIP_KIND_MAXMIN ? solve_maxmin(c, precision) : solve_fair(c, precision);
   if (rc)
     return rc;
@@ -426,7 +432,11 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   switch (G) {
   case 4:
   case 8:  // short rows: one lane per row (more gathers in flight per wave)
-    LAUNCH(2, r, mm_vote_lane, grid, kBlock, d, buf, int(r));
+    if (int64_t(d.nC) <= int64_t(kBitWords) * 64) {
+      LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, buf, int(r));
+    } else {
+      LAUNCH(2, r, (mm_vote_lane<kBlock, false>), grid, kBlock, d, buf, int(r));
+    }
     break;
   case 16:
     LAUNCH(2, r, mm_vote<16>, grid, kBlock, d, buf, int(r));
@@ -441,30 +451,6 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   return 0;
 }
 
-static int launch_saturate(lmmhip_ctx* c, int64_t r, int64_t ncl, int cb, int gL) {
-  const Dev& d = c->d;
-  int64_t g = ncl / kBlock;
-  const int grid = int(g < 1 ? 1 : g > kMaxBlocks ? kMaxBlocks : g);
-  switch (c->group) {
-  case 4:
-    LAUNCH(4, r, mm_saturate<4>, grid, kBlock, d, int(r), cb, gL);
-    break;
-  case 8:
-    LAUNCH(4, r, mm_saturate<8>, grid, kBlock, d, int(r), cb, gL);
-    break;
-  case 16:
-    LAUNCH(4, r, mm_saturate<16>, grid, kBlock, d, int(r), cb, gL);
-    break;
-  case 32:
-    LAUNCH(4, r, mm_saturate<32>, grid, kBlock, d, int(r), cb, gL);
-    break;
-  default:
-    LAUNCH(4, r, mm_saturate<64>, grid, kBlock, d, int(r), cb, gL);
-    break;
-  }
-  return 0;
-}
-
 // Slots: 0 mm_init_cnsts, 1 mm_init_vars, 2 mm_vote, 3 mm_ready, 4 mm_saturate, 5 mm_update,
 // 6 compaction.
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
@@ -474,6 +460,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, mm_init_vars, grid_for(d.nV, kBlock), kBlock, d);
   LAUNCH(1, -1, mm_clist, gC, kBlock, d, 0, 0, 1);
+  HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
+  const int gU = gC;  // mm_update: thread per constraint, identity order
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
   int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
@@ -484,11 +472,10 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
-      if (int rc = launch_saturate(c, r, ncl, cb, gL))
-        return rc;
-      LAUNCH(5, r, mm_update, gL, kBlock, d, int(r), prec, cb);
+      LAUNCH(4, r, mm_saturate, grid_for(ncl, kBlock), kBlock, d, int(r), cb, gL);
+      LAUNCH(5, r, mm_update, gU, kBlock, d, int(r), prec);
     }
-    LAUNCH(6, r, mm_done, 1, kBlock, d, gL);
+    LAUNCH(6, r, mm_done, 1, kBlock, d, gU);
     if (int rc = poll_ctl(c))
       return rc;
     if (c->h_ctl[CTL_DONE])
@@ -576,10 +563,15 @@ int lmmhip_round_profile(lmmhip_ctx* c, int64_t* alive_vars, int64_t* alive_elem
   std::vector<uint32_t> vp(size_t(nV) + 1);
   HIPCHK(hipSetDevice(c->device));
   if (nV) {
-    HIPCHK(hipMemcpyAsync(fr.data(), c->d.fixr, sizeof(int32_t) * nV, hipMemcpyDeviceToHost, c->stream));
+    // maxmin: vstate = exit round + 1 (0 = never fixed); fair bottleneck: fixr = last listed round
+    const int32_t* src = c->last_kind == LMMHIP_KIND_MAXMIN ? c->d.vstate : c->d.fixr;
+    HIPCHK(hipMemcpyAsync(fr.data(), src, sizeof(int32_t) * nV, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(vp.data(), c->d.var_ptr, sizeof(uint32_t) * (nV + 1), hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->last_kind == LMMHIP_KIND_MAXMIN)
+    for (auto& f : fr)
+      f -= 1;
   const int R = int(c->stats.rounds);
   // a variable is alive in rounds 0..fixr (inclusive); -1 = never processed
   std::vector<int64_t> dv(size_t(R) + 2, 0), de(size_t(R) + 2, 0);

@@ -12,7 +12,7 @@
 //                minimal 16-bit key over the row, exact fp64 only on key ties / bound checks; move
 //                the vote; a variable whose level bound*penalty is below its minimum is fixed at its
 //                bound right here (maxmin.cpp:563-595); a variable with no alive constraint drops.
-//   mm_ready     one thread per constraint: votes == alive elements -> ready list.
+//   mm_ready     one thread per constraint: no alive element votes elsewhere (nvote == 0) -> ready list.
 //   mm_saturate  one wave per ready constraint: claim its alive variables (atomicCAS), fix them at
 //                ratio/penalty (maxmin.cpp:583), push w*x, w/p and count decrements (maxmin.cpp:601-606).
 //   mm_update    one thread per constraint: apply decrements, clamp (surf_interface.hpp:34-44 —
@@ -43,15 +43,19 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
       const double bound = s.cbound[c];
       const bool part = bound > bound * prec;
       const double usage = part ? acc : 0.0;
-      s.rem[c] = bound;
-      s.use[c] = usage;
-      reinterpret_cast<double4*>(s.crec)[c] = make_double4(0.0, 0.0, 0.0, 0.0);
-      s.acnt[c] = int32_t(e - b);
-      s.votes[c] = 0;
-      s.chg[c] = uint16_t(0xFFFF);
       const bool alive = part && usage > 0;
       const double r = bound / usage;
-      s.ratio[c] = alive ? r : dinf();
+      CstRec rec;
+      rec.drem = rec.duse = rec.dcnt = 0.0;
+      rec.pad = 0;
+      rec.rem = bound;
+      rec.use = usage;
+      rec.ratio = alive ? r : dinf();
+      rec.bound = bound;
+      s.cst[c] = rec;
+      s.touched[c] = 0;
+      s.nvote[c] = int32_t(e - b);  // no element votes yet
+      s.chg[c] = uint16_t(0xFFFF);
       s.key[c] = alive ? ratio_key(r) : uint16_t(kDeadKey);
       alive_cnt += alive;
     }
@@ -63,7 +67,6 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
 __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
     s.x[v] = 0.0;
-    s.fixr[v] = -1;
     s.vstate[v] = 0;
     s.rtgt[0][v] = kUnvoted;
   }
@@ -79,7 +82,8 @@ __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double 
   const int32_t c = s.csr_c[j];
   if (s.key[c] == kDeadKey)
     return;
-  double* r = s.crec + 4 * int64_t(c);
+  double* r = &s.cst[c].drem;
+  s.touched[c] = 1;
   unsafeAtomicAdd(&r[2], 1.0);
   if (!(s.cflags[c] & 1)) {
     const double w = s.csr_w[j];
@@ -164,11 +168,11 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
       double minr = dinf();
       if (live && (nmin > 1 || vb > 0)) {
         if (h0 && k0 == mk)
-          minr = s.ratio[c0];
+          minr = s.cst[c0].ratio;
         for (uint32_t j = j0 + G; j < e; j += G) {
           const int32_t c = ccol[j];
           if (key[c] == mk)
-            minr = fmin(minr, s.ratio[c]);
+            minr = fmin(minr, s.cst[c].ratio);
         }
       }
       minr = grp_min<G>(minr);
@@ -176,11 +180,11 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
       const bool bounded = live && vb > 0 && vb * p < minr;
       int newt = INT_MAX;
       if (live && !bounded) {
-        if (h0 && k0 == mk && (nmin == 1 || s.ratio[c0] == minr))
+        if (h0 && k0 == mk && (nmin == 1 || s.cst[c0].ratio == minr))
           newt = c0;
         for (uint32_t j = j0 + G; j < e; j += G) {
           const int32_t c = ccol[j];
-          if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
+          if (key[c] == mk && (nmin == 1 || s.cst[c].ratio == minr))
             newt = min(newt, c);
         }
       }
@@ -204,25 +208,23 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
       mult_old = grp_isum<G>(mult_old);
       if (need && !live) {  // every constraint of v left the light table: v stays at 0
         if (g == 0) {
-          s.vstate[v] = 1;
-          s.fixr[v] = round;
+          s.vstate[v] = round + 1;  // fixed / dropped in this round
           rtgt[row] = kRetired;
         }
       } else if (bounded) {  // fixed at its bound (maxmin.cpp:587-589)
         if (g == 0) {
-          s.vstate[v] = 1;
-          s.fixr[v] = round;
+          s.vstate[v] = round + 1;  // fixed / dropped in this round
           s.x[v] = vb;
           rtgt[row] = kRetired;
           if (t >= 0 && key[t] != kDeadKey)
-            atomicSub(&s.votes[t], mult_old);
+            atomicAdd(&s.nvote[t], mult_old);
         }
         for (uint32_t j = s.var_ptr[v] + g; j < s.var_ptr[v + 1]; j += G)
           push_decrement(s, j, vb, p);
       } else if (live && newt != t && g == 0) {
         if (t >= 0 && key[t] != kDeadKey)
-          atomicSub(&s.votes[t], mult_old);
-        atomicAdd(&s.votes[newt], mult_new);
+          atomicAdd(&s.nvote[t], mult_old);
+        atomicSub(&s.nvote[newt], mult_new);
         rtgt[row] = newt;
       }
     }
@@ -299,8 +301,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     nmin += key[ccol[j]] == mk;
   const double vb = s.vbound[v];
   if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
-    s.vstate[v] = 1;
-    s.fixr[v] = round;
+    s.vstate[v] = round + 1;  // fixed / dropped in this round
     rtgt[row] = kRetired;
     return;
   }
@@ -309,11 +310,11 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 #pragma unroll
     for (int i = 0; i < kReg; i++)
       if (kk[i] == mk)
-        minr = fmin(minr, s.ratio[cc[i]]);
+        minr = fmin(minr, s.cst[cc[i]].ratio);
     for (uint32_t j = b + kReg; j < e; j++) {
       const int32_t c = ccol[j];
       if (key[c] == mk)
-        minr = fmin(minr, s.ratio[c]);
+        minr = fmin(minr, s.cst[c].ratio);
     }
   }
   int mult_old = 0;
@@ -324,12 +325,11 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     mult_old += ccol[j] == t;
   const double p = s.pen[v];
   if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
-    s.vstate[v] = 1;
-    s.fixr[v] = round;
+    s.vstate[v] = round + 1;  // fixed / dropped in this round
     s.x[v] = vb;
     rtgt[row] = kRetired;
     if (t >= 0 && key[t] != kDeadKey)
-      atomicSub(&s.votes[t], mult_old);
+      atomicAdd(&s.nvote[t], mult_old);
     for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
       push_decrement(s, j, vb, p);
     return;
@@ -337,11 +337,11 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   int newt = INT_MAX;
 #pragma unroll
   for (int i = 0; i < kReg; i++)
-    if (kk[i] == mk && (nmin == 1 || s.ratio[cc[i]] == minr))
+    if (kk[i] == mk && (nmin == 1 || s.cst[cc[i]].ratio == minr))
       newt = min(newt, cc[i]);
   for (uint32_t j = b + kReg; j < e; j++) {
     const int32_t c = ccol[j];
-    if (key[c] == mk && (nmin == 1 || s.ratio[c] == minr))
+    if (key[c] == mk && (nmin == 1 || s.cst[c].ratio == minr))
       newt = min(newt, c);
   }
   unsigned sk = kDeadKey;  // min key over the other constraints of the row
@@ -364,19 +364,33 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   for (uint32_t j = b + kReg; j < e; j++)
     mult_new += ccol[j] == newt;
   if (t >= 0 && key[t] != kDeadKey)
-    atomicSub(&s.votes[t], mult_old);
-  atomicAdd(&s.votes[newt], mult_new);
+    atomicAdd(&s.nvote[t], mult_old);
+  atomicSub(&s.nvote[newt], mult_new);
   rtgt[row] = newt;
 }
 
-__global__ void __launch_bounds__(kBlock) mm_vote_lane(Dev s, int buf, int round) {
+// kBits: the "target changed last round" test reads a bitmap of the changed constraints held in LDS
+// (built by mm_update, one bit per constraint, loaded once per block) instead of gathering the 16-bit
+// change stamp of every alive row's target from HBM/L2 — the filter then streams only the row
+// targets.  One 1024-thread block per CU (the bitmap takes up to kBitWords * 8 B of LDS).
+constexpr int kVBlock = 1024;
+constexpr int kBitWords = 17408;  // LDS bitmap capacity: 1,114,112 constraints
+template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int buf, int round) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ int st_rows, st_elems;
-  __shared__ int q[kBlock * (kFilt + 1)];  // queued rows (relative to the block's chunk base)
+  __shared__ int q[B * (kFilt + 1)];  // queued rows (relative to the block's chunk base)
   __shared__ int qn;
+  __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
   if (threadIdx.x == 0)
     st_rows = st_elems = qn = 0;
+  if (kBits) {
+    const int n16 = (s.nC + 127) / 128;  // 16-B pieces of the bitmap
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(s.chgbits);
+    uint4* dst = reinterpret_cast<uint4*>(bits);
+    for (int i = threadIdx.x; i < n16; i += B)
+      dst[i] = src[i];
+  }
   __syncthreads();
   const int64_t nrows = s.ctl[CTL_NROWS + buf];
   const int32_t* __restrict__ rtgt = s.rtgt[buf];
@@ -384,7 +398,7 @@ __global__ void __launch_bounds__(kBlock) mm_vote_lane(Dev s, int buf, int round
   const uint16_t* __restrict__ key = s.key;
   const uint16_t prev = uint16_t(round - 1);
   // contiguous chunk per block so queued rows fit in 32-bit offsets from the chunk base
-  constexpr int kStep = kBlock * kFilt;
+  constexpr int kStep = B * kFilt;
   const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kStep - 1) / kStep * kStep;
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
@@ -392,18 +406,22 @@ __global__ void __launch_bounds__(kBlock) mm_vote_lane(Dev s, int buf, int round
     int tt[kFilt];
 #pragma unroll
     for (int u = 0; u < kFilt; u++) {
-      const int64_t row = base + u * kBlock + threadIdx.x;
+      const int64_t row = base + u * B + threadIdx.x;
       tt[u] = row < hi ? rtgt[row] : kRetired;
     }
-    unsigned ch[kFilt];
-#pragma unroll
-    for (int u = 0; u < kFilt; u++)
-      ch[u] = tt[u] >= 0 ? s.chg[tt[u]] : 0u;
+    bool ch[kFilt];
 #pragma unroll
     for (int u = 0; u < kFilt; u++) {
-      const int64_t row = base + u * kBlock + threadIdx.x;
+      if (kBits)
+        ch[u] = tt[u] >= 0 && ((bits[tt[u] >> 6] >> (tt[u] & 63)) & 1);
+      else
+        ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
+    }
+#pragma unroll
+    for (int u = 0; u < kFilt; u++) {
+      const int64_t row = base + u * B + threadIdx.x;
       bool need = tt[u] == kUnvoted;
-      if (tt[u] >= 0 && ch[u] == prev)  // target changed last round: does the vote still stand?
+      if (ch[u])  // target changed last round: does the vote still stand?
         need = !(key[tt[u]] < skey[row]);
       const unsigned long long m = __ballot(need);  // one LDS atomic per wave
       const int lane = threadIdx.x & (kWave - 1);
@@ -417,9 +435,9 @@ __global__ void __launch_bounds__(kBlock) mm_vote_lane(Dev s, int buf, int round
     }
     __syncthreads();
     int n = qn;
-    while (n >= kBlock) {  // resolve full queues: the last kBlock entries each time
-      vote_row(s, buf, round, lo + q[n - kBlock + threadIdx.x], &st_rows, &st_elems);
-      n -= kBlock;
+    while (n >= B) {  // resolve full queues: the last B entries each time
+      vote_row(s, buf, round, lo + q[n - B + threadIdx.x], &st_rows, &st_elems);
+      n -= B;
     }
     __syncthreads();
     if (threadIdx.x == 0)
@@ -456,7 +474,7 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
   for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     const int32_t c = s.clist[cb][i];
-    if (s.key[c] != kDeadKey && s.votes[c] == s.acnt[c])
+    if (s.key[c] != kDeadKey && s.nvote[c] == 0)
       s.ready[lo + atomicAdd(&cnt, 1)] = c;
   }
   __syncthreads();
@@ -464,10 +482,7 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
     s.bready[blockIdx.x] = cnt;
 }
 
-// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.  One wave per ready
-// constraint; its lanes claim the alive variables on it (atomicCAS: duplicates / variables shared by
-// two ready constraints), fix them at ratio/penalty, then G-lane groups push the decrements of the
-// claimed variables' rows in parallel.
+// Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.
 // One wave per ready constraint c.  Per 64-element chunk of c's CSC segment: lanes claim the alive
 // variables (atomicCAS: a duplicate element claims once), fix them at ratio/penalty; then the
 // claimed variables' CSR elements are flattened over the wave (wave prefix of the row lengths, owner
@@ -477,7 +492,7 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
 // skipped: c leaves the light table (every alive variable on it is fixed, usage -> 0,
 // maxmin.cpp:608-615).
 __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane, int* pre) {
-  const double r = s.ratio[c];
+  const double r = s.cst[c].ratio;
   const int q = lane & 3;
   const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
   for (uint32_t base = cb; base < ce; base += kWave) {  // wave-uniform
@@ -485,7 +500,7 @@ __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round,
     int32_t lv = -1;
     if (j < ce) {
       lv = s.csc_v[j];
-      if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, 1) != 0)
+      if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
         lv = -1;
     }
     double lp = 1.0, lx = 0.0;
@@ -495,7 +510,6 @@ __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round,
       lp = s.pen[lv];
       lx = r / lp;
       s.x[lv] = lx;
-      s.fixr[lv] = round;
       rb = s.var_ptr[lv];
       len = int(s.var_ptr[lv + 1] - rb);
     }
@@ -548,77 +562,81 @@ __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round,
         const double e0 = __shfl(a0, e, kWave);
         const double e1 = __shfl(a1, e, kWave);
         if (ec >= 0 && q < 3 && (!ef || q == 2))
-          unsafeAtomicAdd(s.crec + 4 * int64_t(ec) + q, q == 0 ? e0 : q == 1 ? e1 : 1.0);
+          unsafeAtomicAdd(&s.cst[ec].drem + q, q == 0 ? e0 : q == 1 ? e1 : 1.0);
+        if (ec >= 0 && q == 3)
+          s.touched[ec] = 1;  // plain byte store: mm_update reads 1 B per constraint, not the record
       }
     }
     __builtin_amdgcn_wave_barrier();
   }
   if (lane == 0) {
-    s.ratio[c] = dinf();
+    s.cst[c].ratio = dinf();
     s.key[c] = kDeadKey;
     s.chg[c] = uint16_t(round);
   }
 }
 
-template <int G>
+// One wave per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
+// counts in LDS (parallel: 8 segments per thread, wave shuffles, one LDS exchange) and maps its waves
+// onto the ready list by binary search.
 __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, int ready_blocks) {
   if (s.ctl[CTL_DONE])
     return;
-  // exclusive prefix of the per-segment ready counts, in LDS
   __shared__ int pre[kMaxBlocks + 1];
-  __shared__ int part[kBlock + 1];
+  __shared__ int wsum[kBlock / kWave];
   __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_one)
   constexpr int kPer = kMaxBlocks / kBlock;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   int loc[kPer];
   int sum = 0;
+#pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int seg = threadIdx.x * kPer + k;
     loc[k] = seg < ready_blocks ? s.bready[seg] : 0;
     sum += loc[k];
   }
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = 0; i < kBlock; i++) {
-      const int t = part[i];
-      part[i] = acc;
-      acc += t;
-    }
-    part[kBlock] = acc;
+  int incl = sum;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int t = __shfl_up(incl, o, kWave);
+    if (lane >= o)
+      incl += t;
   }
+  if (lane == kWave - 1)
+    wsum[w] = incl;
   __syncthreads();
-  int acc = part[threadIdx.x];
+  int acc = incl - sum, total = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / kWave; i++) {
+    acc += i < w ? wsum[i] : 0;
+    total += wsum[i];
+  }
+#pragma unroll
   for (int k = 0; k < kPer; k++) {
     pre[threadIdx.x * kPer + k] = acc;
     acc += loc[k];
   }
-  if (threadIdx.x == 0)
-    pre[kMaxBlocks] = part[kBlock];
   __syncthreads();
-  const int total = pre[kMaxBlocks];
   if (total && blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-  const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
   const int64_t chunk = chunk_of(s.ctl[CTL_NCL0 + cb], ready_blocks);
   for (int64_t i = wave; i < total; i += nwaves) {
-    int lo = 0, hi = ready_blocks;  // last segment with pre[seg] <= i
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) / 2;
-      if (pre[mid] <= i)
-        lo = mid;
-      else
-        hi = mid;
-    }
-    saturate_one(s, s.ready[lo * chunk + (i - pre[lo])], round, lane, wpre[threadIdx.x / kWave]);
+    int lo = 0;  // last segment with pre[seg] <= i
+#pragma unroll
+    for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
+      if (lo + step < ready_blocks && pre[lo + step] <= i)
+        lo += step;
+    saturate_one(s, s.ready[lo * chunk + (i - pre[lo])], round, lane, wpre[w]);
   }
 }
 
-// Round phase 4 — constraint update: maxmin.cpp:603-658.  balive[block] = constraints of the
-// block's range still in the light table (read by mm_done; plain stores, no global atomic).
-__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec, int cb) {
+// Round phase 4 — constraint update: maxmin.cpp:603-658.  Thread per constraint in identity order
+// (a wave = 64 consecutive constraints), so the changed-constraint bitmap the next vote reads is one
+// ballot per wave.  balive[block] = constraints of the block's range still in the light table (read
+// by mm_done; plain stores, no global atomic).
+__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -627,52 +645,62 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   if (threadIdx.x == 0)
     alive_cnt = 0;
   __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
   int alive = 0, any_touch = 0;
-  const int64_t n = s.ctl[CTL_NCL0 + cb];
-  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-    const int32_t c = s.clist[cb][i];
-    if (s.key[c] == kDeadKey)
-      continue;
-    double4* rec = reinterpret_cast<double4*>(s.crec) + c;
-    const double4 d = *rec;
-    const int dc = int(d.z);
-    if (!dc) {  // untouched: ratio unchanged
-      alive++;
-      continue;
-    }
-    any_touch = 1;
-    *rec = make_double4(0.0, 0.0, 0.0, 0.0);
-    s.acnt[c] -= dc;
-    s.chg[c] = uint16_t(round);
-    const double bound = s.cbound[c];
-    double rem = s.rem[c], use;
-    if (!(s.cflags[c] & 1)) {
-      use = s.use[c] - d.y;
-      rem -= d.x;
-      if (rem < bound * prec)
-        rem = 0.0;
-      if (use < prec)
-        use = 0.0;
-    } else {  // FATPIPE: usage = max w/p over enabled elements whose variable is still at 0
-      use = 0.0;
-      for (uint32_t j = s.cnst_ptr[c]; j < s.cnst_ptr[c + 1]; j++) {
-        const int32_t v = s.csc_v[j];
-        if (s.x[v] > 0)
-          continue;
-        use = fmax(use, s.csc_w[j] / s.pen[v]);
+  for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
+       base += int64_t(gridDim.x) * kBlock) {  // wave-uniform
+    const int64_t c = base + lane;
+    bool changed = false;
+    if (c < s.nC) {
+      if (s.key[c] == kDeadKey) {
+        changed = s.chg[c] == uint16_t(round);  // saturated by mm_saturate this round
+      } else {
+        if (!s.touched[c]) {  // untouched: ratio unchanged
+          alive++;
+        } else {
+          changed = true;
+          any_touch = 1;
+          s.touched[c] = 0;
+          CstRec* rec = s.cst + c;
+          const double dx = rec->drem, dy = rec->duse, dz = rec->dcnt;
+          rec->drem = rec->duse = rec->dcnt = 0.0;
+          s.nvote[c] -= int(dz);  // fixed elements leave (voters of c were compensated)
+          s.chg[c] = uint16_t(round);
+          const double bound = rec->bound;
+          double rem = rec->rem, use;
+          if (!(s.cflags[c] & 1)) {
+            use = rec->use - dy;
+            rem -= dx;
+            if (rem < bound * prec)
+              rem = 0.0;
+            if (use < prec)
+              use = 0.0;
+          } else {  // FATPIPE: usage = max w/p over enabled elements whose variable is still at 0
+            use = 0.0;
+            for (uint32_t j = s.cnst_ptr[c]; j < s.cnst_ptr[c + 1]; j++) {
+              const int32_t v = s.csc_v[j];
+              if (s.x[v] > 0)
+                continue;
+              use = fmax(use, s.csc_w[j] / s.pen[v]);
+            }
+          }
+          rec->rem = rem;
+          rec->use = use;
+          if (!(use > prec) || !(rem > bound * prec)) {
+            s.cst[c].ratio = dinf();
+            s.key[c] = kDeadKey;
+          } else {
+            const double r = rem / use;
+            s.cst[c].ratio = r;
+            s.key[c] = ratio_key(r);
+            alive++;
+          }
+        }
       }
     }
-    s.rem[c] = rem;
-    s.use[c] = use;
-    if (!(use > prec) || !(rem > bound * prec)) {
-      s.ratio[c] = dinf();
-      s.key[c] = kDeadKey;
-    } else {
-      const double r = rem / use;
-      s.ratio[c] = r;
-      s.key[c] = ratio_key(r);
-      alive++;
-    }
+    const unsigned long long word = __ballot(changed);
+    if (lane == 0)
+      s.chgbits[base >> 6] = word;
   }
   if (alive)
     atomicAdd(&alive_cnt, alive);
