@@ -93,6 +93,29 @@ int lmm_gen_maxmin_bench(lmm_sys* s, int klass, int run, int64_t* cnst_out, int6
 int64_t lmm_gen_synthetic(lmm_sys* s, int64_t nb_cnst, int64_t nb_var, int k, uint64_t seed, int max_share,
                           int penalty_mix, int bounded_permille, int fatpipe_permille, int64_t* var_out);
 
+/* Cluster platforms: the links of one FAT_TREE / DRAGONFLY <cluster>
+ * (FatTreeZone.cpp, DragonflyZone.cpp) and n_flows random host-to-host flows turned into variables
+ * the way NetworkCm02Model::communicate (network_cm02.cpp:165-279, CM02 / LV08) or L07Action
+ * (ptask_L07.cpp:143-208) does, in the state after each flow's latency is paid.  See
+ * simgrid_amd/csrc/lmm_platforms.hpp for what is restated. */
+typedef struct lmm_platform_params {
+  int topology;                /* 0 FAT_TREE, 1 DRAGONFLY */
+  const char* topo_parameters; /* e.g. "2;4,4;1,2;1,2" (fat tree), "3,4;4,3;5,1;2" (dragonfly) */
+  double bw, lat;              /* cluster link bandwidth (B/s), latency (s) */
+  int policy;                  /* 0 SHARED, 1 SPLITDUPLEX, 2 FATPIPE */
+  double loopback_bw, loopback_lat, limiter_bw;
+  double speed;                /* host speed (flop/s): L07 CPU constraints */
+  int model;                   /* 0 CM02, 1 LV08, 2 L07 */
+  int crosstraffic;            /* CM02 / LV08: the back route at weight 0.05 */
+  int64_t n_flows;
+  uint64_t seed;
+  double size_min, size_max;   /* L07 flow sizes (bytes) */
+  double tcp_gamma;            /* network/TCP-gamma */
+} lmm_platform_params;
+int lmm_platform_size(const lmm_platform_params* p, int64_t* n_links, int64_t* n_hosts);
+/* constraints: one per link (creation order), then for L07 one CPU per host; returns n_flows or -1 */
+int64_t lmm_gen_platform_flows(lmm_sys* s, const lmm_platform_params* p, int64_t* cnst_out, int64_t* var_out);
+
 int lmm_device_count(void);
 const char* lmm_last_error(void);
 

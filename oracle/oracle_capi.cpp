@@ -6,7 +6,11 @@
 #include <cstdint>
 #include <cstring>
 
+#include <memory>
+
+#include "../include/lmm/lmm_system.h"
 #include "../simgrid_amd/csrc/lmm_generators.hpp"
+#include "../simgrid_amd/csrc/lmm_platforms.hpp"
 #include "lmm_oracle.hpp"
 
 using namespace lmm_oracle;
@@ -185,6 +189,35 @@ long long oracle_gen_synthetic(void* s, long long nb_cnst, long long nb_var, int
   if (var_out)
     std::memcpy(var_out, vs.data(), vs.size() * sizeof(void*));
   return nb_var;
+}
+
+// Cluster platform + flows, same generator as the product's lmm_gen_platform_flows.
+int oracle_platform_size(const lmm_platform_params* p, long long* n_links, long long* n_hosts) {
+  try {
+    std::unique_ptr<lmm_plat::Platform> plat(lmm_plat::make_platform(lmm_plat::params_from(*p)));
+    *n_links = (long long)plat->links.size();
+    *n_hosts = plat->n_hosts;
+    return 0;
+  } catch (const std::exception&) {
+    return -1;
+  }
+}
+long long oracle_gen_platform_flows(void* s, const lmm_platform_params* p, void** cnst_out, void** var_out) {
+  try {
+    const lmm_plat::Params prm = lmm_plat::params_from(*p);
+    std::unique_ptr<lmm_plat::Platform> plat(lmm_plat::make_platform(prm));
+    Builder b{S(s)};
+    std::vector<Constraint*> cs;
+    std::vector<Variable*> vs;
+    lmm_plat::flows(b, *plat, prm, &cs, var_out ? &vs : nullptr);
+    if (cnst_out)
+      std::memcpy(cnst_out, cs.data(), cs.size() * sizeof(void*));
+    if (var_out)
+      std::memcpy(var_out, vs.data(), vs.size() * sizeof(void*));
+    return prm.n_flows;
+  } catch (const std::exception&) {
+    return -1;
+  }
 }
 
 }  // extern "C"

@@ -17,6 +17,26 @@ D = ct.c_double
 I = ct.c_int
 LL = ct.c_longlong
 
+FAT_TREE, DRAGONFLY = 0, 1
+SHARED, SPLITDUPLEX, FATPIPE = 0, 1, 2
+CM02, LV08, L07 = 0, 1, 2
+
+
+class PlatformParams(ct.Structure):
+    """lmm_platform_params (include/lmm/lmm_system.h)."""
+    _fields_ = [("topology", I), ("topo_parameters", ct.c_char_p), ("bw", D), ("lat", D), ("policy", I),
+                ("loopback_bw", D), ("loopback_lat", D), ("limiter_bw", D), ("speed", D), ("model", I),
+                ("crosstraffic", I), ("n_flows", LL), ("seed", ct.c_ulonglong), ("size_min", D), ("size_max", D),
+                ("tcp_gamma", D)]
+
+
+def platform_params(topology=FAT_TREE, topo_parameters="", bw=1.25e8, lat=5e-5, policy=SPLITDUPLEX, loopback_bw=0.0,
+                    loopback_lat=0.0, limiter_bw=0.0, speed=1e9, model=LV08, crosstraffic=True, n_flows=1000,
+                    seed=1, size_min=1e6, size_max=1e9, tcp_gamma=4194304.0):
+    return PlatformParams(topology, topo_parameters.encode(), bw, lat, policy, loopback_bw, loopback_lat, limiter_bw,
+                          speed, model, int(crosstraffic), n_flows, seed, size_min, size_max, tcp_gamma)
+
+
 _SIGS = {
     "oracle_set_precision": (None, [D]),
     "oracle_get_precision": (D, []),
@@ -61,6 +81,8 @@ _SIGS = {
     "oracle_update_constraint_bound": (None, [P, P, D]),
     "oracle_gen_maxmin_bench": (I, [P, I, I, ct.POINTER(P), ct.POINTER(P), ct.POINTER(I), ct.POINTER(I)]),
     "oracle_gen_synthetic": (LL, [P, LL, LL, I, ct.c_ulonglong, I, I, I, I, ct.POINTER(P)]),
+    "oracle_platform_size": (I, [ct.POINTER(PlatformParams), ct.POINTER(LL), ct.POINTER(LL)]),
+    "oracle_gen_platform_flows": (LL, [P, ct.POINTER(PlatformParams), ct.POINTER(P), ct.POINTER(P)]),
 }
 
 
@@ -263,6 +285,17 @@ class System:
         lib().oracle_gen_synthetic(self.h, nb_cnst, nb_var, k, seed, max_share, penalty_mix, bounded_permille,
                                    fatpipe_permille, vs)
         return vs
+
+    def gen_platform_flows(self, p):
+        """Links (+ L07 CPUs) and p.n_flows flows: (constraint list, variable handle array)."""
+        nl, nh = LL(), LL()
+        if lib().oracle_platform_size(ct.byref(p), ct.byref(nl), ct.byref(nh)) != 0:
+            raise ValueError("bad platform parameters")
+        nc = nl.value + (nh.value if p.model == L07 else 0)
+        cs, vs = (P * nc)(), (P * p.n_flows)()
+        if lib().oracle_gen_platform_flows(self.h, ct.byref(p), cs, vs) < 0:
+            raise ValueError("bad platform parameters")
+        return [Constraint(self, cs[i]) for i in range(nc)], vs
 
     def values_of(self, handles, n):
         import numpy as np

@@ -1,12 +1,14 @@
 // lmm_capi.cpp — extern "C" surface of include/lmm/lmm_system.h over simgrid_amd::lmm::System.
 // No exception crosses the ABI: every C++ error becomes a negative return code + lmm_last_error().
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 
 #include "../../include/lmm/lmm_hip.h"
 #include "../../include/lmm/lmm_system.h"
 #include "lmm_generators.hpp"
+#include "lmm_platforms.hpp"
 #include "lmm_system.hpp"
 
 using simgrid_amd::lmm::Id;
@@ -238,6 +240,38 @@ int64_t lmm_gen_synthetic(lmm_sys* s, int64_t nb_cnst, int64_t nb_var, int k, ui
     for (size_t i = 0; var_out && i < vs.size(); i++)
       var_out[i] = vs[i];
     return nb_var;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int lmm_platform_size(const lmm_platform_params* p, int64_t* n_links, int64_t* n_hosts) {
+  try {
+    std::unique_ptr<lmm_plat::Platform> plat(lmm_plat::make_platform(lmm_plat::params_from(*p)));
+    if (n_links)
+      *n_links = int64_t(plat->links.size());
+    if (n_hosts)
+      *n_hosts = plat->n_hosts;
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int64_t lmm_gen_platform_flows(lmm_sys* s, const lmm_platform_params* p, int64_t* cnst_out, int64_t* var_out) {
+  try {
+    const lmm_plat::Params prm = lmm_plat::params_from(*p);
+    std::unique_ptr<lmm_plat::Platform> plat(lmm_plat::make_platform(prm));
+    Builder b{&s->sys};
+    std::vector<Id> cs, vs;
+    lmm_plat::flows(b, *plat, prm, &cs, var_out ? &vs : nullptr);
+    for (size_t i = 0; cnst_out && i < cs.size(); i++)
+      cnst_out[i] = cs[i];
+    for (size_t i = 0; var_out && i < vs.size(); i++)
+      var_out[i] = vs[i];
+    return prm.n_flows;
   } catch (const std::exception& ex) {
     g_err = ex.what();
     return -1;

@@ -17,6 +17,26 @@ LIB_PATH = os.path.join(_HERE, "_lib", "liblmm_amd.so")
 P, D, I, I64, U64 = ct.c_void_p, ct.c_double, ct.c_int, ct.c_int64, ct.c_uint64
 PI, PD, PI64 = ct.POINTER(I), ct.POINTER(D), ct.POINTER(I64)
 
+# cluster platforms (lmm_platform_params, include/lmm/lmm_system.h)
+FAT_TREE, DRAGONFLY = 0, 1
+SHARED, SPLITDUPLEX, FATPIPE = 0, 1, 2
+CM02, LV08, L07 = 0, 1, 2
+
+
+class PlatformParams(ct.Structure):
+    _fields_ = [("topology", I), ("topo_parameters", ct.c_char_p), ("bw", D), ("lat", D), ("policy", I),
+                ("loopback_bw", D), ("loopback_lat", D), ("limiter_bw", D), ("speed", D), ("model", I),
+                ("crosstraffic", I), ("n_flows", I64), ("seed", U64), ("size_min", D), ("size_max", D),
+                ("tcp_gamma", D)]
+
+
+def platform_params(topology=FAT_TREE, topo_parameters="", bw=1.25e8, lat=5e-5, policy=SPLITDUPLEX, loopback_bw=0.0,
+                    loopback_lat=0.0, limiter_bw=0.0, speed=1e9, model=LV08, crosstraffic=True, n_flows=1000,
+                    seed=1, size_min=1e6, size_max=1e9, tcp_gamma=4194304.0):
+    """A <cluster> (bw / lat / loopback / limiter as in examples/platforms/cluster_*.xml) and its flows."""
+    return PlatformParams(topology, topo_parameters.encode(), bw, lat, policy, loopback_bw, loopback_lat, limiter_bw,
+                          speed, model, int(crosstraffic), n_flows, seed, size_min, size_max, tcp_gamma)
+
 SIGNATURES = {
     # include/lmm/lmm_system.h
     "lmm_set_precision": (None, [D]),
@@ -67,6 +87,8 @@ SIGNATURES = {
     "lmm_check_certificate": (I, [P, D, PD, PI64, PI64]),
     "lmm_gen_maxmin_bench": (I, [P, I, I, PI64, PI64, PI, PI]),
     "lmm_gen_synthetic": (I64, [P, I64, I64, I, U64, I, I, I, I, PI64]),
+    "lmm_platform_size": (I, [ct.POINTER(PlatformParams), PI64, PI64]),
+    "lmm_gen_platform_flows": (I64, [P, ct.POINTER(PlatformParams), PI64, PI64]),
     "lmm_device_count": (I, []),
     "lmm_last_error": (ct.c_char_p, []),
     # include/lmm/lmm_hip.h
@@ -133,6 +155,13 @@ def get_precision():
 
 def device_count():
     return lib().lmm_device_count()
+
+
+def platform_size(p):
+    """(links, hosts) of the cluster `p` describes."""
+    nl, nh = I64(), I64()
+    _check(lib().lmm_platform_size(ct.byref(p), ct.byref(nl), ct.byref(nh)))
+    return nl.value, nh.value
 
 
 class Constraint:
@@ -377,6 +406,17 @@ class System:
         if r < 0:
             raise LmmError(lib().lmm_last_error().decode())
         return vs
+
+    def gen_platform_flows(self, p, want_vars=True):
+        """Links (+ L07 CPUs) and p.n_flows flows of a cluster platform: (constraint ids, variable ids)."""
+        nl, nh = platform_size(p)
+        cs = np.empty(nl + (nh if p.model == L07 else 0), dtype=np.int64)
+        vs = np.empty(p.n_flows, dtype=np.int64) if want_vars else None
+        r = lib().lmm_gen_platform_flows(self.h, ct.byref(p), cs.ctypes.data_as(PI64),
+                                         vs.ctypes.data_as(PI64) if want_vars else None)
+        if r < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return cs, vs
 
     def values_of(self, ids):
         ids = np.ascontiguousarray(ids, dtype=np.int64)

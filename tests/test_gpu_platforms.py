@@ -1,0 +1,45 @@
+"""GPU parity on cluster-platform systems (SURVEY.md §8 f3 and configs C4 / C5 at test scale): flows on
+fat trees and dragonflies (lmm_platforms.hpp) solved by the HIP path, compared with the oracle's solve
+of the same system.  Tolerance as everywhere (tests/lmm_cases.py): |x - x_ref| <= max(1e-9, 1e-6 |x_ref|).
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from simgrid_amd import lmm as L
+from tests.lmm_cases import ABS_TOL, REL_TOL
+
+pytestmark = pytest.mark.gpu
+
+EX_FAT_TREE = dict(topology=L.FAT_TREE, topo_parameters="2;4,4;1,2;1,2", loopback_bw=1e8)
+EX_DRAGONFLY = dict(topology=L.DRAGONFLY, topo_parameters="3,4;4,3;5,1;2", loopback_bw=1e8, limiter_bw=1.5e8)
+BIG_FAT_TREE = dict(topology=L.FAT_TREE, topo_parameters="3;8,8,8;1,8,4;1,1,2", loopback_bw=1e9)
+BIG_DRAGONFLY = dict(topology=L.DRAGONFLY, topo_parameters="4,2;4,2;8,1;4", loopback_bw=1e9, limiter_bw=2e8)
+
+CASES = [
+    ("fat_tree_lv08", EX_FAT_TREE, L.LV08, 0, 2000),
+    ("fat_tree_cm02_shared", dict(EX_FAT_TREE, policy=L.SHARED), L.CM02, 0, 2000),
+    ("fat_tree_l07", EX_FAT_TREE, L.L07, 1, 2000),
+    ("dragonfly_lv08", EX_DRAGONFLY, L.LV08, 0, 3000),
+    ("dragonfly_l07", EX_DRAGONFLY, L.L07, 1, 3000),
+    ("big_fat_tree_lv08", BIG_FAT_TREE, L.LV08, 0, 20000),
+    ("big_dragonfly_l07", BIG_DRAGONFLY, L.L07, 1, 20000),
+    ("big_dragonfly_lv08_no_crosstraffic", dict(BIG_DRAGONFLY, crosstraffic=False), L.LV08, 0, 20000),
+]
+
+
+@pytest.mark.parametrize("name,plat,model,kind,n", CASES, ids=[c[0] for c in CASES])
+def test_platform_flows_match_oracle(name, plat, model, kind, n):
+    s, o = L.System(False, kind), O.System(False, kind)
+    _, vs = s.gen_platform_flows(L.platform_params(model=model, n_flows=n, seed=11, **plat))
+    _, ov = o.gen_platform_flows(O.platform_params(model=model, n_flows=n, seed=11, **plat))
+    s.solve()
+    o.solve()
+    got, want = s.values_of(vs), o.values_of(ov, n)
+    tol = np.maximum(ABS_TOL, REL_TOL * np.abs(want))
+    bad = np.nonzero(np.abs(got - want) > tol)[0]
+    assert len(bad) == 0, (name, len(bad), [(int(i), got[i], want[i]) for i in bad[:5]])
+    assert np.all(want > 0)  # every flow gets a share
+    if kind == 0:
+        excess, infeasible, unbottlenecked = s.check_certificate()
+        assert infeasible == 0 and unbottlenecked == 0, (excess, infeasible, unbottlenecked)
