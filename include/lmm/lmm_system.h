@@ -77,6 +77,12 @@ int lmm_last_stats(lmm_sys* s, int64_t* counts4, double* ms4);
 /* The device context a system solves on (created on the current HIP device on first use);
  * gives access to the lmmhip_* measurement calls (profiling, per-round work profile). */
 struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s);
+/* The device input of this system's next solve (System::flatten_into: the host half of solve(), which
+ * resets the solved variables' values as solve() does).  Call with null arrays to get the sizes
+ * (counts3 = n_var, n_cnst, nnz), then with arrays of those sizes; var_ids maps dense index -> variable
+ * id.  Used by simgrid_amd/multi.py to split a system into connected components across GPUs. */
+int lmm_flat_export(lmm_sys* s, int64_t* counts3, int64_t* var_ptr, int32_t* cnst_idx, double* weight, double* penalty,
+                    double* vbound, double* cbound, uint8_t* cflags, int64_t* var_ids);
 /* Solve n independent systems as one device launch sequence (disjoint union). */
 int lmm_solve_batch(lmm_sys** systems, int n);
 

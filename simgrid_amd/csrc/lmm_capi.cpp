@@ -185,6 +185,38 @@ struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s) {
     return nullptr;
   }
 }
+int lmm_flat_export(lmm_sys* s, int64_t* counts3, int64_t* var_ptr, int32_t* cnst_idx, double* weight, double* penalty,
+                    double* vbound, double* cbound, uint8_t* cflags, int64_t* var_ids) {
+  try {
+    System::Flat f;
+    s->sys.flatten_into(f);
+    const size_t nv = f.dense_vars.size(), nc = f.cbound.size(), nnz = f.cnst_idx.size();
+    counts3[0] = int64_t(nv);
+    counts3[1] = int64_t(nc);
+    counts3[2] = int64_t(nnz);
+    if (var_ptr)
+      std::memcpy(var_ptr, f.var_ptr.data(), (nv + 1) * sizeof(int64_t));
+    if (cnst_idx)
+      std::memcpy(cnst_idx, f.cnst_idx.data(), nnz * sizeof(int32_t));
+    if (weight)
+      std::memcpy(weight, f.weight.data(), nnz * sizeof(double));
+    if (penalty)
+      std::memcpy(penalty, f.penalty.data(), nv * sizeof(double));
+    if (vbound)
+      std::memcpy(vbound, f.vbound.data(), nv * sizeof(double));
+    if (cbound)
+      std::memcpy(cbound, f.cbound.data(), nc * sizeof(double));
+    if (cflags)
+      std::memcpy(cflags, f.cflags.data(), nc);
+    for (size_t i = 0; var_ids && i < nv; i++)
+      var_ids[i] = f.dense_vars[i];
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 int lmm_solve_batch(lmm_sys** systems, int n) {
   try {
     std::vector<System*> v(size_t(n > 0 ? n : 0));

@@ -82,6 +82,7 @@ SIGNATURES = {
     "lmm_device_solve": (I, [P]),
     "lmm_fetch": (I, [P]),
     "lmm_last_stats": (I, [P, PI64, PD]),
+    "lmm_flat_export": (I, [P, PI64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8), PI64]),
     "lmm_solve_batch": (I, [ct.POINTER(P), I]),
     "lmm_system_device_ctx": (P, [P]),
     "lmm_check_certificate": (I, [P, D, PD, PI64, PI64]),

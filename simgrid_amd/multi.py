@@ -1,0 +1,234 @@
+"""Multi-GPU layer: one process per GPU, work split so that no collective sits on
+the solve's data path.
+
+* Independent systems (a parameter sweep, or the batched systems of config C3): contiguous blocks of
+  systems per rank balanced by nnz (`balanced_blocks`); each rank solves its block as one device launch
+  sequence (`lmm.solve_batch`).  Weak scaling, nothing exchanged during the solve.
+* Connected components of one system: the closure System::update_modified_set walks
+  (maxmin.cpp:898-922) splits a system into independent sub-systems.  `components` labels them from the
+  flattened device input (`export_flat`, i.e. lmm_flat_export), `pack_components` bin-packs them on the
+  ranks by nnz, every rank solves its share (`solve_components`), and one all-reduce(SUM) of the disjoint
+  per-rank value vectors assembles the result.  A random C2 system or a fat tree carrying random flows
+  is one giant component: such a system is solved by replicas only.
+* The simulation step's only cross-rank dependency is the next event date,
+  `Model::next_occuring_event` (Model.cpp:40-129): one all-reduce(MIN) of a scalar (`next_event_date`).
+
+Launch as `torchrun --nproc-per-node N` with MASTER_ADDR=127.0.0.1; the same code runs on gloo (CPU
+tests) and nccl (RCCL over xGMI).
+"""
+import ctypes as ct
+import os
+from collections import namedtuple
+
+import numpy as np
+
+from simgrid_amd import lmm
+
+Flat = namedtuple("Flat", "var_ptr cnst_idx weight penalty vbound cbound cflags var_ids")
+
+
+def dist_env():
+    """(rank, world, local_rank) from the torchrun environment (1 process when unset)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+# ---- partitioning -----------------------------------------------------------------------------
+
+def balanced_blocks(weights, parts):
+    """Split items 0..n-1 into `parts` contiguous blocks minimising the heaviest block (binary search
+    on the block capacity, greedy fill).  Returns the parts+1 block boundaries."""
+    w = np.asarray(weights, dtype=np.int64)
+    n = len(w)
+    if parts <= 0:
+        raise ValueError("parts must be positive")
+    pre = np.concatenate([[0], np.cumsum(w)])
+
+    def cut(cap):
+        bounds, lo = [0], 0
+        for _ in range(parts):
+            hi = int(np.searchsorted(pre, pre[lo] + cap, side="right")) - 1
+            hi = max(hi, min(lo + 1, n)) if lo < n else n
+            bounds.append(hi)
+            lo = hi
+        return bounds if bounds[-1] == n else None
+
+    lo, hi = int(w.max(initial=0)), int(pre[-1])
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if cut(mid) is None:
+            lo = mid + 1
+        else:
+            hi = mid
+    return cut(lo)
+
+
+def pack_components(sizes, parts):
+    """Longest-processing-time bin packing: component i -> rank, heaviest first onto the lightest rank."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    owner = np.empty(len(sizes), dtype=np.int64)
+    load = np.zeros(parts, dtype=np.int64)
+    for i in np.argsort(-sizes, kind="stable"):
+        r = int(np.argmin(load))
+        owner[i] = r
+        load[r] += sizes[i]
+    return owner
+
+
+# ---- flattened systems and their components --------------------------------------------------
+
+def export_flat(s):
+    """The device input of System `s`'s next solve (lmm_flat_export)."""
+    L = lmm.lib()
+    cnt = (ct.c_int64 * 3)()
+    if L.lmm_flat_export(s.h, cnt, None, None, None, None, None, None, None, None) != 0:
+        raise lmm.LmmError(L.lmm_last_error().decode())
+    nv, nc, nnz = cnt[0], cnt[1], cnt[2]
+    f = Flat(np.empty(nv + 1, np.int64), np.empty(nnz, np.int32), np.empty(nnz, np.float64),
+             np.empty(nv, np.float64), np.empty(nv, np.float64), np.empty(nc, np.float64), np.empty(nc, np.uint8),
+             np.empty(nv, np.int64))
+
+    def p(a, t):
+        return a.ctypes.data_as(ct.POINTER(t))
+
+    if L.lmm_flat_export(s.h, cnt, p(f.var_ptr, ct.c_int64), p(f.cnst_idx, ct.c_int32), p(f.weight, ct.c_double),
+                         p(f.penalty, ct.c_double), p(f.vbound, ct.c_double), p(f.cbound, ct.c_double),
+                         p(f.cflags, ct.c_uint8), p(f.var_ids, ct.c_int64)) != 0:
+        raise lmm.LmmError(L.lmm_last_error().decode())
+    return f
+
+
+def components(f):
+    """Connected components of the variable-constraint graph: (label per variable, label per
+    constraint, count).  Constraints without an element get labels of their own."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+
+    nv, nc = len(f.penalty), len(f.cbound)
+    rows = np.repeat(np.arange(nv, dtype=np.int64), np.diff(f.var_ptr))
+    g = coo_matrix((np.ones(len(rows), np.int8), (rows, nv + f.cnst_idx.astype(np.int64))),
+                   shape=(nv + nc, nv + nc))
+    n, lab = connected_components(g, directed=False)
+    return lab[:nv], lab[nv:], n
+
+
+def sub_flat(f, var_mask, cnst_mask):
+    """The part of `f` on the selected variables / constraints (a union of whole components),
+    re-indexed densely.  Returns (flat, dense indices of its variables in f)."""
+    vsel = np.nonzero(var_mask)[0]
+    cmap = np.full(len(f.cbound), -1, np.int64)
+    csel = np.nonzero(cnst_mask)[0]
+    cmap[csel] = np.arange(len(csel))
+    lens = np.diff(f.var_ptr)[vsel]
+    eidx = np.concatenate([np.arange(f.var_ptr[v], f.var_ptr[v + 1]) for v in vsel]) if len(vsel) else \
+        np.empty(0, np.int64)
+    ci = cmap[f.cnst_idx[eidx]]
+    if np.any(ci < 0):
+        raise ValueError("selection is not a union of components")
+    out = Flat(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), ci.astype(np.int32), f.weight[eidx],
+               f.penalty[vsel], f.vbound[vsel], f.cbound[csel], f.cflags[csel], f.var_ids[vsel])
+    return out, vsel
+
+
+def device_solve_flat(f, kind, precision=None, device=None):
+    """Solve a flattened system on the current HIP device with the lmmhip_* ABI: dense values."""
+    L = lmm.lib()
+    prec = lmm.get_precision() if precision is None else precision
+    if device is None:
+        import torch
+
+        device = torch.cuda.current_device()
+    ctx = ct.c_void_p()
+    if L.lmmhip_ctx_create(device, ct.byref(ctx)) != 0:
+        raise lmm.LmmError(L.lmmhip_last_error().decode())
+    try:
+        def p(a, t):
+            return a.ctypes.data_as(ct.POINTER(t))
+
+        nv, nc, nnz = len(f.penalty), len(f.cbound), len(f.cnst_idx)
+        if L.lmmhip_upload(ctx, nv, nc, nnz, p(f.var_ptr, ct.c_int64), p(f.cnst_idx, ct.c_int32),
+                           p(f.weight, ct.c_double), p(f.penalty, ct.c_double), p(f.vbound, ct.c_double),
+                           p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8)) != 0 \
+                or L.lmmhip_solve(ctx, kind, prec) != 0:
+            raise lmm.LmmError(L.lmmhip_last_error().decode())
+        x = np.empty(nv, np.float64)
+        if L.lmmhip_get_values(ctx, p(x, ct.c_double)) != 0:
+            raise lmm.LmmError(L.lmmhip_last_error().decode())
+        return x
+    finally:
+        L.lmmhip_ctx_destroy(ctx)
+
+
+# ---- collectives ------------------------------------------------------------------------------
+
+class LocalExchange:
+    """World of one process: the collectives are identities."""
+    rank, world = 0, 1
+
+    def sum(self, x):
+        return x
+
+    def min(self, x):
+        return x
+
+
+class DistExchange:
+    """torch.distributed collectives on numpy data (gloo: CPU tensors, nccl/RCCL: device tensors)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.dist, self.group = dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.device = torch.device("cuda", torch.cuda.current_device()) \
+            if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+    def _reduce(self, x, op):
+        import torch
+
+        t = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64)).to(self.device)
+        self.dist.all_reduce(t, op=op, group=self.group)
+        return t.cpu().numpy()
+
+    def sum(self, x):
+        return self._reduce(x, self.dist.ReduceOp.SUM)
+
+    def min(self, x):
+        return self._reduce(x, self.dist.ReduceOp.MIN)
+
+
+def next_event_date(local_min, exchange):
+    """Model::next_occuring_event across ranks (Model.cpp:40-129): every rank's earliest date, -1 = none."""
+    v = float(local_min) if local_min >= 0 else np.inf
+    m = float(exchange.min(np.array([v]))[0])
+    return -1.0 if m == np.inf else m
+
+
+# ---- sharded solves ---------------------------------------------------------------------------
+
+def solve_components(f, kind, exchange, solve_flat=None):
+    """Solve flattened system `f` (identical on every rank) with its connected components spread over
+    the ranks.  Returns the dense value vector (all ranks get all values).  `solve_flat(sub, kind)`
+    defaults to the device solver."""
+    solve_flat = solve_flat or device_solve_flat
+    var_lab, cnst_lab, n = components(f)
+    nnz = np.bincount(np.repeat(var_lab, np.diff(f.var_ptr)), minlength=n) + np.bincount(var_lab, minlength=n)
+    owner = pack_components(nnz, exchange.world)
+    mine = owner == exchange.rank
+    x = np.zeros(len(f.penalty), np.float64)
+    if np.any(mine[var_lab]):
+        sub, idx = sub_flat(f, mine[var_lab], mine[cnst_lab])
+        x[idx] = solve_flat(sub, kind)
+    return exchange.sum(x)
+
+
+def solve_batch_block(build, n_systems, weights, exchange, solve=None):
+    """Independent systems 0..n-1 spread over ranks in nnz-balanced contiguous blocks; `build(i)`
+    makes system i on this rank.  Returns {i: system} of this rank's block, solved."""
+    bounds = balanced_blocks(weights, exchange.world)
+    lo, hi = bounds[exchange.rank], bounds[exchange.rank + 1]
+    mine = {i: build(i) for i in range(lo, hi)}
+    if mine:
+        (solve or lmm.solve_batch)(list(mine.values()))
+    return mine

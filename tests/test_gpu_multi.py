@@ -1,0 +1,26 @@
+"""Component-sharded solve on the device (simgrid_amd/multi.py): every component of a multi-component
+system solved through the lmmhip_* ABI on its own context, compared with the oracle's solve of the
+whole system.  One process (LocalExchange); the cross-rank path is covered on gloo in test_multi.py."""
+import numpy as np
+import pytest
+
+from simgrid_amd import multi as M
+from tests.lmm_cases import ABS_TOL, REL_TOL
+from tests.test_multi import build_pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_device_component_sharded_solve(kind):
+    s, o, ovars = build_pair(kind)
+    f = M.export_flat(s)
+    for world in (1, 3):  # pretend to be every rank of a 3-rank job in turn
+        x = np.zeros(len(f.penalty))
+        for rank in range(world):
+            ex = M.LocalExchange()
+            ex.rank, ex.world = rank, world
+            x += M.solve_components(f, kind, ex)
+        o.solve()
+        want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+        assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want))), world
