@@ -92,6 +92,26 @@ int lmmhip_round_profile(lmmhip_ctx* ctx, int64_t* alive_vars, int64_t* alive_el
  * elements.  Returns the number of rounds. */
 int lmmhip_vote_profile(lmmhip_ctx* ctx, int64_t* reeval_vars, int64_t* reeval_elems, int cap);
 
+/* Launch on `hip_stream` (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream) instead of the
+ * context's own stream; null restores the own stream.  Lets a caller order its collectives and the
+ * solver's kernels on one stream without host synchronisation. */
+int lmmhip_ctx_set_stream(lmmhip_ctx* ctx, void* hip_stream);
+
+/* FairBottleneck with the variables sharded over ranks (simgrid_amd/multi.py).  The
+ * context holds this rank's variables and EVERY constraint (constraint indices are global).  A round
+ * (fair_bottleneck.cpp:59-145) is three phases; between them the caller all-reduces the exchange
+ * buffers over the ranks, on the context's stream:
+ *   step(0) -> xnb[0..n_cnst) listed variables per constraint, xnb[n_cnst] variables still listed;
+ *              all-reduce SUM xnb
+ *   step(1) -> shares, increments; xsum = sum of w*mu per shared constraint, xmin = min of w*mu per
+ *              FATPIPE constraint; all-reduce SUM xsum, MIN xmin
+ *   step(2) -> remaining, erasure and delisting (identical decisions on every rank)
+ * xnb (int32[n_cnst+1]), xsum, xmin (double[n_cnst]) are device buffers owned by the caller.  The
+ * solve is over when poll() reports done (the same round on every rank: it is decided from xnb). */
+int lmmhip_fb_shard_begin(lmmhip_ctx* ctx, double precision, int32_t* xnb, double* xsum, double* xmin);
+int lmmhip_fb_shard_step(lmmhip_ctx* ctx, int phase);
+int lmmhip_fb_shard_poll(lmmhip_ctx* ctx, int* done, int64_t* rounds); /* synchronises the stream */
+
 /* Number of visible HIP devices (0 when none; never initialises a context). */
 int lmmhip_device_count(void);
 

@@ -90,6 +90,17 @@ struct Dev {
   int32_t* rtgt[3];  // per row: constraint the variable votes for; kUnvoted / kRetired
   uint16_t* skey[3];  // per row: min key over the row's OTHER constraints at its last vote (0 if bounded)
   int32_t* bsum;    // compaction scratch: per-block rows / elems (2 x blocks)
+  // fair bottleneck: CSC chunks (lmm_fb_kernels.hpp) and the per-constraint exchange buffers
+  int32_t nch;               // number of chunks
+  const int32_t* ch_cnst;    // [nch] constraint of each chunk
+  const uint32_t* ch_beg;    // [nch] first CSC element of each chunk
+  const int32_t* c_ch;       // [nC+1] first chunk of each constraint
+  int32_t* pcnt;             // [nch] listed variables per chunk
+  double* pacc;              // [nch] sum / min of w*mu per chunk
+  uint8_t* erased;           // [nC] erased in the current round
+  int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag), all-reduce SUM
+  double* xsum;              // [nC] sum of w*mu per shared constraint, all-reduce SUM
+  double* xmin;              // [nC] min of w*mu per FATPIPE constraint, all-reduce MIN
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };

@@ -1,8 +1,24 @@
 // lmm_fb_kernels.hpp — FairBottleneck::bottleneck_solve on gfx950 (included by lmm_hip.hip).
+//
+// One reference round (fair_bottleneck.cpp:59-145) is Jacobi-style: every constraint's share is
+// computed before any variable moves, every variable's increment before any constraint is updated.
+// The device round is the same three phases; the two per-constraint reductions between them go
+// through exchange buffers so that a variable-sharded solve (multi.py) can all-reduce
+// them across ranks between the phases:
+//   phase 0  fbk_count, fbk_nb      listed-variable count per constraint          -> xnb  (SUM)
+//   phase 1  fbk_share, fb_var_inc, fbk_acc, fbk_accc
+//                                   shares, increments, sum / min of w*mu          -> xsum (SUM), xmin (MIN)
+//   phase 2  fbk_update, fbk_unlist remaining, erasure, delisting
+// Element work is cut into CSC chunks of at most kFbChunk elements (one wave each), so a constraint
+// with 10^6 elements (a CPU under thousands of flows, C5) spreads over the chip instead of
+// serialising one wave; per-chunk partials are combined per constraint in chunk order, so every
+// reduction is deterministic.
 #pragma once
 #include "lmm_dev.hpp"
 
 namespace lmmdev {
+
+constexpr int kFbChunk = 1024;
 
 __global__ void __launch_bounds__(kBlock) fb_init(Dev s) {
   const int64_t n = s.nV > s.nC ? s.nV : s.nC;
@@ -17,43 +33,76 @@ __global__ void __launch_bounds__(kBlock) fb_init(Dev s) {
       s.rem[i] = s.cbound[i];
       s.use[i] = 0.0;
       s.ratio[i] = 0.0;  // 0 = in the constraint list, +inf = erased
+      s.erased[i] = 0;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_ANY0] = s.nV > 0;
 }
 
-// :65-87 — usage = remaining / (number of listed variables with w > 0), FATPIPE -> 1.
-__global__ void __launch_bounds__(kBlock) fb_cnst_share(Dev s, int par) {
+__device__ __forceinline__ uint32_t chunk_end(const Dev& s, int q, int c) {
+  const uint32_t e = s.ch_beg[q] + kFbChunk, ce = s.cnst_ptr[c + 1];
+  return e < ce ? e : ce;
+}
+
+// :67-74 — listed variables (w > 0: every flattened element) of each chunk of a listed constraint
+__global__ void __launch_bounds__(kBlock) fbk_count(Dev s) {
   if (s.ctl[CTL_DONE])
     return;
-  if (!s.ctl[CTL_ANY0 + par]) {
-    s.ctl[CTL_DONE] = 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wpb = kBlock / kWave;
+  for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < s.nch; q += gridDim.x * wpb) {
+    const int c = s.ch_cnst[q];
+    int nb = 0;
+    if (s.ratio[c] == 0.0)
+      for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave)
+        nb += s.vst[s.csc_v[j]];
+    nb = grp_isum<kWave>(nb);
+    if (lane == 0)
+      s.pcnt[q] = nb;
+  }
+}
+
+// per constraint: chunk counts -> xnb[c]; xnb[nC] = "a variable of this shard is still listed"
+__global__ void __launch_bounds__(kBlock) fbk_nb(Dev s, int par) {
+  if (s.ctl[CTL_DONE])
+    return;
+  for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
+    int nb = 0;
+    for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
+      nb += s.pcnt[q];
+    s.xnb[c] = nb;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.xnb[s.nC] = s.ctl[CTL_ANY0 + par];
+}
+
+// :65-87 — usage = remaining / nb (FATPIPE: nb -> 1); nb == 0 erases the constraint.  xnb holds the
+// counts of every shard; xnb[nC] == 0 means no variable is listed anywhere: the solve is over (:145).
+__global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (s.xnb[s.nC] == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      s.ctl[CTL_DONE] = 1;
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
     s.ctl[CTL_ROUNDS] += 1;
   }
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wpb = kBlock / kWave;
-  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
+  for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
     if (s.ratio[c] != 0.0)
       continue;
-    int nb = 0;
-    for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave)
-      nb += s.vst[s.csc_v[j]];
-    nb = grp_isum<kWave>(nb);
-    if (lane == 0) {
-      if (nb > 0 && (s.cflags[c] & 1))
-        nb = 1;
-      if (nb == 0) {
-        s.rem[c] = 0.0;
-        s.use[c] = 0.0;
-        s.ratio[c] = dinf();
-      } else {
-        s.use[c] = s.rem[c] / nb;
-      }
+    int nb = s.xnb[c];
+    if (nb > 0 && (s.cflags[c] & 1))
+      nb = 1;
+    if (nb == 0) {
+      s.rem[c] = 0.0;
+      s.use[c] = 0.0;
+      s.ratio[c] = dinf();
+    } else {
+      s.use[c] = s.rem[c] / nb;
     }
   }
 }
@@ -83,51 +132,95 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
       any = 1;
     s.fixr[v] = round;  // last round in which v was listed
   }
-  if (any)
+  if (__any(any) && (threadIdx.x & (kWave - 1)) == 0)
     s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
 }
 
-// :107-144 — remaining -= sum w*mu over ALL enabled elements (stale mu of variables that already
-// left the list included), FATPIPE: remaining -= min(usage, min w*mu); remaining <= 0 erases the
-// constraint and every listed variable on it.
-__global__ void __launch_bounds__(kBlock) fb_cnst_update(Dev s, double prec) {
+// :107-127 — per chunk of a listed constraint: sum (or FATPIPE: min) of w*mu over ALL its elements
+// (the stale mu of variables that already left the list included)
+__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
   if (s.ctl[CTL_DONE])
     return;
   const int lane = threadIdx.x & (kWave - 1);
   const int wpb = kBlock / kWave;
-  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
+  for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < s.nch; q += gridDim.x * wpb) {
+    const int c = s.ch_cnst[q];
     if (s.ratio[c] != 0.0)
       continue;
-    const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
     const bool fat = s.cflags[c] & 1;
     double acc = fat ? dinf() : 0.0;
-    for (uint32_t j = b + lane; j < e; j += kWave) {
+    for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave) {
       const double d = s.csc_w[j] * s.vtmp[s.csc_v[j]];
       acc = fat ? fmin(acc, d) : acc + d;
     }
     acc = fat ? wave_min(acc) : wave_sum(acc);
+    if (lane == 0)
+      s.pacc[q] = acc;
+  }
+}
+
+// per constraint: chunk partials in chunk order -> xsum (shared) / xmin (FATPIPE); the other one
+// gets the neutral element of its all-reduce
+__global__ void __launch_bounds__(kBlock) fbk_accc(Dev s) {
+  if (s.ctl[CTL_DONE])
+    return;
+  for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
+    double sum = 0.0, mn = dinf();
+    if (s.ratio[c] == 0.0) {
+      if (s.cflags[c] & 1)
+        for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
+          mn = fmin(mn, s.pacc[q]);
+      else
+        for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
+          sum += s.pacc[q];
+    }
+    s.xsum[c] = sum;
+    s.xmin[c] = mn;
+  }
+}
+
+// :110-140 — remaining -= sum w*mu (FATPIPE: remaining -= min(usage, min w*mu)), clamped at the
+// precision; remaining <= 0 erases the constraint.  Same inputs on every shard, same decision.
+__global__ void __launch_bounds__(kBlock) fbk_update(Dev s, double prec) {
+  if (s.ctl[CTL_DONE])
+    return;
+  for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
+    s.erased[c] = 0;
+    if (s.ratio[c] != 0.0)
+      continue;
     double rem = s.rem[c];
-    if (!fat) {
-      rem -= acc;
-    } else {
+    if (s.cflags[c] & 1) {
       double u = s.use[c];
       if (s.cflags[c] & 2)
         u = fmin(u, 0.0);
-      u = fmin(u, acc);
+      u = fmin(u, s.xmin[c]);
       s.use[c] = u;
       rem -= u;
+    } else {
+      rem -= s.xsum[c];
     }
     if (rem < prec)
       rem = 0.0;
-    const bool erase = rem <= 0.0;
-    if (lane == 0) {
-      s.rem[c] = rem;
-      if (erase)
-        s.ratio[c] = dinf();
+    s.rem[c] = rem;
+    if (rem <= 0.0) {
+      s.ratio[c] = dinf();
+      s.erased[c] = 1;
     }
-    if (erase)
-      for (uint32_t j = b + lane; j < e; j += kWave)
-        s.vst[s.csc_v[j]] = 0;
+  }
+}
+
+// :132-139 — the listed variables of an erased constraint leave the list
+__global__ void __launch_bounds__(kBlock) fbk_unlist(Dev s) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wpb = kBlock / kWave;
+  for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < s.nch; q += gridDim.x * wpb) {
+    const int c = s.ch_cnst[q];
+    if (!s.erased[c])
+      continue;
+    for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave)
+      s.vst[s.csc_v[j]] = 0;
   }
 }
 

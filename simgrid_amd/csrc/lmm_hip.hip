@@ -41,7 +41,8 @@ int fail(int code, const std::string& msg) {
 // =============================================================================================
 struct lmmhip_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // the stream every launch and copy goes to
+  hipStream_t own_stream = nullptr;  // the context's own stream (lmmhip_ctx_set_stream(nullptr))
   Dev d{};
   std::vector<void*> allocs;  // owned device allocations
   int32_t* h_ctl = nullptr;   // pinned mirror of the control words
@@ -59,6 +60,12 @@ struct lmmhip_ctx {
   lmmhip_stats stats{};
   int last_kind = LMMHIP_KIND_MAXMIN;
   int32_t* vstat = nullptr;  // profiling counters of mm_vote ([round][block] x 2)
+  // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
+  int64_t fb_round = 0;
+  double fb_prec = 0;
+  bool fb_shard = false;
+  int32_t* xnb_own = nullptr;  // the context's own exchange buffers (unsharded solves)
+  double *xsum_own = nullptr, *xmin_own = nullptr;
 };
 
 static void free_all(lmmhip_ctx* c) {
@@ -67,6 +74,9 @@ static void free_all(lmmhip_ctx* c) {
   c->allocs.clear();
   c->d = Dev{};
   c->uploaded = false;
+  c->xnb_own = nullptr;
+  c->xsum_own = c->xmin_own = nullptr;
+  c->fb_shard = false;
 }
 
 template <class T> static int dalloc(lmmhip_ctx* c, T** out, int64_t n) {
@@ -108,7 +118,8 @@ int lmmhip_ctx_create(int device, lmmhip_ctx** out) {
   if (e == hipSuccess)
     e = hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e == hipSuccess)
-    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  c->stream = c->own_stream;
   if (e == hipSuccess)
     e = hipHostMalloc((void**)&c->h_ctl, CTL_WORDS * sizeof(int32_t), hipHostMallocDefault);
   if (e == hipSuccess)
@@ -129,6 +140,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream)
     (void)hipStreamSynchronize(c->stream);
+  if (c->own_stream && c->own_stream != c->stream)
+    (void)hipStreamSynchronize(c->own_stream);
   free_all(c);
   if (c->h_ctl)
     (void)hipHostFree(c->h_ctl);
@@ -140,8 +153,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipEventDestroy(c->ev1);
   for (hipEvent_t ev : c->pool)
     (void)hipEventDestroy(ev);
-  if (c->stream)
-    (void)hipStreamDestroy(c->stream);
+  if (c->own_stream)
+    (void)hipStreamDestroy(c->own_stream);
   delete c;
   return 0;
 }
@@ -193,6 +206,18 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
         cw[pos] = weight[j];
       }
   }
+  // fair bottleneck CSC chunks (lmm_fb_kernels.hpp)
+  std::vector<int32_t> c_ch(static_cast<size_t>(nC) + 1, 0), ch_cnst;
+  std::vector<uint32_t> ch_beg;
+  for (int64_t k = 0; k < nC; k++) {
+    c_ch[size_t(k)] = int32_t(ch_cnst.size());
+    for (uint32_t b = cptr[size_t(k)]; b < cptr[size_t(k) + 1]; b += kFbChunk) {
+      ch_cnst.push_back(int32_t(k));
+      ch_beg.push_back(b);
+    }
+  }
+  const int64_t nch = int64_t(ch_cnst.size());
+  c_ch[size_t(nC)] = int32_t(nch);
   std::vector<int32_t> iota(static_cast<size_t>(nV));
   for (int64_t v = 0; v < nV; v++)
     iota[size_t(v)] = int32_t(v);
@@ -251,6 +276,17 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &d.clist[1], nC);
   rc |= dalloc(c, &d.bsum, 2 * nblk);
   rc |= dalloc(c, &d.ctl, CTL_WORDS);
+  int32_t *chc, *cch;
+  uint32_t* chb;
+  rc |= dalloc(c, &chc, nch);
+  rc |= dalloc(c, &chb, nch);
+  rc |= dalloc(c, &cch, nC + 1);
+  rc |= dalloc(c, &d.pcnt, nch);
+  rc |= dalloc(c, &d.pacc, nch);
+  rc |= dalloc(c, &d.erased, nC);
+  rc |= dalloc(c, &c->xnb_own, nC + 1);
+  rc |= dalloc(c, &c->xsum_own, nC);
+  rc |= dalloc(c, &c->xmin_own, nC);
   if (rc) {
     free_all(c);
     return LMMHIP_E_HIP;
@@ -272,7 +308,19 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
     HIPCHK(hipMemcpyAsync(cb, cnst_bound, sizeof(double) * nC, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(cf, cnst_flags, sizeof(uint8_t) * nC, hipMemcpyHostToDevice, c->stream));
   }
+  if (nch > 0) {
+    HIPCHK(hipMemcpyAsync(chc, ch_cnst.data(), sizeof(int32_t) * nch, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(chb, ch_beg.data(), sizeof(uint32_t) * nch, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipMemcpyAsync(cch, c_ch.data(), sizeof(int32_t) * (nC + 1), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));  // host staging vectors die at return
+  d.nch = int32_t(nch);
+  d.ch_cnst = chc;
+  d.ch_beg = chb;
+  d.c_ch = cch;
+  d.xnb = c->xnb_own;
+  d.xsum = c->xsum_own;
+  d.xmin = c->xmin_own;
   d.var_ptr = vp;
   d.csr_c = csr_c;
   d.csr_w = csr_w;
@@ -513,33 +561,118 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   return 0;
 }
 
-static int solve_fair(lmmhip_ctx* c, double prec) {
+static int fb_begin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
-  const int gC4 = grid_for(d.nC, kBlock / kWave);
-  const int gVC = grid_for(std::max(d.nV, d.nC), kBlock);
+  c->fb_round = 0;
+  c->fb_prec = prec;
+  LAUNCH(0, -1, fb_init, grid_for(std::max(d.nV, d.nC), kBlock), kBlock, d);
+  return 0;
+}
+
+// One phase of a fair-bottleneck round (lmm_fb_kernels.hpp); phase 2 ends the round.
+static int fb_phase(lmmhip_ctx* c, int phase) {
+  Dev& d = c->d;
+  const int64_t r = c->fb_round;
+  const int par = int(r & 1);
+  const int gQ = grid_for(d.nch, kBlock / kWave);
+  const int gC = grid_for(d.nC, kBlock);
   const int gV = grid_for(d.nV, kBlock);
-  LAUNCH(0, -1, fb_init, gVC, kBlock, d);
+  switch (phase) {
+  case 0:
+    LAUNCH(2, r, fbk_count, gQ, kBlock, d);
+    LAUNCH(2, r, fbk_nb, gC, kBlock, d, par);
+    break;
+  case 1:
+    LAUNCH(3, r, fbk_share, gC, kBlock, d, par);
+    LAUNCH(3, r, fb_var_inc, gV, kBlock, d, par, int(r));
+    LAUNCH(4, r, fbk_acc, gQ, kBlock, d);
+    LAUNCH(4, r, fbk_accc, gC, kBlock, d);
+    break;
+  case 2:
+    LAUNCH(5, r, fbk_update, gC, kBlock, d, c->fb_prec);
+    LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
+    c->fb_round++;
+    break;
+  default:
+    return fail(LMMHIP_E_ARG, "fair-bottleneck phase must be 0, 1 or 2");
+  }
+  return 0;
+}
+
+static int solve_fair(lmmhip_ctx* c, double prec) {
+  c->fb_shard = false;
+  c->d.xnb = c->xnb_own;
+  c->d.xsum = c->xsum_own;
+  c->d.xmin = c->xmin_own;
+  if (int rc = fb_begin(c, prec))
+    return rc;
   // The reference's rounds are not bounded by the system size (FATPIPE remaining can shrink
   // geometrically: millions of rounds on 60-variable systems); give up past this budget.
-  const int64_t max_rounds = 64 * (int64_t(d.nV) + int64_t(d.nC)) + 4096;
-  int64_t r = 0;
+  const int64_t max_rounds = 64 * (int64_t(c->d.nV) + int64_t(c->d.nC)) + 4096;
   int chunk = 4;
   for (;;) {
-    for (int k = 0; k < chunk; k++, r++) {
-      const int par = int(r & 1);
-      LAUNCH(2, r, fb_cnst_share, gC4, kBlock, d, par);
-      LAUNCH(3, r, fb_var_inc, gV, kBlock, d, par, int(r));
-      LAUNCH(4, r, fb_cnst_update, gC4, kBlock, d, prec);
-    }
+    for (int k = 0; k < chunk; k++)
+      for (int ph = 0; ph < 3; ph++)
+        if (int rc = fb_phase(c, ph))
+          return rc;
     if (int rc = poll_ctl(c))
       return rc;
     if (c->h_ctl[CTL_DONE])
       break;
-    if (r > max_rounds)
+    if (c->fb_round > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "fair-bottleneck round guard tripped");
     if (chunk < 64)
       chunk *= 2;
   }
+  return 0;
+}
+
+int lmmhip_ctx_set_stream(lmmhip_ctx* c, void* stream) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->stream = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+  return 0;
+}
+
+int lmmhip_fb_shard_begin(lmmhip_ctx* c, double precision, int32_t* xnb, double* xsum, double* xmin) {
+  if (!c || !c->uploaded)
+    return fail(LMMHIP_E_STATE, "no system uploaded");
+  if (!xnb || !xsum || !xmin)
+    return fail(LMMHIP_E_ARG, "null exchange buffer");
+  HIPCHK(hipSetDevice(c->device));
+  c->pool_used = 0;
+  c->launch_slot.clear();
+  c->launch_round.clear();
+  c->launch_ms.clear();
+  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+  c->d.xnb = xnb;
+  c->d.xsum = xsum;
+  c->d.xmin = xmin;
+  c->fb_shard = true;
+  c->last_kind = LMMHIP_KIND_FAIR_BOTTLENECK;
+  return fb_begin(c, precision);
+}
+
+int lmmhip_fb_shard_step(lmmhip_ctx* c, int phase) {
+  if (!c || !c->fb_shard)
+    return fail(LMMHIP_E_STATE, "lmmhip_fb_shard_begin first");
+  HIPCHK(hipSetDevice(c->device));
+  return fb_phase(c, phase);
+}
+
+int lmmhip_fb_shard_poll(lmmhip_ctx* c, int* done, int64_t* rounds) {
+  if (!c || !c->fb_shard)
+    return fail(LMMHIP_E_STATE, "lmmhip_fb_shard_begin first");
+  HIPCHK(hipSetDevice(c->device));
+  if (int rc = poll_ctl(c))
+    return rc;
+  if (done)
+    *done = c->h_ctl[CTL_DONE];
+  if (rounds)
+    *rounds = c->h_ctl[CTL_ROUNDS];
+  c->stats.rounds = c->h_ctl[CTL_ROUNDS];
   return 0;
 }
 

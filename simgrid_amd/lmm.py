@@ -106,6 +106,10 @@ SIGNATURES = {
     "lmmhip_launch_profile": (I, [P, PI, PI, ct.POINTER(ct.c_float), I]),
     "lmmhip_round_profile": (I, [P, PI64, PI64, I]),
     "lmmhip_vote_profile": (I, [P, PI64, PI64, I]),
+    "lmmhip_ctx_set_stream": (I, [P, P]),
+    "lmmhip_fb_shard_begin": (I, [P, D, P, P, P]),
+    "lmmhip_fb_shard_step": (I, [P, I]),
+    "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
     "lmmhip_device_count": (I, []),
     "lmmhip_last_error": (ct.c_char_p, []),
 }

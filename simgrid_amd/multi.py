@@ -10,6 +10,11 @@ the solve's data path.
   ranks by nnz, every rank solves its share (`solve_components`), and one all-reduce(SUM) of the disjoint
   per-rank value vectors assembles the result.  A random C2 system or a fat tree carrying random flows
   is one giant component: such a system is solved by replicas only.
+* FairBottleneck sharded by variables (config C5: one system, one exchange per phase): each rank holds
+  an nnz-balanced block of the variables and every constraint; a round's two per-constraint reductions
+  (listed counts; sum / min of w*mu, fair_bottleneck.cpp:65-127) are all-reduced between the phases
+  (`fb_solve_sharded`, device side: lmmhip_fb_shard_*).  Every rank takes the same erase decisions
+  from the same reduced values, so the round count is global.
 * The simulation step's only cross-rank dependency is the next event date,
   `Model::next_occuring_event` (Model.cpp:40-129): one all-reduce(MIN) of a scalar (`next_event_date`).
 
@@ -120,12 +125,12 @@ def sub_flat(f, var_mask, cnst_mask):
     csel = np.nonzero(cnst_mask)[0]
     cmap[csel] = np.arange(len(csel))
     lens = np.diff(f.var_ptr)[vsel]
-    eidx = np.concatenate([np.arange(f.var_ptr[v], f.var_ptr[v + 1]) for v in vsel]) if len(vsel) else \
-        np.empty(0, np.int64)
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    eidx = np.arange(int(ptr[-1]), dtype=np.int64) + np.repeat(f.var_ptr[vsel] - ptr[:-1], lens)
     ci = cmap[f.cnst_idx[eidx]]
     if np.any(ci < 0):
         raise ValueError("selection is not a union of components")
-    out = Flat(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), ci.astype(np.int32), f.weight[eidx],
+    out = Flat(ptr, ci.astype(np.int32), f.weight[eidx],
                f.penalty[vsel], f.vbound[vsel], f.cbound[csel], f.cflags[csel], f.var_ids[vsel])
     return out, vsel
 
@@ -171,6 +176,9 @@ class LocalExchange:
     def min(self, x):
         return x
 
+    def allreduce_(self, buf, op):
+        pass
+
 
 class DistExchange:
     """torch.distributed collectives on numpy data (gloo: CPU tensors, nccl/RCCL: device tensors)."""
@@ -196,6 +204,18 @@ class DistExchange:
 
     def min(self, x):
         return self._reduce(x, self.dist.ReduceOp.MIN)
+
+    def allreduce_(self, buf, op):
+        """In place on a torch tensor (on this backend's device) or a numpy array; op "sum" / "min"."""
+        import torch
+
+        rop = self.dist.ReduceOp.SUM if op == "sum" else self.dist.ReduceOp.MIN
+        if isinstance(buf, torch.Tensor) and buf.device.type == self.device.type:
+            self.dist.all_reduce(buf, op=rop, group=self.group)
+        else:
+            t = torch.as_tensor(np.asarray(buf)).to(self.device)
+            self.dist.all_reduce(t, op=rop, group=self.group)
+            buf[...] = t.cpu().numpy() if not isinstance(buf, torch.Tensor) else t.to(buf.device)
 
 
 def next_event_date(local_min, exchange):
@@ -232,3 +252,114 @@ def solve_batch_block(build, n_systems, weights, exchange, solve=None):
     if mine:
         (solve or lmm.solve_batch)(list(mine.values()))
     return mine
+
+
+class DeviceFbShard:
+    """One rank's part of a variable-sharded FairBottleneck solve on the current HIP device: its block
+    of variables and every constraint, the three phases of lmmhip_fb_shard_step, and the exchange
+    buffers as torch tensors on the device (so RCCL all-reduces them in place, stream-ordered with the
+    solver's kernels: the context launches on torch's current stream)."""
+
+    def __init__(self, f, precision=None):
+        import torch
+
+        L = lmm.lib()
+        self.L, self.n = L, len(f.penalty)
+        self.ctx = ct.c_void_p()
+        if L.lmmhip_ctx_create(torch.cuda.current_device(), ct.byref(self.ctx)) != 0:
+            raise lmm.LmmError(L.lmmhip_last_error().decode())
+
+        def p(a, t):
+            return a.ctypes.data_as(ct.POINTER(t))
+
+        nc = len(f.cbound)
+        self._check(L.lmmhip_ctx_set_stream(self.ctx, ct.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        self._check(L.lmmhip_upload(self.ctx, self.n, nc, len(f.cnst_idx), p(f.var_ptr, ct.c_int64),
+                                    p(f.cnst_idx, ct.c_int32), p(f.weight, ct.c_double), p(f.penalty, ct.c_double),
+                                    p(f.vbound, ct.c_double), p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8)))
+        self.xnb = torch.zeros(nc + 1, dtype=torch.int32, device="cuda")
+        self.xsum = torch.zeros(nc, dtype=torch.float64, device="cuda")
+        self.xmin = torch.zeros(nc, dtype=torch.float64, device="cuda")
+        prec = lmm.get_precision() if precision is None else precision
+        self._check(L.lmmhip_fb_shard_begin(self.ctx, prec, ct.c_void_p(self.xnb.data_ptr()),
+                                            ct.c_void_p(self.xsum.data_ptr()), ct.c_void_p(self.xmin.data_ptr())))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise lmm.LmmError(self.L.lmmhip_last_error().decode())
+
+    def step(self, phase):
+        self._check(self.L.lmmhip_fb_shard_step(self.ctx, phase))
+
+    def buffers(self, phase):
+        return [(self.xnb, "sum")] if phase == 0 else [(self.xsum, "sum"), (self.xmin, "min")]
+
+    def poll(self):
+        done, rounds = ct.c_int(), ct.c_int64()
+        self._check(self.L.lmmhip_fb_shard_poll(self.ctx, ct.byref(done), ct.byref(rounds)))
+        return bool(done.value), rounds.value
+
+    def values(self):
+        x = np.empty(self.n, np.float64)
+        self._check(self.L.lmmhip_get_values(self.ctx, x.ctypes.data_as(ct.POINTER(ct.c_double))))
+        return x
+
+    def close(self):
+        if self.ctx:
+            self.L.lmmhip_ctx_destroy(self.ctx)
+            self.ctx = None
+
+
+def shard_variables(f, parts):
+    """Contiguous nnz-balanced variable blocks of flat `f`, every constraint kept in each: the per-rank
+    inputs of a variable-sharded FairBottleneck solve.  Returns [(flat, dense indices)]."""
+    bounds = balanced_blocks(np.diff(f.var_ptr) + 1, parts)
+    out = []
+    nv = len(f.penalty)
+    for lo, hi in zip(bounds, bounds[1:]):
+        mask = np.zeros(nv, bool)
+        mask[lo:hi] = True
+        out.append(sub_flat(f, mask, np.ones(len(f.cbound), bool)))
+    return out
+
+
+def _reduce_local(shards, phase):
+    """Combine the exchange buffers of the shards living in this process (same order every round)."""
+    if len(shards) < 2:
+        return
+    for i, (buf, op) in enumerate(shards[0].buffers(phase)):
+        acc = buf.clone() if hasattr(buf, "clone") else buf.copy()
+        for sh in shards[1:]:
+            other = sh.buffers(phase)[i][0]
+            acc = acc + other if op == "sum" else (acc.minimum(other) if hasattr(acc, "minimum")
+                                                   else np.minimum(acc, other))
+        for sh in shards:
+            sh.buffers(phase)[i][0][...] = acc
+
+
+def fb_solve_sharded(shards, exchange, n_var_total, n_cnst, poll_every=16):
+    """Drive the three-phase FairBottleneck rounds of `shards` (this process's shards: usually one per
+    rank) with the exchange buffers reduced over the local shards, then over the ranks.  Returns the
+    round count.  All ranks stop in the same round: `done` comes from the reduced counts, and the stop
+    decision itself is all-reduced."""
+    max_rounds = 64 * (n_var_total + n_cnst) + 4096
+    rounds = 0
+    while True:
+        for _ in range(poll_every):
+            for phase in (0, 1, 2):
+                for sh in shards:
+                    sh.step(phase)
+                if phase < 2:
+                    _reduce_local(shards, phase)
+                    for buf, op in shards[0].buffers(phase):
+                        exchange.allreduce_(buf, op)
+                    for sh in shards[1:]:
+                        for (b0, _), (b, _) in zip(shards[0].buffers(phase), sh.buffers(phase)):
+                            b[...] = b0
+            rounds += 1
+        states = [sh.poll() for sh in shards]
+        done = float(all(d for d, _ in states))
+        if exchange.min(np.array([done]))[0] == 1.0:
+            return max(r for _, r in states)
+        if rounds > max_rounds:
+            raise lmm.LmmError("fair-bottleneck round guard tripped")

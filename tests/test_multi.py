@@ -139,3 +139,66 @@ def test_batch_block_partition():
         mine = M.solve_batch_block(build, 5, weights, ex, solve=lambda systems: [o.solve() for o in systems])
         got.update({i: rank for i in mine})
     assert sorted(got) == list(range(5)) and set(got.values()) == {0, 1}
+
+
+# ---- variable-sharded FairBottleneck ----------------------------------------------------------
+
+def fb_pair(seed=4):
+    """A FairBottleneck system: L07 flows on the example dragonfly (FATPIPE loopbacks included)."""
+    s, o = L.System(False, 1), O.System(False, 1)
+    p = dict(topology=L.DRAGONFLY, topo_parameters="3,4;4,3;5,1;2", loopback_bw=1e8, limiter_bw=1.5e8,
+             model=L.L07, n_flows=400, seed=seed)
+    s.gen_platform_flows(L.platform_params(**p))
+    _, ov = o.gen_platform_flows(O.platform_params(**p))
+    return s, o, [O.Variable(o, ov[i]) for i in range(400)]
+
+
+def sharded_fb_values(f, exchange, local_parts, shard_cls):
+    parts = M.shard_variables(f, exchange.world * local_parts)
+    mine = parts[exchange.rank * local_parts:(exchange.rank + 1) * local_parts]
+    shards = [shard_cls(sub) for sub, _ in mine]
+    M.fb_solve_sharded(shards, exchange, len(f.penalty), len(f.cbound))
+    x = np.zeros(len(f.penalty))
+    for sh, (_, idx) in zip(shards, mine):
+        x[idx] = sh.values()
+    return exchange.sum(x)
+
+
+def numpy_shard(sub):
+    from tests.fb_shard_model import NumpyFbShard
+
+    return NumpyFbShard(sub, L.get_precision())
+
+
+@pytest.mark.parametrize("local_parts", [1, 3])
+def test_fb_sharded_single_process(local_parts):
+    s, o, ovars = fb_pair()
+    f = M.export_flat(s)
+    x = sharded_fb_values(f, M.LocalExchange(), local_parts, numpy_shard)
+    o.solve()
+    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+    assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want)))
+
+
+def _fb_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        s, _, _ = fb_pair()
+        f = M.export_flat(s)
+        x = sharded_fb_values(f, M.DistExchange(), 2, numpy_shard)
+        np.save(os.path.join(out_dir, f"fb{rank}.npy"), x)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_fb_sharded(tmp_path):
+    mp.spawn(_fb_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    s, o, ovars = fb_pair()
+    f = M.export_flat(s)
+    o.solve()
+    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+    for r in range(2):
+        x = np.load(tmp_path / f"fb{r}.npy")
+        assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want)))
