@@ -71,7 +71,12 @@ def main():
     ap.add_argument("--cpu-sample-div", type=int, default=10, help="CPU baseline sample = 1/div of the workload")
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON, help="per-kernel HBM bytes from a rocprofv3 --pmc pass")
     ap.add_argument("--profile-json", default=None, help="write the per-launch profile here")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="c2 = the BASELINE metric's config (default); c3/c4/c5 = the other SURVEY.md §8(d) configs")
+    ap.add_argument("--flows", type=int, default=None, help="c4/c5: number of flows (default 1e5 / 1e7)")
     args = ap.parse_args()
+    if args.workload != "c2":
+        return run_config(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -197,6 +202,131 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+C4_PLATFORM = dict(topology=0, topo_parameters="3;16,16,16;1,16,16;1,1,1", loopback_bw=1e8)  # FAT_TREE
+C5_PLATFORM = dict(topology=1, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8)  # DRAGONFLY
+
+
+def run_config(args):
+    """The other SURVEY.md §8(d) configs, each with its multi-GPU scheme (§8(e)):
+    c3  4096 independent maxmin_bench "medium" systems (one disjoint-union system per rank, systems
+        split over the ranks in nnz-balanced blocks): strong scaling, no data-path collective;
+    c4  LV08 flows on a 4096-host fat tree (SMPI-style cluster, crosstraffic on), maxmin: one giant
+        component, so replicas (weak scaling);
+    c5  L07 flows on a 4096-host dragonfly, FairBottleneck, variables sharded over the ranks with the
+        per-round all-reduces of multi.fb_solve_sharded (strong scaling).
+    One step = one full solve with the inputs resident in HBM."""
+    import numpy as np
+    import torch
+
+    from simgrid_amd import lmm
+    from simgrid_amd import multi as M
+
+    rank, world, local_rank = M.dist_env()
+    assert torch.cuda.is_available(), "bench.py needs an MI355X"
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    ex = M.DistExchange() if dist is not None else M.LocalExchange()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    t = time.time()
+    shards = None
+    if args.workload == "c3":
+        n_sys = 4096
+        bounds = M.balanced_blocks(np.ones(n_sys), world)
+        s = lmm.System(False)
+        for i in range(bounds[rank], bounds[rank + 1]):
+            s.gen_maxmin_bench(1, i)
+        work_vars, scaling = 100 * n_sys, "strong"
+        desc = dict(workload="C3: 4096 independent maxmin_bench medium systems (100 cnst x 100 vars), "
+                             "one disjoint-union solve per rank", systems=n_sys,
+                    parallelism=f"systems in nnz-balanced blocks x{world}")
+    elif args.workload == "c4":
+        flows = args.flows or 100_000
+        s = lmm.System(False)
+        s.gen_platform_flows(lmm.platform_params(model=lmm.LV08, n_flows=flows, seed=rank + 1, **C4_PLATFORM),
+                             want_vars=False)
+        work_vars, scaling = flows * world, "weak"
+        desc = dict(workload=f"C4: {flows} LV08 flows on fat tree {C4_PLATFORM['topo_parameters']} (4096 hosts)",
+                    flows=flows, parallelism=f"replicas x{world} (one component per system)")
+    else:
+        flows = args.flows or 10_000_000
+        s = lmm.System(False, lmm.System.FAIR_BOTTLENECK)
+        s.gen_platform_flows(lmm.platform_params(model=lmm.L07, n_flows=flows, seed=1, **C5_PLATFORM),
+                             want_vars=False)
+        f = M.export_flat(s)
+        del s
+        sub, _ = M.shard_variables(f, world)[rank]
+        shards = [M.DeviceFbShard(sub)]
+        nV_total, nC_total = len(f.penalty), len(f.cbound)
+        del f
+        work_vars, scaling = flows, "strong"
+        desc = dict(workload=f"C5: {flows} L07 flows on dragonfly {C5_PLATFORM['topo_parameters']} (4096 hosts), "
+                             "FairBottleneck", flows=flows,
+                    parallelism=f"variables sharded x{world}, 2 all-reduces per round")
+    if shards is None:
+        s.prepare()
+        st = s.last_stats()
+        nV, nC, nnz = st["n_var"], st["n_cnst"], st["nnz"]
+    else:
+        nV, nC, nnz = len(sub.penalty), len(sub.cbound), len(sub.cnst_idx)
+    log(f"[rank {rank}] {args.workload}: built in {time.time() - t:.1f}s: nV={nV} nC={nC} nnz={nnz}")
+
+    def step():
+        if shards is None:
+            s.device_solve()
+            return s.last_stats()["rounds"]
+        for sh in shards:
+            sh.begin()
+        return M.fb_solve_sharded(shards, ex, nV_total, nC_total)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rounds = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tot = np.array([nV, nnz, nC], dtype=np.float64)  # summed over ranks below
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = ex.sum(tot)
+    ms_per_step = 1000.0 * elapsed / args.steps
+    # algorithmic bytes of one solve (SURVEY.md §8(d)): maxmin 56 B/element + 24 B/variable + 32 B/constraint;
+    # fair bottleneck 36 B/element + 32 B/variable + 32 B/constraint per round
+    if args.workload == "c5":  # every rank sweeps all constraints: tot[2] = world x nC
+        alg = rounds * (36 * tot[1] + 32 * tot[0] + 32 * tot[2])
+    else:
+        alg = 56 * tot[1] + 24 * tot[0] + 32 * tot[2]
+    ach = alg / (ms_per_step * 1e-3) / 1e9
+    if rank == 0:
+        desc.update(active_vars=int(tot[0]), nnz=int(tot[1]), device_rounds=int(rounds))
+        print(json.dumps({
+            "metric": "LMM solve throughput (vars/s)", "value": round(work_vars * args.steps / elapsed, 1),
+            "unit": "vars/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic (generators of simgrid_amd/csrc/lmm_generators.hpp / lmm_platforms.hpp)",
+            "config": desc,
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "whole solve"},
+            "cpu_baseline": None}), flush=True)
+    if shards is not None:
+        for sh in shards:
+            sh.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -280,9 +280,14 @@ class DeviceFbShard:
         self.xnb = torch.zeros(nc + 1, dtype=torch.int32, device="cuda")
         self.xsum = torch.zeros(nc, dtype=torch.float64, device="cuda")
         self.xmin = torch.zeros(nc, dtype=torch.float64, device="cuda")
-        prec = lmm.get_precision() if precision is None else precision
-        self._check(L.lmmhip_fb_shard_begin(self.ctx, prec, ct.c_void_p(self.xnb.data_ptr()),
-                                            ct.c_void_p(self.xsum.data_ptr()), ct.c_void_p(self.xmin.data_ptr())))
+        self.prec = lmm.get_precision() if precision is None else precision
+        self.begin()
+
+    def begin(self):
+        """Start a solve (fair_bottleneck.cpp:29-50 initialisation); rounds follow with step()."""
+        self._check(self.L.lmmhip_fb_shard_begin(self.ctx, self.prec, ct.c_void_p(self.xnb.data_ptr()),
+                                                 ct.c_void_p(self.xsum.data_ptr()),
+                                                 ct.c_void_p(self.xmin.data_ptr())))
 
     def _check(self, rc):
         if rc != 0:
