@@ -112,6 +112,32 @@ int lmmhip_fb_shard_begin(lmmhip_ctx* ctx, double precision, int32_t* xnb, doubl
 int lmmhip_fb_shard_step(lmmhip_ctx* ctx, int phase);
 int lmmhip_fb_shard_poll(lmmhip_ctx* ctx, int* done, int64_t* rounds); /* synchronises the stream */
 
+/* Model-side step glue on the device, over the values of the context's last solve:
+ * the actions' remains / max duration / latency stay in HBM between steps.
+ *   var_index[i]        dense index (CSR order of lmmhip_upload) of action i's variable, -1 = not solved
+ *   penalty[i]          the variable's current penalty (finish test: remains <= 0 && penalty > 0)
+ *   sharing_penalty[i]  CM02: the penalty restored when the latency is paid (network_cm02.cpp:145)
+ *   flags[i]            bit0 = the variable has no constraint, bit1 = suspended
+ * lmmhip_next_event_full: Model::next_occuring_event_full (Model.cpp:103-129), with_latency adds the
+ *   network / ptask latency term (network_interface.cpp:57-70, ptask_L07.cpp:69-82); -1 = no event.
+ * lmmhip_update_actions_full: update_actions_state_full of model LMMHIP_MODEL_CPU (cpu_interface.cpp:37-51),
+ *   _CM02 (network_cm02.cpp:128-163) or _L07 (ptask_L07.cpp:84-118); events[i] gets
+ *   LMMHIP_EV_FINISHED / LMMHIP_EV_LATENCY_PAID (the host then finishes the action / updates the
+ *   variable's penalty, and for L07 its bound); *n_events = actions with an event. */
+#define LMMHIP_MODEL_CPU 0
+#define LMMHIP_MODEL_CM02 1
+#define LMMHIP_MODEL_L07 2
+#define LMMHIP_EV_FINISHED 1
+#define LMMHIP_EV_LATENCY_PAID 2
+int lmmhip_actions_upload(lmmhip_ctx* ctx, int64_t n, const int32_t* var_index, const double* remains,
+                          const double* max_duration, const double* latency, const double* penalty,
+                          const double* sharing_penalty, const uint8_t* flags);
+int lmmhip_next_event_full(lmmhip_ctx* ctx, int with_latency, double* out);
+int lmmhip_update_actions_full(lmmhip_ctx* ctx, int model, double delta, double maxmin_precision,
+                               double surf_precision, int64_t* n_events);
+int lmmhip_actions_download(lmmhip_ctx* ctx, double* remains, double* max_duration, double* latency, double* penalty,
+                            uint8_t* events);
+
 /* Number of visible HIP devices (0 when none; never initialises a context). */
 int lmmhip_device_count(void);
 

@@ -6,6 +6,8 @@
 // reference (the FairBottleneck `value == bound` test is exact).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include <algorithm>
 #include <string>
 #include <vector>
@@ -13,6 +15,7 @@
 #include "../../include/lmm/lmm_hip.h"
 #include "lmm_dev.hpp"
 #include "lmm_fb_kernels.hpp"
+#include "lmm_step_kernels.hpp"
 #include "lmm_maxmin_kernels.hpp"
 
 using namespace lmmdev;
@@ -64,6 +67,8 @@ struct lmmhip_ctx {
   int64_t fb_round = 0;
   double fb_prec = 0;
   bool fb_shard = false;
+  ActDev act{};                        // model-side action state (lmm_step_kernels.hpp)
+  std::vector<void*> act_allocs;
   int32_t* xnb_own = nullptr;  // the context's own exchange buffers (unsharded solves)
   double *xsum_own = nullptr, *xmin_own = nullptr;
 };
@@ -143,6 +148,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   if (c->own_stream && c->own_stream != c->stream)
     (void)hipStreamSynchronize(c->own_stream);
   free_all(c);
+  for (void* p : c->act_allocs)
+    (void)hipFree(p);
   if (c->h_ctl)
     (void)hipHostFree(c->h_ctl);
   if (c->vstat)
@@ -673,6 +680,125 @@ int lmmhip_fb_shard_poll(lmmhip_ctx* c, int* done, int64_t* rounds) {
   if (rounds)
     *rounds = c->h_ctl[CTL_ROUNDS];
   c->stats.rounds = c->h_ctl[CTL_ROUNDS];
+  return 0;
+}
+
+// ---- model-side step glue (lmm_step_kernels.hpp) ----
+extern "C++" template <class T> static int act_alloc(lmmhip_ctx* c, T** out, int64_t n, const T* src) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, size_t(n > 0 ? n : 1) * sizeof(T)));
+  c->act_allocs.push_back(p);
+  *out = static_cast<T*>(p);
+  if (src && n > 0)
+    HIPCHK(hipMemcpyAsync(p, src, size_t(n) * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+int lmmhip_actions_upload(lmmhip_ctx* c, int64_t n, const int32_t* var_index, const double* remains,
+                          const double* max_duration, const double* latency, const double* penalty,
+                          const double* sharing_penalty, const uint8_t* flags) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (n < 0 || (n > 0 && (!var_index || !remains || !max_duration || !latency || !penalty || !sharing_penalty ||
+                          !flags)))
+    return fail(LMMHIP_E_ARG, "null action arrays");
+  const int64_t nV = c->uploaded ? c->d.nV : 0;
+  for (int64_t i = 0; i < n; i++)
+    if (var_index[i] < -1 || var_index[i] >= nV)
+      return fail(LMMHIP_E_ARG, "action var_index out of range of the uploaded system");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (void* p : c->act_allocs)
+    (void)hipFree(p);
+  c->act_allocs.clear();
+  ActDev& a = c->act;
+  a = ActDev{};
+  a.n = n;
+  int32_t* vidx;
+  double *sp;
+  uint8_t* fl;
+  int rc = 0;
+  rc |= act_alloc(c, &vidx, n, var_index);
+  rc |= act_alloc(c, &a.remains, n, remains);
+  rc |= act_alloc(c, &a.max_duration, n, max_duration);
+  rc |= act_alloc(c, &a.latency, n, latency);
+  rc |= act_alloc(c, &a.penalty, n, penalty);
+  rc |= act_alloc(c, &sp, n, sharing_penalty);
+  rc |= act_alloc(c, &fl, n, flags);
+  rc |= act_alloc<uint8_t>(c, &a.events, n, nullptr);
+  rc |= act_alloc<unsigned long long>(c, &a.umin, 1, nullptr);
+  rc |= act_alloc<int32_t>(c, &a.nev, 1, nullptr);
+  if (rc)
+    return rc;
+  a.vidx = vidx;
+  a.share_pen = sp;
+  a.flags = fl;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_next_event_full(lmmhip_ctx* c, int with_latency, double* out) {
+  if (!c || !out)
+    return fail(LMMHIP_E_ARG, "null argument");
+  if (!c->act.umin)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_upload first");
+  HIPCHK(hipSetDevice(c->device));
+  unsigned long long h = ~0ull;
+  HIPCHK(hipMemsetAsync(c->act.umin, 0xFF, sizeof(unsigned long long), c->stream));
+  if (c->act.n > 0)
+    LAUNCH(7, -1, act_next_event, grid_for(c->act.n, kBlock), kBlock, c->act, c->d.x, with_latency);
+  HIPCHK(hipMemcpyAsync(&h, c->act.umin, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (h == ~0ull) {
+    *out = -1.0;
+  } else {
+    double m;
+    std::memcpy(&m, &h, sizeof(m));
+    *out = m;
+  }
+  return 0;
+}
+
+int lmmhip_update_actions_full(lmmhip_ctx* c, int model, double delta, double maxmin_precision,
+                               double surf_precision, int64_t* n_events) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (!c->act.nev)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_upload first");
+  if (model != MODEL_CPU && model != MODEL_CM02 && model != MODEL_L07)
+    return fail(LMMHIP_E_ARG, "unknown model");
+  HIPCHK(hipSetDevice(c->device));
+  int32_t h = 0;
+  HIPCHK(hipMemsetAsync(c->act.nev, 0, sizeof(int32_t), c->stream));
+  if (c->act.n > 0)
+    LAUNCH(7, -1, act_update, grid_for(c->act.n, kBlock), kBlock, c->act, c->d.x, model, delta, maxmin_precision,
+           surf_precision);
+  HIPCHK(hipMemcpyAsync(&h, c->act.nev, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (n_events)
+    *n_events = h;
+  return 0;
+}
+
+int lmmhip_actions_download(lmmhip_ctx* c, double* remains, double* max_duration, double* latency, double* penalty,
+                            uint8_t* events) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t n = size_t(c->act.n);
+  if (n) {
+    if (remains)
+      HIPCHK(hipMemcpyAsync(remains, c->act.remains, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (max_duration)
+      HIPCHK(hipMemcpyAsync(max_duration, c->act.max_duration, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (latency)
+      HIPCHK(hipMemcpyAsync(latency, c->act.latency, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (penalty)
+      HIPCHK(hipMemcpyAsync(penalty, c->act.penalty, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (events)
+      HIPCHK(hipMemcpyAsync(events, c->act.events, n, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 

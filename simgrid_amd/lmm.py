@@ -110,6 +110,10 @@ SIGNATURES = {
     "lmmhip_fb_shard_begin": (I, [P, D, P, P, P]),
     "lmmhip_fb_shard_step": (I, [P, I]),
     "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
+    "lmmhip_actions_upload": (I, [P, I64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_next_event_full": (I, [P, I, PD]),
+    "lmmhip_update_actions_full": (I, [P, I, D, D, D, PI64]),
+    "lmmhip_actions_download": (I, [P, PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
     "lmmhip_device_count": (I, []),
     "lmmhip_last_error": (ct.c_char_p, []),
 }
