@@ -52,6 +52,7 @@ struct lmmhip_ctx {
   bool uploaded = false;
   bool profiling = false;
   int group = 8;  // lanes per row in mm_vote (power of two >= mean row length, <= 64)
+  int sat_waves = 1;  // waves per ready constraint in mm_saturate (mean 64-element CSC chunks, 1/2/4)
   int n_cu = 256;  // compute units (grid of the one-block-per-CU kernels)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // per-launch event pairs (profiling mode): recorded without synchronising, resolved after the
@@ -349,6 +350,8 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   d.ccol[2] = ccol2;
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
+  const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
+  c->sat_waves = cmean <= 64 ? 1 : cmean <= 160 ? 2 : 4;
   c->uploaded = true;
   c->stats = lmmhip_stats{};
   c->stats.n_var = nV;
@@ -527,7 +530,12 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
-      LAUNCH(4, r, mm_saturate, grid_for(ncl, kBlock), kBlock, d, int(r), cb, gL);
+      if (c->sat_waves == 1)
+        LAUNCH(4, r, mm_saturate<1>, gL, kBlock, d, int(r), cb, gL);
+      else if (c->sat_waves == 2)
+        LAUNCH(4, r, mm_saturate<2>, grid_for(2 * ncl, kBlock), kBlock, d, int(r), cb, gL);
+      else
+        LAUNCH(4, r, mm_saturate<4>, grid_for(4 * ncl, kBlock), kBlock, d, int(r), cb, gL);
       LAUNCH(5, r, mm_update, gU, kBlock, d, int(r), prec);
     }
     LAUNCH(6, r, mm_done, 1, kBlock, d, gU);

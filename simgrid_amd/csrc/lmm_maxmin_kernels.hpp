@@ -483,108 +483,123 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
 }
 
 // Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.
-// One wave per ready constraint c.  Per 64-element chunk of c's CSC segment: lanes claim the alive
-// variables (atomicCAS: a duplicate element claims once), fix them at ratio/penalty; then the
-// claimed variables' CSR elements are flattened over the wave (wave prefix of the row lengths, owner
-// found by binary search in LDS), one lane per element loads it, and the element's three pushes are
-// issued by a quad of lanes into the constraint's 32-B record (4 wave instructions per 64 elements,
-// each ONE atomic request per element; scripts/ubench_atomic.hip).  Decrements to c itself are
-// skipped: c leaves the light table (every alive variable on it is fixed, usage -> 0,
-// maxmin.cpp:608-615).
-__device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int round, int lane, int* pre) {
-  const double r = s.cst[c].ratio;
+// K waves per ready constraint c (K = the host's estimate of c's 64-element CSC chunks), wave k taking
+// chunks k, k + K, ...  Per chunk: lanes claim the alive variables (atomicCAS: a duplicate element
+// claims once, also across the waves of c), fix them at ratio/penalty; then the claimed variables'
+// CSR elements are flattened over the wave (wave prefix of the row lengths in LDS, owner lane found by
+// binary search), kSatU x kWave elements at a time so that their gathers are in flight together, and
+// each element's three pushes are issued by a quad of lanes into the constraint's 32-B record (ONE
+// atomic request per element; scripts/ubench_atomic.hip).  Decrements to c itself are skipped: c
+// leaves the light table (every alive variable on it is fixed, usage -> 0, maxmin.cpp:608-615).
+// c's ratio is left in place (the other waves of c read it; the dead key hides it from later readers).
+constexpr int kSatU = 4;
+
+__device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
+                                               int round, int lane, int* pre) {
   const int q = lane & 3;
-  const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
-  for (uint32_t base = cb; base < ce; base += kWave) {  // wave-uniform
-    const uint32_t j = base + lane;
-    int32_t lv = -1;
-    if (j < ce) {
-      lv = s.csc_v[j];
-      if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
-        lv = -1;
-    }
-    double lp = 1.0, lx = 0.0;
-    uint32_t rb = 0;
-    int len = 0;
-    if (lv >= 0) {
-      lp = s.pen[lv];
-      lx = r / lp;
-      s.x[lv] = lx;
-      rb = s.var_ptr[lv];
-      len = int(s.var_ptr[lv + 1] - rb);
-    }
-    // inclusive wave scan of the row lengths
-    int incl = len;
+  const uint32_t j = j0 + lane;
+  int32_t lv = -1;
+  if (j < ce) {
+    lv = s.csc_v[j];
+    if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
+      lv = -1;
+  }
+  double lp = 1.0, lx = 0.0;
+  uint32_t rb = 0;
+  int len = 0;
+  if (lv >= 0) {
+    lp = s.pen[lv];
+    lx = r / lp;
+    s.x[lv] = lx;
+    rb = s.var_ptr[lv];
+    len = int(s.var_ptr[lv + 1] - rb);
+  }
+  int incl = len;  // inclusive wave scan of the row lengths
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const int t = __shfl_up(incl, o, kWave);
-      if (lane >= o)
-        incl += t;
-    }
-    const int total = __shfl(incl, kWave - 1, kWave);
-    pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
-    __builtin_amdgcn_wave_barrier();
-    for (int f0 = 0; f0 < total; f0 += kWave) {  // wave-uniform
-      const int f = f0 + lane;
-      const bool valid = f < total;
-      int o = 0;  // owner lane: last lane with pre <= f and len > 0 (== last with pre <= f)
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int t = __shfl_up(incl, o, kWave);
+    if (lane >= o)
+      incl += t;
+  }
+  const int total = __shfl(incl, kWave - 1, kWave);
+  pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
+  __builtin_amdgcn_wave_barrier();
+  for (int f0 = 0; f0 < total; f0 += kSatU * kWave) {  // wave-uniform
+    int32_t cc[kSatU];
+    uint32_t kk[kSatU];
+    int ol[kSatU];
+#pragma unroll
+    for (int u = 0; u < kSatU; u++) {  // owner lanes and element indices, then independent gathers
+      const int f = f0 + u * kWave + lane;
+      int o = 0;  // owner lane: last lane with pre <= f
 #pragma unroll
       for (int step = kWave / 2; step > 0; step >>= 1)
-        if (o + step < kWave && pre[o + step] <= f)
+        if (pre[o + step] <= f)
           o += step;
-      const int orb = __shfl(int(rb), o, kWave);
-      const int opre = pre[o];
-      const double ox = __shfl(lx, o, kWave);
-      const double op = __shfl(lp, o, kWave);
-      int32_t cc = -1;
-      double a0 = 0.0, a1 = 0.0;
-      bool fat = false;
-      if (valid) {
-        const uint32_t k = uint32_t(orb) + uint32_t(f - opre);
-        cc = s.csr_c[k];
-        if (cc == c || s.key[cc] == kDeadKey) {
-          cc = -1;
-        } else {
-          fat = s.cflags[cc] & 1;
-          const double w = s.csr_w[k];
-          a0 = w * ox;
-          a1 = w / op;
-        }
+      ol[u] = o;
+      kk[u] = uint32_t(__shfl(int(rb), o, kWave)) + uint32_t(f - pre[o]);
+      cc[u] = f < total ? s.csr_c[kk[u]] : -1;
+    }
+    double a0[kSatU], a1[kSatU];
+    bool fat[kSatU];
+#pragma unroll
+    for (int u = 0; u < kSatU; u++) {
+      const double ox = __shfl(lx, ol[u], kWave);
+      const double op = __shfl(lp, ol[u], kWave);
+      fat[u] = false;
+      a0[u] = a1[u] = 0.0;
+      if (cc[u] >= 0 && (cc[u] == c || s.key[cc[u]] == kDeadKey))
+        cc[u] = -1;
+      if (cc[u] >= 0) {
+        fat[u] = s.cflags[cc[u]] & 1;
+        const double w = s.csr_w[kk[u]];
+        a0[u] = w * ox;
+        a1[u] = w / op;
       }
-      const int nel = total - f0 < kWave ? total - f0 : kWave;
+    }
+#pragma unroll
+    for (int u = 0; u < kSatU; u++) {
+      const int nel = total - f0 - u * kWave;
 #pragma unroll
       for (int t = 0; t < kWave / 16; t++) {
         if (t * 16 >= nel)
           break;
         const int e = t * 16 + (lane >> 2);
-        const int ec = __shfl(cc, e, kWave);
-        const int ef = __shfl(int(fat), e, kWave);
-        const double e0 = __shfl(a0, e, kWave);
-        const double e1 = __shfl(a1, e, kWave);
+        const int ec = __shfl(cc[u], e, kWave);
+        const int ef = __shfl(int(fat[u]), e, kWave);
+        const double e0 = __shfl(a0[u], e, kWave);
+        const double e1 = __shfl(a1[u], e, kWave);
         if (ec >= 0 && q < 3 && (!ef || q == 2))
           unsafeAtomicAdd(&s.cst[ec].drem + q, q == 0 ? e0 : q == 1 ? e1 : 1.0);
         if (ec >= 0 && q == 3)
           s.touched[ec] = 1;  // plain byte store: mm_update reads 1 B per constraint, not the record
       }
     }
-    __builtin_amdgcn_wave_barrier();
   }
-  if (lane == 0) {
-    s.cst[c].ratio = dinf();
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int k, int round, int lane,
+                                                              int* pre) {
+  const double r = s.cst[c].ratio;
+  const uint32_t ce = s.cnst_ptr[c + 1];
+  for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
+    saturate_chunk(s, c, r, base, ce, round, lane, pre);
+  if (k == 0 && lane == 0) {
     s.key[c] = kDeadKey;
     s.chg[c] = uint16_t(round);
   }
 }
 
-// One wave per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
+// K waves per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
 // counts in LDS (parallel: 8 segments per thread, wave shuffles, one LDS exchange) and maps its waves
 // onto the ready list by binary search.
-__global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, int ready_blocks) {
+template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, int ready_blocks) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ int pre[kMaxBlocks + 1];
   __shared__ int wsum[kBlock / kWave];
-  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_one)
+  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
   constexpr int kPer = kMaxBlocks / kBlock;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   int loc[kPer];
@@ -622,13 +637,15 @@ __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, 
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
   const int64_t chunk = chunk_of(s.ctl[CTL_NCL0 + cb], ready_blocks);
-  for (int64_t i = wave; i < total; i += nwaves) {
+  for (int64_t g = wave; g < int64_t(total) * K; g += nwaves) {
+    const int64_t i = g / K;
+    const int k = int(g % K);
     int lo = 0;  // last segment with pre[seg] <= i
 #pragma unroll
     for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
       if (lo + step < ready_blocks && pre[lo + step] <= i)
         lo += step;
-    saturate_one(s, s.ready[lo * chunk + (i - pre[lo])], round, lane, wpre[w]);
+    saturate_one<K>(s, s.ready[lo * chunk + (i - pre[lo])], k, round, lane, wpre[w]);
   }
 }
 
