@@ -210,6 +210,37 @@ C4_PLATFORM = dict(topology=0, topo_parameters="3;16,16,16;1,16,16;1,1,1", loopb
 C5_PLATFORM = dict(topology=1, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8)  # DRAGONFLY
 
 
+def config_cpu_baseline(workload, flows):
+    """The oracle (single-threaded restatement of maxmin.cpp / fair_bottleneck.cpp) on a bounded sample of
+    the same workload, rank 0, N=1: C3 solves its 4096 medium systems one lmm_solve each (the reference
+    solves independent systems one by one), C4 the same 1e5-flow fat-tree system, C5 the same dragonfly
+    generator at 1e6 flows (1/10 of the GPU workload)."""
+    from oracle import pyoracle as O
+
+    if workload == "c3":
+        tcpu, rounds = 0.0, 0
+        for i in range(4096):
+            o = O.System(False)
+            o.gen_maxmin_bench(1, i)
+            tcpu += o.timed_solve()
+            rounds += o.last_rounds
+        return {"value": round(100 * 4096 / tcpu, 1), "unit": "vars/s", "cores": 1, "kind": "port",
+                "sample": f"the same 4096 medium systems, one solve() each timed with steady_clock: {tcpu:.3f} s in"
+                          f" total, {rounds} sequential rounds"}
+    if workload == "c4":
+        n = flows or 100_000
+        o = O.System(False)
+        o.gen_platform_flows(O.platform_params(model=O.LV08, n_flows=n, seed=1, **C4_PLATFORM))
+    else:
+        n = min(flows or 10_000_000, 1_000_000)
+        o = O.System(False, O.System.FAIR_BOTTLENECK)
+        o.gen_platform_flows(O.platform_params(model=O.L07, n_flows=n, seed=1, **C5_PLATFORM))
+    tcpu = o.timed_solve()
+    return {"value": round(n / tcpu, 1), "unit": "vars/s", "cores": 1, "kind": "port",
+            "sample": f"same generator, {n} flows, one solve() timed with steady_clock: {tcpu:.2f} s,"
+                      f" {o.last_rounds} sequential rounds"}
+
+
 def run_config(args):
     """The other SURVEY.md §8(d) configs, each with its multi-GPU scheme (§8(e)):
     c3  4096 independent maxmin_bench "medium" systems (one disjoint-union system per rank, systems
@@ -313,6 +344,9 @@ def run_config(args):
     else:
         alg = 56 * tot[1] + 24 * tot[0] + 32 * tot[2]
     ach = alg / (ms_per_step * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = config_cpu_baseline(args.workload, args.flows)
     if rank == 0:
         desc.update(active_vars=int(tot[0]), nnz=int(tot[1]), device_rounds=int(rounds))
         print(json.dumps({
@@ -323,7 +357,7 @@ def run_config(args):
             "config": desc,
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "whole solve"},
-            "cpu_baseline": None}), flush=True)
+            "cpu_baseline": cpu}), flush=True)
     if shards is not None:
         for sh in shards:
             sh.close()

@@ -258,7 +258,8 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int f
 // re-vote in LDS; each full queue of kBlock rows is then resolved one lane per row, with up to kReg
 // independent gathers in flight, so the rare slow rows no longer stall whole waves of fast ones.
 constexpr int kReg = 8;
-constexpr int kFilt = 4;
+constexpr int kFilt = 4;  // rows per lane per filter step (their loads in flight together)
+constexpr int kFlush = 4;  // filter rows between two queue flushes (queue capacity (kFlush + 1) x B)
 
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems) {
@@ -379,7 +380,7 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
   if (s.ctl[CTL_DONE])
     return;
   __shared__ int st_rows, st_elems;
-  __shared__ int q[B * (kFilt + 1)];  // queued rows (relative to the block's chunk base)
+  __shared__ int q[B * (kFlush + 1)];  // queued rows (relative to the block's chunk base)
   __shared__ int qn;
   __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
   if (threadIdx.x == 0)
@@ -399,7 +400,7 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
   const uint16_t prev = uint16_t(round - 1);
   // contiguous chunk per block so queued rows fit in 32-bit offsets from the chunk base
   constexpr int kStep = B * kFilt;
-  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kStep - 1) / kStep * kStep;
+  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + B - 1) / B * B;  // rows per block
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
   for (int64_t base = lo; base < hi; base += kStep) {  // block-uniform
@@ -417,12 +418,22 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
       else
         ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
     }
+    unsigned kt[kFilt], sk[kFilt];  // target key and the row's other-key floor, gathered together
+#pragma unroll
+    for (int u = 0; u < kFilt; u++) {
+      kt[u] = 0;
+      sk[u] = 0;
+      if (ch[u]) {
+        kt[u] = key[tt[u]];
+        sk[u] = skey[base + u * B + threadIdx.x];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < kFilt; u++) {
       const int64_t row = base + u * B + threadIdx.x;
       bool need = tt[u] == kUnvoted;
       if (ch[u])  // target changed last round: does the vote still stand?
-        need = !(key[tt[u]] < skey[row]);
+        need = !(kt[u] < sk[u]);
       const unsigned long long m = __ballot(need);  // one LDS atomic per wave
       const int lane = threadIdx.x & (kWave - 1);
       const int leader = m ? __ffsll((long long)m) - 1 : 0;
@@ -432,17 +443,19 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
       at = __shfl(at, leader, kWave);
       if (need)
         q[at + __popcll(m & ((1ull << lane) - 1))] = int(row - lo);
+      if ((u % kFlush) == kFlush - 1) {  // at most kFlush * B rows queued since the last flush
+        __syncthreads();
+        int n = qn;
+        while (n >= B) {  // resolve full queues: the last B entries each time
+          vote_row(s, buf, round, lo + q[n - B + threadIdx.x], &st_rows, &st_elems);
+          n -= B;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+          qn = n;
+        __syncthreads();
+      }
     }
-    __syncthreads();
-    int n = qn;
-    while (n >= B) {  // resolve full queues: the last B entries each time
-      vote_row(s, buf, round, lo + q[n - B + threadIdx.x], &st_rows, &st_elems);
-      n -= B;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-      qn = n;
-    __syncthreads();
   }
   const int n = qn;
   if (threadIdx.x < n)
