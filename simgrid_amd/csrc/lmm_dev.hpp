@@ -55,6 +55,7 @@ struct Dev {
   const uint32_t* cnst_ptr;  // [nC+1] CSC offsets (constraint-major)
   const int32_t* csc_v;      // [nnz]
   const double* csc_w;       // [nnz]
+  double* csc_u;             // [nnz] w / penalty of each CSC element (recomputed when penalties change)
   const double* pen;         // [nV]
   const double* vbound;      // [nV]
   const double* cbound;      // [nC]

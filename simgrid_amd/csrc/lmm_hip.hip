@@ -248,6 +248,7 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   rc |= dalloc(c, &cp, nC + 1);
   rc |= dalloc(c, &csc_v, nnz);
   rc |= dalloc(c, &csc_w, nnz);
+  rc |= dalloc(c, &d.csc_u, nnz);
   rc |= dalloc(c, &pen, nV);
   rc |= dalloc(c, &vb, nV);
   rc |= dalloc(c, &cb, nC);
@@ -352,6 +353,11 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
   const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
   c->sat_waves = cmean <= 64 ? 1 : cmean <= 160 ? 2 : 4;
+  if (nnz > 0) {  // per-element usage w / penalty, kept in step with pen (lmmhip_update_vars)
+    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, c->stream, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
   c->uploaded = true;
   c->stats = lmmhip_stats{};
   c->stats.n_var = nV;
@@ -366,6 +372,10 @@ int lmmhip_update_vars(lmmhip_ctx* c, const double* penalty, const double* var_b
   HIPCHK(hipSetDevice(c->device));
   if (penalty && c->d.nV)
     HIPCHK(hipMemcpyAsync((void*)c->d.pen, penalty, sizeof(double) * c->d.nV, hipMemcpyHostToDevice, c->stream));
+  if (penalty && c->d.nnz) {
+    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(c->d.nnz, kBlock)), dim3(kBlock), 0, c->stream, c->d);
+    HIPCHK(hipGetLastError());
+  }
   if (var_bound && c->d.nV)
     HIPCHK(
         hipMemcpyAsync((void*)c->d.vbound, var_bound, sizeof(double) * c->d.nV, hipMemcpyHostToDevice, c->stream));

@@ -24,6 +24,13 @@
 
 namespace lmmdev {
 
+// Per-element usage w / penalty of every CSC element (maxmin.cpp:531-533's summand), computed at upload
+// and whenever the penalties change, so the per-solve init streams it instead of gathering pen[v].
+__global__ void __launch_bounds__(kBlock) mm_elem_usage(Dev s) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz; j += int64_t(gridDim.x) * kBlock)
+    s.csc_u[j] = s.csc_w[j] / s.pen[s.csc_v[j]];
+}
+
 // Init, one wave per constraint: maxmin.cpp:520-555.  remaining = bound; skipped when
 // bound <= bound*prec; usage = sum (SHARED) or max (FATPIPE) of w/p over the active elements.
 __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
@@ -35,7 +42,7 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
     const bool fat = s.cflags[c] & 1;
     double acc = 0.0;
     for (uint32_t j = b + lane; j < e; j += kWave) {
-      double u = s.csc_w[j] / s.pen[s.csc_v[j]];
+      const double u = s.csc_u[j];
       acc = fat ? fmax(acc, u) : acc + u;
     }
     acc = fat ? wave_max(acc) : wave_sum(acc);
@@ -711,7 +718,7 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
               const int32_t v = s.csc_v[j];
               if (s.x[v] > 0)
                 continue;
-              use = fmax(use, s.csc_w[j] / s.pen[v]);
+              use = fmax(use, s.csc_u[j]);
             }
           }
           rec->rem = rem;
