@@ -70,6 +70,35 @@ int lmmhip_upload(lmmhip_ctx* ctx, int64_t n_var, int64_t n_cnst, int64_t nnz, c
 int lmmhip_update_vars(lmmhip_ctx* ctx, const double* penalty, const double* var_bound);
 int lmmhip_update_cnsts(lmmhip_ctx* ctx, const double* cnst_bound);
 
+/* ---- Resident System mirror + device-side delta log ----
+ * Replaces the per-solve host flatten + full upload (System::lmm_solve's init walk, maxmin.cpp:509-555,
+ * preceded by the mutations of maxmin.cpp:205-323 / 703-888) with: the host System's element /
+ * variable / constraint records mirrored in HBM, only the records a mutation touched shipped per
+ * solve, and the solver's CSR/CSC rebuilt on the device with System::flatten_maxmin's rules.
+ *
+ * lmmhip_res_apply: one delta batch.  *_total = sizes of the host tables (the mirror grows to them,
+ *   keeping its contents).  Element e: constraint id (-1 = unused), weight, flags bit0 = in its
+ *   constraint's enabled list.  Variable v: slab base (first element id), elements in use (0 = dead),
+ *   penalty, bound.  Constraint c: bound, flags bit0 = FATPIPE.  Host arrays are borrowed.
+ * lmmhip_res_flatten: build the max-min system of the listed constraints (list order = dense order:
+ *   the active set, or the modified set in selective mode) from the mirror; then lmmhip_solve(MAXMIN)
+ *   as after lmmhip_upload.  counts3 (optional) = {n_var, n_cnst, nnz} of the built system.
+ * lmmhip_res_values: after the solve, per variable slot (n = n_var_total of the mirror): values[v]
+ *   and reset[v] = 1 iff lmm_solve assigns v (its solved value, or 0 for a variable seen through an
+ *   enabled element of a listed constraint that is not part of the system, maxmin.cpp:509-514). */
+int lmmhip_res_apply(lmmhip_ctx* ctx, int64_t n_elem_total, int64_t n_var_total, int64_t n_cnst_total, int64_t ne,
+                     const int64_t* e_id, const int32_t* e_cnst, const double* e_weight, const uint8_t* e_flags,
+                     int64_t nv, const int32_t* v_id, const int64_t* v_ebase, const int32_t* v_nelem,
+                     const double* v_penalty, const double* v_bound, int64_t nc, const int32_t* c_id,
+                     const double* c_bound, const uint8_t* c_flags);
+int lmmhip_res_flatten(lmmhip_ctx* ctx, int64_t n_list, const int32_t* cnst_list, double precision, int64_t* counts3);
+int lmmhip_res_values(lmmhip_ctx* ctx, int64_t n, double* values, uint8_t* reset);
+/* Inspection: download the flattened system the next lmmhip_solve runs on (from lmmhip_upload or
+ * lmmhip_res_flatten).  counts3 = {n_var, n_cnst, nnz}; null arrays are skipped (sizes first). */
+int lmmhip_flat_download(lmmhip_ctx* ctx, int64_t* counts3, uint32_t* var_ptr, int32_t* csr_c, double* csr_w,
+                         uint32_t* cnst_ptr, int32_t* csc_v, double* csc_w, double* penalty, double* var_bound,
+                         double* cnst_bound, uint8_t* cnst_flags);
+
 /* Solve on the device; values stay resident in HBM until lmmhip_get_values(). */
 int lmmhip_solve(lmmhip_ctx* ctx, int kind, double precision);
 

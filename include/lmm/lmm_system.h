@@ -74,6 +74,24 @@ int lmm_device_solve(lmm_sys* s);
 int lmm_fetch(lmm_sys* s);
 /* stats of the last solve: rounds, n_var, n_cnst, nnz (int64[4]); device/flatten/upload/fetch ms */
 int lmm_last_stats(lmm_sys* s, int64_t* counts4, double* ms4);
+/* Resident mode (lmmhip_res_*): the system lives in HBM, mutations since the
+ * last solve (maxmin.cpp:205-323, 703-888) are shipped as a delta log and the max-min system is
+ * flattened on the device.  Replaces the host flatten of lmm_prepare for max-min solves. */
+int lmm_set_resident(lmm_sys* s, int on);
+int lmm_is_resident(lmm_sys* s);
+/* pending delta-log sizes {elements, variables, constraints}; -1 each = whole system pending */
+int lmm_pending_deltas(lmm_sys* s, int64_t* out3);
+/* records (elements + variables + constraints) shipped by the last resident solve */
+int64_t lmm_last_delta_records(lmm_sys* s);
+/* host table sizes {element slots, variable slots, constraint slots} (ids are < these) */
+int lmm_table_sizes(lmm_sys* s, int64_t* out3);
+/* Test/inspection hook: drain the pending delta log into caller buffers instead of shipping it (the
+ * records lmmhip_res_apply would receive).  sizes6 in: capacities {elements, variables, constraints}
+ * (>= lmm_pending_deltas, table sizes when -1); out: {ne, nv, nc, n_elem_total, n_var_total,
+ * n_cnst_total}. */
+int lmm_resident_drain(lmm_sys* s, int64_t* sizes6, int64_t* e_id, int32_t* e_cnst, double* e_weight,
+                       uint8_t* e_flags, int32_t* v_id, int64_t* v_ebase, int32_t* v_nelem, double* v_penalty,
+                       double* v_bound, int32_t* c_id, double* c_bound, uint8_t* c_flags);
 /* The device context a system solves on (created on the current HIP device on first use);
  * gives access to the lmmhip_* measurement calls (profiling, per-round work profile). */
 struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s);

@@ -165,6 +165,55 @@ int lmm_is_modified(lmm_sys* s) { return s->sys.modified(); }
 int lmm_prepare(lmm_sys* s) { GUARD(s->sys.prepare()) }
 int lmm_device_solve(lmm_sys* s) { GUARD(s->sys.device_solve()) }
 int lmm_fetch(lmm_sys* s) { GUARD(s->sys.fetch()) }
+int lmm_set_resident(lmm_sys* s, int on) { GUARD(s->sys.set_resident(on != 0)) }
+int lmm_is_resident(lmm_sys* s) { return s->sys.resident() ? 1 : 0; }
+int lmm_pending_deltas(lmm_sys* s, int64_t* out3) { GUARD(s->sys.pending_deltas(out3)) }
+int64_t lmm_last_delta_records(lmm_sys* s) { return s->sys.last_stats().delta_records; }
+int lmm_table_sizes(lmm_sys* s, int64_t* out3) {
+  out3[0] = int64_t(s->sys.n_elem_slots());
+  out3[1] = int64_t(s->sys.n_var_slots());
+  out3[2] = int64_t(s->sys.n_cnst_slots());
+  return 0;
+}
+int lmm_resident_drain(lmm_sys* s, int64_t* sizes6, int64_t* e_id, int32_t* e_cnst, double* e_weight,
+                       uint8_t* e_flags, int32_t* v_id, int64_t* v_ebase, int32_t* v_nelem, double* v_penalty,
+                       double* v_bound, int32_t* c_id, double* c_bound, uint8_t* c_flags) {
+  int64_t pend[3];
+  s->sys.pending_deltas(pend);
+  const int64_t want[3] = {pend[0] < 0 ? int64_t(s->sys.n_elem_slots()) : pend[0],
+                           pend[1] < 0 ? int64_t(s->sys.n_var_slots()) : pend[1],
+                           pend[2] < 0 ? int64_t(s->sys.n_cnst_slots()) : pend[2]};
+  if (!s->sys.resident() || want[0] > sizes6[0] || want[1] > sizes6[1] || want[2] > sizes6[2]) {
+    g_err = "lmm_resident_drain: not resident, or buffers smaller than lmm_pending_deltas";
+    return 1;
+  }
+  simgrid_amd::lmm::System::ResPacked p;
+  try {
+    s->sys.drain_deltas(p);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+  std::copy(p.e_id.begin(), p.e_id.end(), e_id);
+  std::copy(p.e_cnst.begin(), p.e_cnst.end(), e_cnst);
+  std::copy(p.e_w.begin(), p.e_w.end(), e_weight);
+  std::copy(p.e_fl.begin(), p.e_fl.end(), e_flags);
+  std::copy(p.v_id.begin(), p.v_id.end(), v_id);
+  std::copy(p.v_eb.begin(), p.v_eb.end(), v_ebase);
+  std::copy(p.v_n.begin(), p.v_n.end(), v_nelem);
+  std::copy(p.v_p.begin(), p.v_p.end(), v_penalty);
+  std::copy(p.v_b.begin(), p.v_b.end(), v_bound);
+  std::copy(p.c_id.begin(), p.c_id.end(), c_id);
+  std::copy(p.c_b.begin(), p.c_b.end(), c_bound);
+  std::copy(p.c_fl.begin(), p.c_fl.end(), c_flags);
+  sizes6[0] = int64_t(p.e_id.size());
+  sizes6[1] = int64_t(p.v_id.size());
+  sizes6[2] = int64_t(p.c_id.size());
+  sizes6[3] = p.n_elem_total;
+  sizes6[4] = p.n_var_total;
+  sizes6[5] = p.n_cnst_total;
+  return 0;
+}
 int lmm_last_stats(lmm_sys* s, int64_t* counts4, double* ms4) {
   const auto& st = s->sys.last_stats();
   counts4[0] = st.rounds;

@@ -17,6 +17,8 @@
 #include "lmm_fb_kernels.hpp"
 #include "lmm_step_kernels.hpp"
 #include "lmm_maxmin_kernels.hpp"
+#include "lmm_resident_kernels.hpp"
+#include "lmm_scan.hpp"
 
 using namespace lmmdev;
 
@@ -72,6 +74,19 @@ struct lmmhip_ctx {
   std::vector<void*> act_allocs;
   int32_t* xnb_own = nullptr;  // the context's own exchange buffers (unsharded solves)
   double *xsum_own = nullptr, *xmin_own = nullptr;
+  // resident System mirror (lmmhip_res_*, lmm_resident_kernels.hpp): outlives uploads, freed with the
+  // context.  Mirror arrays keep their contents when they grow; scratch buffers do not.
+  struct Scr {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  ResDev res{};
+  int64_t res_capE = 0, res_capV = 0, res_capC = 0;
+  int64_t res_nE = 0, res_nV = 0, res_nC = 0;  // host table sizes of the last delta batch
+  bool res_flat = false;                        // the uploaded system came from lmmhip_res_flatten
+  int64_t res_flat_nv = 0;                      // variable slots covered by that flatten
+  Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
+      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp;
 };
 
 static void free_all(lmmhip_ctx* c) {
@@ -83,6 +98,7 @@ static void free_all(lmmhip_ctx* c) {
   c->xnb_own = nullptr;
   c->xsum_own = c->xmin_own = nullptr;
   c->fb_shard = false;
+  c->res_flat = false;
 }
 
 template <class T> static int dalloc(lmmhip_ctx* c, T** out, int64_t n) {
@@ -149,6 +165,19 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   if (c->own_stream && c->own_stream != c->stream)
     (void)hipStreamSynchronize(c->own_stream);
   free_all(c);
+  for (void* p : {(void*)c->res.e_cnst, (void*)c->res.e_w, (void*)c->res.e_fl, (void*)c->res.v_ebase,
+                  (void*)c->res.v_n, (void*)c->res.v_pen, (void*)c->res.v_bound, (void*)c->res.c_bound,
+                  (void*)c->res.c_fl})
+    if (p)
+      (void)hipFree(p);
+  for (lmmhip_ctx::Scr* b : {&c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+                             &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
+                             &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp})
+    if (b->p)
+      (void)hipFree(b->p);
+  for (lmmhip_ctx::Scr& b : c->rs_stage)
+    if (b.p)
+      (void)hipFree(b.p);
   for (void* p : c->act_allocs)
     (void)hipFree(p);
   if (c->h_ctl)
@@ -167,70 +196,16 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   return 0;
 }
 
-int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int64_t* var_ptr,
-                  const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
-                  const double* cnst_bound, const uint8_t* cnst_flags) {
-  if (!c)
-    return fail(LMMHIP_E_ARG, "null context");
-  if (nV < 0 || nC < 0 || nnz < 0 || nV >= (1 << 30) || nC >= (1 << 30) || nnz > INT32_MAX)
-    return fail(LMMHIP_E_ARG, "sizes out of range");
-  if (nV > 0 && (!var_ptr || !penalty || !var_bound))
-    return fail(LMMHIP_E_ARG, "null variable arrays");
-  if (nC > 0 && (!cnst_bound || !cnst_flags))
-    return fail(LMMHIP_E_ARG, "null constraint arrays");
-  if (nnz > 0 && (!cnst_idx || !weight))
-    return fail(LMMHIP_E_ARG, "null element arrays");
-  if (nV > 0 && (var_ptr[0] != 0 || var_ptr[nV] != nnz))
-    return fail(LMMHIP_E_ARG, "var_ptr must start at 0 and end at nnz");
-  // host-side validation + 32-bit offsets + CSC (constraint-major) mirror by a stable counting sort
-  std::vector<uint32_t> vp32(static_cast<size_t>(nV) + 1, 0);
-  for (int64_t v = 0; v < nV; v++) {
-    if (var_ptr[v + 1] < var_ptr[v])
-      return fail(LMMHIP_E_ARG, "var_ptr not monotone");
-    vp32[size_t(v) + 1] = uint32_t(var_ptr[v + 1]);
-  }
-  std::vector<uint32_t> cptr(static_cast<size_t>(nC) + 1, 0);
-  for (int64_t j = 0; j < nnz; j++) {
-    int32_t k = cnst_idx[j];
-    if (k < 0 || k >= nC)
-      return fail(LMMHIP_E_ARG, "cnst_idx out of range");
-    if (!(weight[j] > 0))
-      return fail(LMMHIP_E_ARG, "element weights must be > 0 (only active elements are flattened)");
-    cptr[size_t(k) + 1]++;
-  }
-  for (int64_t v = 0; v < nV; v++)
-    if (!(penalty[v] > 0))
-      return fail(LMMHIP_E_ARG, "penalties must be > 0 (only enabled variables are flattened)");
-  for (int64_t k = 0; k < nC; k++)
-    cptr[size_t(k) + 1] += cptr[size_t(k)];
-  std::vector<int32_t> cv(static_cast<size_t>(nnz));
-  std::vector<double> cw(static_cast<size_t>(nnz));
-  {
-    std::vector<uint32_t> cur(cptr.begin(), cptr.end() - 1);
-    for (int64_t v = 0; v < nV; v++)
-      for (int64_t j = var_ptr[v]; j < var_ptr[v + 1]; j++) {
-        uint32_t pos = cur[size_t(cnst_idx[j])]++;
-        cv[pos] = int32_t(v);
-        cw[pos] = weight[j];
-      }
-  }
-  // fair bottleneck CSC chunks (lmm_fb_kernels.hpp)
-  std::vector<int32_t> c_ch(static_cast<size_t>(nC) + 1, 0), ch_cnst;
-  std::vector<uint32_t> ch_beg;
-  for (int64_t k = 0; k < nC; k++) {
-    c_ch[size_t(k)] = int32_t(ch_cnst.size());
-    for (uint32_t b = cptr[size_t(k)]; b < cptr[size_t(k) + 1]; b += kFbChunk) {
-      ch_cnst.push_back(int32_t(k));
-      ch_beg.push_back(b);
-    }
-  }
-  const int64_t nch = int64_t(ch_cnst.size());
-  c_ch[size_t(nC)] = int32_t(nch);
-  std::vector<int32_t> iota(static_cast<size_t>(nV));
-  for (int64_t v = 0; v < nV; v++)
-    iota[size_t(v)] = int32_t(v);
-  HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));
+// Device buffers of one flattened system: allocated by alloc_flat, filled by the host upload
+// (lmmhip_upload) or on the device by the resident flatten (lmmhip_res_flatten).
+struct FlatBufs {
+  uint32_t *vp, *cp, *chb;
+  int32_t *csr_c, *csc_v, *cvar0, *chc, *cch;
+  double *csr_w, *csc_w, *pen, *vb, *cb;
+  uint8_t* cf;
+};
+
+static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_t nch, FlatBufs* o) {
   free_all(c);
   Dev& d = c->d;
   d.nV = int32_t(nV);
@@ -300,29 +275,6 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
     free_all(c);
     return LMMHIP_E_HIP;
   }
-  HIPCHK(hipMemcpyAsync(vp, vp32.data(), sizeof(uint32_t) * (nV + 1), hipMemcpyHostToDevice, c->stream));
-  if (nnz > 0) {
-    HIPCHK(hipMemcpyAsync(csr_c, cnst_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(csr_w, weight, sizeof(double) * nnz, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(csc_v, cv.data(), sizeof(int32_t) * nnz, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(csc_w, cw.data(), sizeof(double) * nnz, hipMemcpyHostToDevice, c->stream));
-  }
-  HIPCHK(hipMemcpyAsync(cp, cptr.data(), sizeof(uint32_t) * (nC + 1), hipMemcpyHostToDevice, c->stream));
-  if (nV > 0) {
-    HIPCHK(hipMemcpyAsync(pen, penalty, sizeof(double) * nV, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(vb, var_bound, sizeof(double) * nV, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(cvar0, iota.data(), sizeof(int32_t) * nV, hipMemcpyHostToDevice, c->stream));
-  }
-  if (nC > 0) {
-    HIPCHK(hipMemcpyAsync(cb, cnst_bound, sizeof(double) * nC, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(cf, cnst_flags, sizeof(uint8_t) * nC, hipMemcpyHostToDevice, c->stream));
-  }
-  if (nch > 0) {
-    HIPCHK(hipMemcpyAsync(chc, ch_cnst.data(), sizeof(int32_t) * nch, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(chb, ch_beg.data(), sizeof(uint32_t) * nch, hipMemcpyHostToDevice, c->stream));
-  }
-  HIPCHK(hipMemcpyAsync(cch, c_ch.data(), sizeof(int32_t) * (nC + 1), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));  // host staging vectors die at return
   d.nch = int32_t(nch);
   d.ch_cnst = chc;
   d.ch_beg = chb;
@@ -349,6 +301,13 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   d.cvar[2] = cvar2;
   d.crow[2] = crow2;
   d.ccol[2] = ccol2;
+  *o = FlatBufs{vp, cp, chb, csr_c, csc_v, cvar0, chc, cch, csr_w, csc_w, pen, vb, cb, cf};
+  return 0;
+}
+
+// Solver launch parameters from the system's shape + per-element usage; the system is then solvable.
+static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
+  Dev& d = c->d;
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
   const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
@@ -364,6 +323,103 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
   c->stats.n_cnst = nC;
   c->stats.nnz = nnz;
   return 0;
+}
+
+int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int64_t* var_ptr,
+                  const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
+                  const double* cnst_bound, const uint8_t* cnst_flags) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (nV < 0 || nC < 0 || nnz < 0 || nV >= (1 << 30) || nC >= (1 << 30) || nnz > INT32_MAX)
+    return fail(LMMHIP_E_ARG, "sizes out of range");
+  if (nV > 0 && (!var_ptr || !penalty || !var_bound))
+    return fail(LMMHIP_E_ARG, "null variable arrays");
+  if (nC > 0 && (!cnst_bound || !cnst_flags))
+    return fail(LMMHIP_E_ARG, "null constraint arrays");
+  if (nnz > 0 && (!cnst_idx || !weight))
+    return fail(LMMHIP_E_ARG, "null element arrays");
+  if (nV > 0 && (var_ptr[0] != 0 || var_ptr[nV] != nnz))
+    return fail(LMMHIP_E_ARG, "var_ptr must start at 0 and end at nnz");
+  // host-side validation + 32-bit offsets + CSC (constraint-major) mirror by a stable counting sort
+  std::vector<uint32_t> vp32(static_cast<size_t>(nV) + 1, 0);
+  for (int64_t v = 0; v < nV; v++) {
+    if (var_ptr[v + 1] < var_ptr[v])
+      return fail(LMMHIP_E_ARG, "var_ptr not monotone");
+    vp32[size_t(v) + 1] = uint32_t(var_ptr[v + 1]);
+  }
+  std::vector<uint32_t> cptr(static_cast<size_t>(nC) + 1, 0);
+  for (int64_t j = 0; j < nnz; j++) {
+    int32_t k = cnst_idx[j];
+    if (k < 0 || k >= nC)
+      return fail(LMMHIP_E_ARG, "cnst_idx out of range");
+    if (!(weight[j] > 0))
+      return fail(LMMHIP_E_ARG, "element weights must be > 0 (only active elements are flattened)");
+    cptr[size_t(k) + 1]++;
+  }
+  for (int64_t v = 0; v < nV; v++)
+    if (!(penalty[v] > 0))
+      return fail(LMMHIP_E_ARG, "penalties must be > 0 (only enabled variables are flattened)");
+  for (int64_t k = 0; k < nC; k++)
+    cptr[size_t(k) + 1] += cptr[size_t(k)];
+  std::vector<int32_t> cv(static_cast<size_t>(nnz));
+  std::vector<double> cw(static_cast<size_t>(nnz));
+  {
+    std::vector<uint32_t> cur(cptr.begin(), cptr.end() - 1);
+    for (int64_t v = 0; v < nV; v++)
+      for (int64_t j = var_ptr[v]; j < var_ptr[v + 1]; j++) {
+        uint32_t pos = cur[size_t(cnst_idx[j])]++;
+        cv[pos] = int32_t(v);
+        cw[pos] = weight[j];
+      }
+  }
+  // fair bottleneck CSC chunks (lmm_fb_kernels.hpp)
+  std::vector<int32_t> c_ch(static_cast<size_t>(nC) + 1, 0), ch_cnst;
+  std::vector<uint32_t> ch_beg;
+  for (int64_t k = 0; k < nC; k++) {
+    c_ch[size_t(k)] = int32_t(ch_cnst.size());
+    for (uint32_t b = cptr[size_t(k)]; b < cptr[size_t(k) + 1]; b += kFbChunk) {
+      ch_cnst.push_back(int32_t(k));
+      ch_beg.push_back(b);
+    }
+  }
+  const int64_t nch = int64_t(ch_cnst.size());
+  c_ch[size_t(nC)] = int32_t(nch);
+  std::vector<int32_t> iota(static_cast<size_t>(nV));
+  for (int64_t v = 0; v < nV; v++)
+    iota[size_t(v)] = int32_t(v);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  FlatBufs fb;
+  if (int rc = alloc_flat(c, nV, nC, nnz, nch, &fb))
+    return rc;
+  uint32_t *vp = fb.vp, *cp = fb.cp, *chb = fb.chb;
+  int32_t *csr_c = fb.csr_c, *csc_v = fb.csc_v, *cvar0 = fb.cvar0, *chc = fb.chc, *cch = fb.cch;
+  double *csr_w = fb.csr_w, *csc_w = fb.csc_w, *pen = fb.pen, *vb = fb.vb, *cb = fb.cb;
+  uint8_t* cf = fb.cf;
+  HIPCHK(hipMemcpyAsync(vp, vp32.data(), sizeof(uint32_t) * (nV + 1), hipMemcpyHostToDevice, c->stream));
+  if (nnz > 0) {
+    HIPCHK(hipMemcpyAsync(csr_c, cnst_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(csr_w, weight, sizeof(double) * nnz, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(csc_v, cv.data(), sizeof(int32_t) * nnz, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(csc_w, cw.data(), sizeof(double) * nnz, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipMemcpyAsync(cp, cptr.data(), sizeof(uint32_t) * (nC + 1), hipMemcpyHostToDevice, c->stream));
+  if (nV > 0) {
+    HIPCHK(hipMemcpyAsync(pen, penalty, sizeof(double) * nV, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(vb, var_bound, sizeof(double) * nV, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(cvar0, iota.data(), sizeof(int32_t) * nV, hipMemcpyHostToDevice, c->stream));
+  }
+  if (nC > 0) {
+    HIPCHK(hipMemcpyAsync(cb, cnst_bound, sizeof(double) * nC, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(cf, cnst_flags, sizeof(uint8_t) * nC, hipMemcpyHostToDevice, c->stream));
+  }
+  if (nch > 0) {
+    HIPCHK(hipMemcpyAsync(chc, ch_cnst.data(), sizeof(int32_t) * nch, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(chb, ch_beg.data(), sizeof(uint32_t) * nch, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipMemcpyAsync(cch, c_ch.data(), sizeof(int32_t) * (nC + 1), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));  // host staging vectors die at return
+  return finish_flat(c, nV, nC, nnz);
 }
 
 int lmmhip_update_vars(lmmhip_ctx* c, const double* penalty, const double* var_bound) {
@@ -394,6 +450,296 @@ int lmmhip_update_cnsts(lmmhip_ctx* c, const double* cnst_bound) {
   return 0;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// resident System mirror + delta log (lmm_resident_kernels.hpp)
+// ---------------------------------------------------------------------------------------------
+template <class T> static int scratch(lmmhip_ctx* c, lmmhip_ctx::Scr& b, int64_t n, T** out) {
+  const size_t need = size_t(n > 0 ? n : 1) * sizeof(T);
+  if (b.bytes < need) {
+    HIPCHK(hipStreamSynchronize(c->stream));  // the old buffer may still be read by queued work
+    if (b.p)
+      HIPCHK(hipFree(b.p));
+    const size_t bytes = std::max(need, b.bytes + b.bytes / 2);
+    b.p = nullptr;
+    b.bytes = 0;
+    HIPCHK(hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+  }
+  *out = static_cast<T*>(b.p);
+  return 0;
+}
+
+// Grow a mirror array to `cap` elements, keeping the first `used` ones.
+template <class T> static int res_grow(lmmhip_ctx* c, T** p, int64_t used, int64_t cap) {
+  T* q = nullptr;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&q), size_t(cap > 0 ? cap : 1) * sizeof(T)));
+  HIPCHK(hipMemsetAsync(q, 0, size_t(cap > 0 ? cap : 1) * sizeof(T), c->stream));
+  if (*p && used > 0)
+    HIPCHK(hipMemcpyAsync(q, *p, size_t(used) * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (*p)
+    HIPCHK(hipFree(*p));
+  *p = q;
+  return 0;
+}
+
+template <class T> static int stage(lmmhip_ctx* c, int slot, const T* host, int64_t n, const T** out) {
+  T* d = nullptr;
+  if (int rc = scratch(c, c->rs_stage[slot], n, &d))
+    return rc;
+  if (n > 0)
+    HIPCHK(hipMemcpyAsync(d, host, size_t(n) * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  *out = d;
+  return 0;
+}
+
+static int dev_scan(lmmhip_ctx* c, const int64_t* in, int64_t* out, int64_t n) {
+  size_t tb = 0;
+  HIPCHK(scan_i64(nullptr, tb, in, out, n, c->stream));
+  uint8_t* t = nullptr;
+  if (int rc = scratch(c, c->rs_tmp, int64_t(tb), &t))
+    return rc;
+  HIPCHK(scan_i64(t, tb, in, out, n, c->stream));
+  return 0;
+}
+
+static int64_t read_i64(lmmhip_ctx* c, const int64_t* dptr, int* rc) {
+  int64_t h = 0;
+  if (hipMemcpyAsync(&h, dptr, sizeof(h), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    *rc = fail(LMMHIP_E_HIP, "resident flatten: reading a count back failed");
+  return h;
+}
+
+#define RS_LAUNCH(kern, n, ...)                                                                     \
+  do {                                                                                              \
+    hipLaunchKernelGGL(kern, dim3(grid_for((n) + 1, kBlock)), dim3(kBlock), 0, c->stream, __VA_ARGS__); \
+    HIPCHK(hipGetLastError());                                                                      \
+  } while (0)
+
+extern "C" {
+
+int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, int64_t n_cnst_total, int64_t ne,
+                     const int64_t* e_id, const int32_t* e_cnst, const double* e_weight, const uint8_t* e_flags,
+                     int64_t nv, const int32_t* v_id, const int64_t* v_ebase, const int32_t* v_nelem,
+                     const double* v_penalty, const double* v_bound, int64_t nc, const int32_t* c_id,
+                     const double* c_bound, const uint8_t* c_flags) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (n_elem_total < 0 || n_var_total < 0 || n_cnst_total < 0 || ne < 0 || nv < 0 || nc < 0 ||
+      n_var_total >= (1 << 30) || n_cnst_total >= (1 << 30) || n_elem_total > INT32_MAX)
+    return fail(LMMHIP_E_ARG, "resident sizes out of range");
+  if ((ne && (!e_id || !e_cnst || !e_weight || !e_flags)) ||
+      (nv && (!v_id || !v_ebase || !v_nelem || !v_penalty || !v_bound)) || (nc && (!c_id || !c_bound || !c_flags)))
+    return fail(LMMHIP_E_ARG, "null delta arrays");
+  // host-side validation: every record lands inside the tables, every slab inside the element table
+  for (int64_t i = 0; i < ne; i++)
+    if (e_id[i] < 0 || e_id[i] >= n_elem_total || e_cnst[i] < -1 || e_cnst[i] >= n_cnst_total)
+      return fail(LMMHIP_E_ARG, "element delta out of range");
+  for (int64_t i = 0; i < nv; i++)
+    if (v_id[i] < 0 || v_id[i] >= n_var_total || v_nelem[i] < 0 || v_ebase[i] < 0 ||
+        v_ebase[i] + v_nelem[i] > n_elem_total)
+      return fail(LMMHIP_E_ARG, "variable delta out of range");
+  for (int64_t i = 0; i < nc; i++)
+    if (c_id[i] < 0 || c_id[i] >= n_cnst_total)
+      return fail(LMMHIP_E_ARG, "constraint delta out of range");
+  HIPCHK(hipSetDevice(c->device));
+  ResDev& r = c->res;
+  if (n_elem_total > c->res_capE) {
+    const int64_t cap = std::max(n_elem_total, c->res_capE + c->res_capE / 2);
+    int rc = res_grow(c, &r.e_cnst, c->res_nE, cap) | res_grow(c, &r.e_w, c->res_nE, cap) |
+             res_grow(c, &r.e_fl, c->res_nE, cap);
+    if (rc)
+      return rc;
+    c->res_capE = cap;
+  }
+  if (n_var_total > c->res_capV) {
+    const int64_t cap = std::max(n_var_total, c->res_capV + c->res_capV / 2);
+    int rc = res_grow(c, &r.v_ebase, c->res_nV, cap) | res_grow(c, &r.v_n, c->res_nV, cap) |
+             res_grow(c, &r.v_pen, c->res_nV, cap) | res_grow(c, &r.v_bound, c->res_nV, cap);
+    if (rc)
+      return rc;
+    c->res_capV = cap;
+  }
+  if (n_cnst_total > c->res_capC) {
+    const int64_t cap = std::max(n_cnst_total, c->res_capC + c->res_capC / 2);
+    int rc = res_grow(c, &r.c_bound, c->res_nC, cap) | res_grow(c, &r.c_fl, c->res_nC, cap);
+    if (rc)
+      return rc;
+    c->res_capC = cap;
+  }
+  c->res_nE = std::max(c->res_nE, n_elem_total);
+  c->res_nV = std::max(c->res_nV, n_var_total);
+  c->res_nC = std::max(c->res_nC, n_cnst_total);
+  if (ne) {
+    const int64_t* did;
+    const int32_t* dcn;
+    const double* dw;
+    const uint8_t* dfl;
+    int rc = stage(c, 0, e_id, ne, &did) | stage(c, 1, e_cnst, ne, &dcn) | stage(c, 2, e_weight, ne, &dw) |
+             stage(c, 3, e_flags, ne, &dfl);
+    if (rc)
+      return rc;
+    RS_LAUNCH(rs_apply_e, ne, ne, did, dcn, dw, dfl, r);
+  }
+  if (nv) {
+    const int32_t* did;
+    const int64_t* deb;
+    const int32_t* dn;
+    const double *dp, *db;
+    int rc = stage(c, 4, v_id, nv, &did) | stage(c, 5, v_ebase, nv, &deb) | stage(c, 6, v_nelem, nv, &dn) |
+             stage(c, 7, v_penalty, nv, &dp) | stage(c, 8, v_bound, nv, &db);
+    if (rc)
+      return rc;
+    RS_LAUNCH(rs_apply_v, nv, nv, did, deb, dn, dp, db, r);
+  }
+  if (nc) {
+    const int32_t* did;
+    const double* db;
+    const uint8_t* dfl;
+    int rc = stage(c, 9, c_id, nc, &did) | stage(c, 10, c_bound, nc, &db) | stage(c, 11, c_flags, nc, &dfl);
+    if (rc)
+      return rc;
+    RS_LAUNCH(rs_apply_c, nc, nc, did, db, dfl, r);
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));  // host delta arrays are borrowed for the call only
+  return 0;
+}
+
+int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, double precision, int64_t* counts3) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (n_list < 0 || (n_list && !cnst_list))
+    return fail(LMMHIP_E_ARG, "bad constraint list");
+  for (int64_t i = 0; i < n_list; i++)
+    if (cnst_list[i] < 0 || cnst_list[i] >= c->res_nC)
+      return fail(LMMHIP_E_ARG, "listed constraint is not in the resident mirror");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const ResDev& r = c->res;
+  const int64_t nl = n_list, nvs = c->res_nV;
+  int32_t *pos, *list;
+  uint8_t *lpart, *vrst;
+  int64_t *lany, *dcl, *cdeg, *cptr, *vm, *dv, *rl, *ro;
+  int rc = scratch(c, c->rs_pos, c->res_nC, &pos) | scratch(c, c->rs_list, nl, &list) |
+           scratch(c, c->rs_lpart, nl, &lpart) | scratch(c, c->rs_lany, nl + 1, &lany) |
+           scratch(c, c->rs_dcl, nl + 1, &dcl) | scratch(c, c->rs_cdeg, nl + 1, &cdeg) |
+           scratch(c, c->rs_cptr, nl + 1, &cptr) | scratch(c, c->rs_vrst, nvs, &vrst) |
+           scratch(c, c->rs_vm, nvs + 1, &vm) | scratch(c, c->rs_dv, nvs + 1, &dv) |
+           scratch(c, c->rs_rl, nvs + 1, &rl) | scratch(c, c->rs_ro, nvs + 1, &ro);
+  if (rc)
+    return rc;
+  if (nl)
+    HIPCHK(hipMemcpyAsync(list, cnst_list, size_t(nl) * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  if (c->res_nC)
+    HIPCHK(hipMemsetAsync(pos, 0xFF, size_t(c->res_nC) * sizeof(int32_t), c->stream));
+  HIPCHK(hipMemsetAsync(cdeg, 0, size_t(nl + 1) * sizeof(int64_t), c->stream));
+  RS_LAUNCH(rs_pos, nl, nl, list, r, precision, pos, lpart, lany);
+  RS_LAUNCH(rs_mark, nvs, nvs, r, pos, lpart, lany, vrst, vm);
+  if ((rc = dev_scan(c, lany, dcl, nl + 1)))
+    return rc;
+  RS_LAUNCH(rs_rowlen, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
+  if ((rc = dev_scan(c, vm, dv, nvs + 1)) || (rc = dev_scan(c, rl, ro, nvs + 1)) ||
+      (rc = dev_scan(c, cdeg, cptr, nl + 1)))
+    return rc;
+  const int64_t nC = read_i64(c, dcl + nl, &rc);
+  const int64_t nV = read_i64(c, dv + nvs, &rc);
+  const int64_t nnz = read_i64(c, ro + nvs, &rc);
+  if (rc)
+    return rc;
+  if (nnz > INT32_MAX)
+    return fail(LMMHIP_E_ARG, "resident flatten: more than 2^31 active elements");
+  FlatBufs fb;
+  if ((rc = alloc_flat(c, nV, nC, nnz, 0, &fb)))
+    return rc;
+  c->res_flat = true;
+  c->res_flat_nv = nvs;
+  int32_t *rowid, *kidx, *skey, *sval;
+  rc = scratch(c, c->rs_rowid, nnz, &rowid) | scratch(c, c->rs_kidx, nnz, &kidx) |
+       scratch(c, c->rs_skey, nnz, &skey) | scratch(c, c->rs_sval, nnz, &sval);
+  if (rc)
+    return rc;
+  RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, fb.cb, fb.cf);
+  RS_LAUNCH(rs_write, nvs, nvs, r, pos, lany, dcl, vm, dv, ro, fb.vp, fb.csr_c, fb.csr_w, fb.pen, fb.vb, fb.cvar0,
+            rowid, kidx);
+  const uint32_t nnz32 = uint32_t(nnz);
+  HIPCHK(hipMemcpyAsync(fb.vp + nV, &nnz32, sizeof(nnz32), hipMemcpyHostToDevice, c->stream));
+  RS_LAUNCH(rs_ptr32, nC, nC, cptr, fb.cp);
+  HIPCHK(hipMemsetAsync(fb.cch, 0, size_t(nC + 1) * sizeof(int32_t), c->stream));  // no FB chunks
+  if (nnz) {
+    int bits = 1;
+    while (bits < 31 && (int64_t(1) << bits) < nC)
+      bits++;
+    size_t tb = 0;
+    HIPCHK(sort_pairs_i32(nullptr, tb, fb.csr_c, skey, kidx, sval, nnz, bits, c->stream));
+    uint8_t* t = nullptr;
+    if ((rc = scratch(c, c->rs_tmp, int64_t(tb), &t)))
+      return rc;
+    HIPCHK(sort_pairs_i32(t, tb, fb.csr_c, skey, kidx, sval, nnz, bits, c->stream));
+    RS_LAUNCH(rs_csc, nnz, nnz, sval, rowid, fb.csr_w, fb.csc_v, fb.csc_w);
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));  // before the host's list buffer is released
+  if ((rc = finish_flat(c, nV, nC, nnz)))
+    return rc;
+  if (counts3) {
+    counts3[0] = nV;
+    counts3[1] = nC;
+    counts3[2] = nnz;
+  }
+  return 0;
+}
+
+int lmmhip_flat_download(lmmhip_ctx* c, int64_t* counts3, uint32_t* var_ptr, int32_t* csr_c, double* csr_w,
+                         uint32_t* cnst_ptr, int32_t* csc_v, double* csc_w, double* penalty, double* var_bound,
+                         double* cnst_bound, uint8_t* cnst_flags) {
+  if (!c || !c->uploaded)
+    return fail(LMMHIP_E_STATE, "no system uploaded");
+  if (!counts3)
+    return fail(LMMHIP_E_ARG, "null counts");
+  const Dev& d = c->d;
+  counts3[0] = d.nV;
+  counts3[1] = d.nC;
+  counts3[2] = d.nnz;
+  HIPCHK(hipSetDevice(c->device));
+  auto get = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (dst && bytes)
+      HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  };
+  int rc = get(var_ptr, d.var_ptr, sizeof(uint32_t) * (size_t(d.nV) + 1)) |
+           get(csr_c, d.csr_c, sizeof(int32_t) * size_t(d.nnz)) | get(csr_w, d.csr_w, sizeof(double) * size_t(d.nnz)) |
+           get(cnst_ptr, d.cnst_ptr, sizeof(uint32_t) * (size_t(d.nC) + 1)) |
+           get(csc_v, d.csc_v, sizeof(int32_t) * size_t(d.nnz)) | get(csc_w, d.csc_w, sizeof(double) * size_t(d.nnz)) |
+           get(penalty, d.pen, sizeof(double) * size_t(d.nV)) | get(var_bound, d.vbound, sizeof(double) * size_t(d.nV)) |
+           get(cnst_bound, d.cbound, sizeof(double) * size_t(d.nC)) | get(cnst_flags, d.cflags, size_t(d.nC));
+  if (rc)
+    return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_res_values(lmmhip_ctx* c, int64_t n, double* values, uint8_t* reset) {
+  if (!c || !c->uploaded || !c->res_flat)
+    return fail(LMMHIP_E_STATE, "no resident flatten to read values from");
+  if (n != c->res_flat_nv || (n && (!values || !reset)))
+    return fail(LMMHIP_E_ARG, "values: n must be the variable slot count of the last resident flatten");
+  HIPCHK(hipSetDevice(c->device));
+  double* vout = nullptr;
+  if (int rc = scratch(c, c->rs_vout, n, &vout))
+    return rc;
+  const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
+  const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
+  if (n) {
+    RS_LAUNCH(rs_values, n, n, vm, dv, c->d.x, vout);
+    HIPCHK(hipMemcpyAsync(values, vout, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(reset, c->rs_vrst.p, size_t(n), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 int lmmhip_set_profiling(lmmhip_ctx* c, int on) {
   if (!c)
     return fail(LMMHIP_E_ARG, "null context");
@@ -410,6 +756,8 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
     return fail(LMMHIP_E_STATE, "solve before upload");
   if (kind != LMMHIP_KIND_MAXMIN && kind != LMMHIP_KIND_FAIR_BOTTLENECK)
     return fail(LMMHIP_E_ARG, "unknown solver kind");
+  if (kind == LMMHIP_KIND_FAIR_BOTTLENECK && c->res_flat)
+    return fail(LMMHIP_E_STATE, "a resident flatten builds a max-min system (no fair-bottleneck chunks)");
   HIPCHK(hipSetDevice(c->device));
   for (int i = 0; i < 8; i++) {
     c->stats.kernel_ms[i] = 0;

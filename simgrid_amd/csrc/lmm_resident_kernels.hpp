@@ -1,0 +1,216 @@
+// lmm_resident_kernels.hpp — device-resident System mirror and its delta log.
+//
+// The host System (lmm_system.cpp) keeps the reference's bookkeeping (maxmin.cpp:205-323, 703-888:
+// expand / expand_add / variable_free / update_* and the concurrency staging).  Instead of flattening
+// the active part of the system on the host before every solve (O(nnz) host work + a full PCIe upload),
+// resident mode mirrors the host's element / variable / constraint records in HBM, ships only the
+// records a mutation touched (the delta log: rs_apply_*), and rebuilds the solver's CSR / CSC on the
+// device with the exact selection rules of System::flatten_maxmin (lmm_system.cpp, which follows
+// lmm_solve's init, maxmin.cpp:509-540):
+//   * listed constraint c (active set, or the modified set in selective mode), in list order, is part
+//     of the system iff bound > bound * prec and an enabled element with w > 0 lies on it;
+//   * a variable is part of the system iff it has such an element; its CSR row is its slab in slot
+//     order, keeping the elements with w > 0 on a constraint that is part of the system;
+//   * every variable with an enabled element on a listed constraint has its value reset to 0;
+//   * dense constraint ids follow the list order, dense variable ids ascending variable ids, and the
+//     CSC lists a constraint's elements in CSR order (stable radix sort) — the very arrays the host
+//     path uploads, so both paths give bit-identical solves (tests/test_gpu_resident.py).
+// All kernels are element-wise / per-slab streams (HBM-bound, no atomics on the hot arrays except the
+// per-constraint degree counts).
+#pragma once
+
+#include "lmm_dev.hpp"
+
+namespace lmmdev {
+
+// Resident mirror (host ids; capacities grow on demand, contents survive growth).
+struct ResDev {
+  int32_t* e_cnst;   // [capE] constraint of element slot e
+  double* e_w;       // [capE] consumption weight
+  uint8_t* e_fl;     // [capE] bit0: in its constraint's enabled list
+  int64_t* v_ebase;  // [capV] first element slot of the variable's slab
+  int32_t* v_n;      // [capV] elements in use (0 for a dead variable)
+  double* v_pen;     // [capV] sharing penalty
+  double* v_bound;   // [capV] bound (-1 = none)
+  double* c_bound;   // [capC]
+  uint8_t* c_fl;     // [capC] bit0: FATPIPE
+};
+
+constexpr uint8_t kResElemEnabled = 1;
+constexpr uint8_t kResCnstFatpipe = 1;
+
+__global__ void __launch_bounds__(kBlock)
+    rs_apply_e(int64_t n, const int64_t* __restrict__ id, const int32_t* __restrict__ cn,
+               const double* __restrict__ w, const uint8_t* __restrict__ fl, ResDev r) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const int64_t e = id[i];
+    r.e_cnst[e] = cn[i];
+    r.e_w[e] = w[i];
+    r.e_fl[e] = fl[i];
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+    rs_apply_v(int64_t n, const int32_t* __restrict__ id, const int64_t* __restrict__ eb,
+               const int32_t* __restrict__ ne, const double* __restrict__ pen, const double* __restrict__ bnd,
+               ResDev r) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const int32_t v = id[i];
+    r.v_ebase[v] = eb[i];
+    r.v_n[v] = ne[i];
+    r.v_pen[v] = pen[i];
+    r.v_bound[v] = bnd[i];
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+    rs_apply_c(int64_t n, const int32_t* __restrict__ id, const double* __restrict__ b,
+               const uint8_t* __restrict__ fl, ResDev r) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    r.c_bound[id[i]] = b[i];
+    r.c_fl[id[i]] = fl[i];
+  }
+}
+
+// pos[c] = list position of listed constraint c (pos pre-set to -1); lpart[i] = bound > bound * prec
+// (maxmin.cpp:523-525).  lany[i] (int64, scanned later) is cleared here.
+__global__ void __launch_bounds__(kBlock)
+    rs_pos(int64_t nl, const int32_t* __restrict__ list, ResDev r, double prec, int32_t* pos, uint8_t* lpart,
+           int64_t* lany) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i <= nl; i += int64_t(gridDim.x) * kBlock) {
+    lany[i] = 0;
+    if (i == nl)
+      break;
+    const int32_t c = list[i];
+    pos[c] = int32_t(i);
+    const double b = r.c_bound[c];
+    lpart[i] = b > b * prec;
+  }
+}
+
+// Per variable slot: value reset (enabled element on a listed constraint, maxmin.cpp:509-514) and
+// membership (such an element with w > 0 on a part constraint, :527-538); marks the constraints that
+// have one (lany, plain stores of 1: the race is benign).
+__global__ void __launch_bounds__(kBlock)
+    rs_mark(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const uint8_t* __restrict__ lpart,
+            int64_t* lany, uint8_t* vrst, int64_t* vm) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
+    if (v == nv) {
+      vm[v] = 0;  // scan sentinel
+      break;
+    }
+    uint8_t rst = 0;
+    int64_t mk = 0;
+    const int64_t b = r.v_ebase[v];
+    const int n = r.v_n[v];
+    for (int i = 0; i < n; i++) {
+      if (!(r.e_fl[b + i] & kResElemEnabled))
+        continue;
+      const int32_t p = pos[r.e_cnst[b + i]];
+      if (p < 0)
+        continue;
+      rst = 1;
+      if (r.e_w[b + i] > 0 && lpart[p]) {
+        mk = 1;
+        lany[p] = 1;
+      }
+    }
+    vrst[v] = rst;
+    vm[v] = mk;
+  }
+}
+
+// Row lengths of the member variables (elements with w > 0 on a part constraint, in slot order, no
+// enabled-list test: System::flatten_maxmin) and the per-constraint degrees (dense ids = dcl).
+__global__ void __launch_bounds__(kBlock)
+    rs_rowlen(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
+              const int64_t* __restrict__ dcl, const int64_t* __restrict__ vm, int64_t* rl, int64_t* cdeg) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
+    if (v == nv) {
+      rl[v] = 0;
+      break;
+    }
+    int64_t cnt = 0;
+    if (vm[v]) {
+      const int64_t b = r.v_ebase[v];
+      const int n = r.v_n[v];
+      for (int i = 0; i < n; i++) {
+        const int32_t p = pos[r.e_cnst[b + i]];
+        if (p >= 0 && lany[p] && r.e_w[b + i] > 0) {
+          cnt++;
+          atomicAdd(reinterpret_cast<unsigned long long*>(cdeg + dcl[p]), 1ull);
+        }
+      }
+    }
+    rl[v] = cnt;
+  }
+}
+
+// Dense constraint records in list order.
+__global__ void __launch_bounds__(kBlock)
+    rs_cmeta(int64_t nl, const int32_t* __restrict__ list, ResDev r, const int64_t* __restrict__ lany,
+             const int64_t* __restrict__ dcl, double* cbound, uint8_t* cflags) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nl; i += int64_t(gridDim.x) * kBlock) {
+    if (!lany[i])
+      continue;
+    const int32_t c = list[i];
+    cbound[dcl[i]] = r.c_bound[c];
+    cflags[dcl[i]] = (r.c_fl[c] & kResCnstFatpipe) ? 1 : 0;
+  }
+}
+
+// CSR rows, per-variable arrays and the dense -> slot map.
+__global__ void __launch_bounds__(kBlock)
+    rs_write(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
+             const int64_t* __restrict__ dcl, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
+             const int64_t* __restrict__ ro, uint32_t* var_ptr, int32_t* csr_c, double* csr_w, double* pen,
+             double* vbound, int32_t* cvar0, int32_t* rowid, int32_t* kidx) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
+    if (!vm[v])
+      continue;
+    const int64_t i = dv[v];
+    int64_t k = ro[v];
+    var_ptr[i] = uint32_t(k);
+    pen[i] = r.v_pen[v];
+    vbound[i] = r.v_bound[v];
+    cvar0[i] = int32_t(i);
+    const int64_t b = r.v_ebase[v];
+    const int n = r.v_n[v];
+    for (int j = 0; j < n; j++) {
+      const int32_t p = pos[r.e_cnst[b + j]];
+      if (p >= 0 && lany[p] && r.e_w[b + j] > 0) {
+        csr_c[k] = int32_t(dcl[p]);
+        csr_w[k] = r.e_w[b + j];
+        rowid[k] = int32_t(i);
+        kidx[k] = int32_t(k);
+        k++;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+    rs_csc(int64_t nnz, const int32_t* __restrict__ sk, const int32_t* __restrict__ rowid,
+           const double* __restrict__ csr_w, int32_t* csc_v, double* csc_w) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < nnz; j += int64_t(gridDim.x) * kBlock) {
+    const int32_t k = sk[j];
+    csc_v[j] = rowid[k];
+    csc_w[j] = csr_w[k];
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) rs_ptr32(int64_t n, const int64_t* __restrict__ in, uint32_t* out) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i <= n; i += int64_t(gridDim.x) * kBlock)
+    out[i] = uint32_t(in[i]);
+}
+
+// Per variable slot after the solve: the solved value of a member, 0 for the others (only slots with
+// vrst set are written back by the host).
+__global__ void __launch_bounds__(kBlock)
+    rs_values(int64_t nv, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
+              const double* __restrict__ x, double* out) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock)
+    out[v] = vm[v] ? x[dv[v]] : 0.0;
+}
+
+}  // namespace lmmdev

@@ -72,6 +72,7 @@ void System::en_push_front(Id c, Id e) {
   k.en_head = e;
   x.where = 1;
   k.n_en++;
+  touch_e(e);
 }
 
 void System::dis_push_back(Id c, Id e) {
@@ -86,6 +87,7 @@ void System::dis_push_back(Id c, Id e) {
   k.dis_tail = e;
   x.where = 2;
   k.n_dis++;
+  touch_e(e);
 }
 
 void System::elem_unlink(Id e) {
@@ -106,6 +108,7 @@ void System::elem_unlink(Id e) {
   (x.where == 1 ? k.n_en : k.n_dis)--;
   x.prev = x.next = kNone;
   x.where = 0;
+  touch_e(e);
 }
 
 void System::vset_push_front(Id v) {
@@ -247,6 +250,7 @@ Id System::constraint_new(void* id, double bound) {
   k.conc_limit = concurrency_limit;
   cnsts_.push_back(k);
   flat_valid_ = false;
+  touch_c(Id(cnsts_.size() - 1));
   return Id(cnsts_.size() - 1);
 }
 
@@ -283,6 +287,7 @@ Id System::variable_new(void* id, double penalty, double bound, size_t n_cnst) {
     vset_push_back(v);
   n_live_vars_++;
   flat_valid_ = false;
+  touch_v(v);
   return v;
 }
 
@@ -318,6 +323,7 @@ void System::var_free(Id v) {
   }
   rr.n_elems = 0;
   rr.live = false;
+  touch_v(v);
   free_var_ids_.push_back(v);
   n_live_vars_--;
 }
@@ -364,6 +370,8 @@ void System::expand(Id c, Id v, double w) {
   x.weight = w;
   x.cnst = c;
   x.var = v;
+  touch_e(e);
+  touch_v(v);
   if (r->penalty != 0) {
     en_push_front(c, e);
     inc_conc(e);
@@ -400,6 +408,7 @@ void System::expand_add(Id c, Id v, double w) {
     elems_[found].weight += w;
   else
     elems_[found].weight = std::max(elems_[found].weight, w);
+  touch_e(found);
   if (vars_[v].penalty != 0) {
     if (cnsts_[c].slack() < elems_[found].concurrency()) {
       double pen = vars_[v].penalty;
@@ -420,6 +429,7 @@ void System::enable_var(Id v) {
   VarRec& r = vars_[v];
   r.penalty = r.staged;
   r.staged = 0;
+  touch_v(v);
   vset_erase(v);
   vset_push_front(v);
   for (int i = 0; i < r.n_elems; i++) {
@@ -449,6 +459,7 @@ void System::disable_var(Id v) {
   r.penalty = 0.0;
   r.staged = 0.0;
   r.value = 0.0;
+  touch_v(v);
   flat_valid_ = false;
 }
 
@@ -475,6 +486,7 @@ void System::update_variable_bound(Id v, double bound) {
   modified_ = true;
   flat_valid_ = false;
   vars_[v].bound = bound;
+  touch_v(v);
   if (vars_[v].n_elems)
     update_modified_set(elems_[vars_[v].ebase].cnst);
 }
@@ -497,6 +509,7 @@ void System::update_variable_penalty(Id v, double penalty) {
     disable_var(v);
   } else {
     r.penalty = penalty;
+    touch_v(v);
   }
 }
 
@@ -505,6 +518,7 @@ void System::update_constraint_bound(Id c, double bound) {
   flat_valid_ = false;
   update_modified_set(c);
   cnsts_[c].bound = bound;
+  touch_c(c);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -800,6 +814,11 @@ void System::finish_solve() {
 // solve
 // ------------------------------------------------------------------------------------------
 void System::prepare() {
+  if (resident_ && kind_ == SolverKind::MAXMIN) {
+    prepare_resident();
+    return;
+  }
+  res_prepared_ = false;
   auto t0 = std::chrono::steady_clock::now();
   flat_ = Flat();
   flatten_into(flat_);
@@ -831,12 +850,184 @@ void System::device_solve() {
 }
 
 void System::fetch() {
+  if (res_prepared_) {
+    fetch_resident();
+    return;
+  }
   auto t0 = std::chrono::steady_clock::now();
   xbuf_.resize(flat_.dense_vars.size());
   int rc = lmmhip_get_values(ctx(), xbuf_.data());
   if (rc)
     fatal(std::string("fetch failed: ") + lmmhip_last_error());
   scatter_values(xbuf_.data());
+  stats_.fetch_ms = ms_since(t0);
+  finish_solve();
+}
+
+// ------------------------------------------------------------------------------------------
+// resident mode: delta log + device flatten (lmm_resident_kernels.hpp)
+// ------------------------------------------------------------------------------------------
+static void log_id(std::vector<uint8_t>& flag, std::vector<Id>& ids, Id i, size_t table) {
+  if (flag.size() < table)
+    flag.resize(std::max(table, flag.size() * 2), 0);
+  if (!flag[size_t(i)]) {
+    flag[size_t(i)] = 1;
+    ids.push_back(i);
+  }
+}
+
+void System::touch_e(Id e) {
+  if (resident_ && !res_full_)
+    log_id(res_de_, res_le_, e, elems_.size());
+}
+void System::touch_v(Id v) {
+  if (resident_ && !res_full_)
+    log_id(res_dv_, res_lv_, v, vars_.size());
+}
+void System::touch_c(Id c) {
+  if (resident_ && !res_full_)
+    log_id(res_dc_, res_lc_, c, cnsts_.size());
+}
+
+void System::set_resident(bool on) {
+  resident_ = on;
+  res_full_ = true;
+  res_prepared_ = false;
+  res_de_.clear();
+  res_dv_.clear();
+  res_dc_.clear();
+  res_le_.clear();
+  res_lv_.clear();
+  res_lc_.clear();
+}
+
+void System::pending_deltas(int64_t out3[3]) const {
+  out3[0] = res_full_ ? -1 : int64_t(res_le_.size());
+  out3[1] = res_full_ ? -1 : int64_t(res_lv_.size());
+  out3[2] = res_full_ ? -1 : int64_t(res_lc_.size());
+}
+
+// Pack the delta log (or, after set_resident(true), every record) and clear it.
+void System::drain_deltas(ResPacked& p) {
+  if (res_full_) {
+    res_le_.resize(elems_.size());
+    for (size_t i = 0; i < elems_.size(); i++)
+      res_le_[i] = Id(i);
+    res_lv_.resize(vars_.size());
+    for (size_t i = 0; i < vars_.size(); i++)
+      res_lv_[i] = Id(i);
+    res_lc_.resize(cnsts_.size());
+    for (size_t i = 0; i < cnsts_.size(); i++)
+      res_lc_[i] = Id(i);
+  }
+  const size_t ne = res_le_.size(), nv = res_lv_.size(), nc = res_lc_.size();
+  p.n_elem_total = int64_t(elems_.size());
+  p.n_var_total = int64_t(vars_.size());
+  p.n_cnst_total = int64_t(cnsts_.size());
+  p.e_id.resize(ne);
+  p.e_cnst.resize(ne);
+  p.e_w.resize(ne);
+  p.e_fl.resize(ne);
+  p.v_id = res_lv_;
+  p.v_eb.resize(nv);
+  p.v_n.resize(nv);
+  p.v_p.resize(nv);
+  p.v_b.resize(nv);
+  p.c_id = res_lc_;
+  p.c_b.resize(nc);
+  p.c_fl.resize(nc);
+  for (size_t i = 0; i < ne; i++) {
+    const ElemRec& x = elems_[res_le_[i]];
+    p.e_id[i] = res_le_[i];
+    p.e_cnst[i] = x.cnst;
+    p.e_w[i] = x.weight;
+    p.e_fl[i] = x.where == 1 ? 1 : 0;
+  }
+  for (size_t i = 0; i < nv; i++) {
+    const VarRec& r = vars_[res_lv_[i]];
+    p.v_eb[i] = r.ebase;
+    p.v_n[i] = r.live ? r.n_elems : 0;
+    p.v_p[i] = r.penalty;
+    p.v_b[i] = r.bound;
+  }
+  for (size_t i = 0; i < nc; i++) {
+    const CnstRec& k = cnsts_[res_lc_[i]];
+    p.c_b[i] = k.bound;
+    p.c_fl[i] = k.policy == SharingPolicy::FATPIPE ? 1 : 0;
+  }
+  if (!res_full_) {
+    for (Id e : res_le_)
+      res_de_[size_t(e)] = 0;
+    for (Id v : res_lv_)
+      res_dv_[size_t(v)] = 0;
+    for (Id c : res_lc_)
+      res_dc_[size_t(c)] = 0;
+  }
+  res_le_.clear();
+  res_lv_.clear();
+  res_lc_.clear();
+  res_full_ = false;
+}
+
+// Ship the delta log to the device mirror.
+void System::res_sync() {
+  ResPacked p;
+  drain_deltas(p);
+  int rc = lmmhip_res_apply(ctx(), p.n_elem_total, p.n_var_total, p.n_cnst_total, int64_t(p.e_id.size()),
+                            p.e_id.data(), p.e_cnst.data(), p.e_w.data(), p.e_fl.data(), int64_t(p.v_id.size()),
+                            p.v_id.data(), p.v_eb.data(), p.v_n.data(), p.v_p.data(), p.v_b.data(),
+                            int64_t(p.c_id.size()), p.c_id.data(), p.c_b.data(), p.c_fl.data());
+  if (rc)
+    fatal(std::string("resident delta upload failed: ") + lmmhip_last_error());
+  stats_.delta_records = int64_t(p.e_id.size() + p.v_id.size() + p.c_id.size());
+}
+
+void System::prepare_resident() {
+  auto t0 = std::chrono::steady_clock::now();
+  res_sync();
+  const std::vector<Id> list = solve_constraint_list();
+  if (selective_) {  // Lazy side effect, maxmin.cpp:536-538 (the walk the reference does at init)
+    const double prec = maxmin_precision;
+    for (Id c : list) {
+      const CnstRec& k = cnsts_[c];
+      if (!(k.bound > k.bound * prec))
+        continue;
+      for (Id e = k.en_head; e != kNone; e = elems_[e].next) {
+        const ElemRec& x = elems_[e];
+        if (x.weight > 0 && !vars_[x.var].in_modified_set) {
+          vars_[x.var].in_modified_set = true;
+          modified_actions_.push_back(x.var);
+        }
+      }
+    }
+  }
+  stats_.flatten_ms = ms_since(t0);
+  auto t1 = std::chrono::steady_clock::now();
+  int64_t cnt[3] = {0, 0, 0};
+  int rc = lmmhip_res_flatten(ctx(), int64_t(list.size()), list.data(), maxmin_precision, cnt);
+  if (rc)
+    fatal(std::string("resident flatten failed: ") + lmmhip_last_error());
+  stats_.upload_ms = ms_since(t1);
+  stats_.n_var = cnt[0];
+  stats_.n_cnst = cnt[1];
+  stats_.nnz = cnt[2];
+  flat_ = Flat();
+  flat_valid_ = false;
+  res_prepared_ = true;
+}
+
+void System::fetch_resident() {
+  auto t0 = std::chrono::steady_clock::now();
+  const size_t n = vars_.size();
+  std::vector<double> vals(n);
+  std::vector<uint8_t> rst(n);
+  int rc = lmmhip_res_values(ctx(), int64_t(n), vals.data(), rst.data());
+  if (rc)
+    fatal(std::string("resident fetch failed: ") + lmmhip_last_error());
+  for (size_t v = 0; v < n; v++)
+    if (rst[v])
+      vars_[v].value = vals[v];
+  res_prepared_ = false;
   stats_.fetch_ms = ms_since(t0);
   finish_solve();
 }

@@ -70,6 +70,7 @@ struct VarRec {
 struct SolveStats {
   int64_t rounds = 0, n_var = 0, n_cnst = 0, nnz = 0;
   double device_ms = 0.0, flatten_ms = 0.0, upload_ms = 0.0, fetch_ms = 0.0;
+  int64_t delta_records = 0;  // resident mode: element + variable + constraint records shipped
 };
 
 class System {
@@ -88,7 +89,10 @@ public:
   void update_variable_bound(Id v, double bound);
   void update_variable_penalty(Id v, double penalty);
   void update_constraint_bound(Id c, double bound);
-  void unshare(Id c) { cnsts_[c].policy = SharingPolicy::FATPIPE; }
+  void unshare(Id c) {
+    cnsts_[c].policy = SharingPolicy::FATPIPE;
+    touch_c(c);
+  }
   void set_concurrency_limit(Id c, int limit);
   void set_concurrency_share(Id v, int share) { vars_[v].share = share; }
   bool constraint_used(Id c) const { return cnsts_[c].in_active; }
@@ -137,6 +141,9 @@ public:
   std::vector<Id>& modified_actions() { return modified_actions_; }
   void clear_modified_actions();
   int64_t live_variables() const { return n_live_vars_; }
+  size_t n_elem_slots() const { return elems_.size(); }
+  size_t n_var_slots() const { return vars_.size(); }
+  size_t n_cnst_slots() const { return cnsts_.size(); }
 
   // ---- flattening (also used by the batched multi-system path) ----
   struct Flat {
@@ -154,7 +161,33 @@ public:
 
   lmmhip_ctx* ctx();
 
+  // ---- resident mode ----
+  // The element / variable / constraint records are mirrored in HBM (lmmhip_res_apply); every
+  // mutation logs the records it touched, the log is shipped at the next max-min solve, and the
+  // solver's CSR/CSC is rebuilt on the device (lmmhip_res_flatten) instead of flatten_maxmin + a full
+  // upload.  Same results bit for bit (tests/test_gpu_resident.py).  FairBottleneck::solve keeps the
+  // host flatten.  Turning it on ships the whole system at the next solve.
+  void set_resident(bool on);
+  bool resident() const { return resident_; }
+  // Pending delta-log sizes (elements, variables, constraints; -1 each = full re-ship pending).
+  void pending_deltas(int64_t out3[3]) const;
+  // The delta log packed as lmmhip_res_apply takes it (res_sync ships it); draining clears the log.
+  struct ResPacked {
+    int64_t n_elem_total = 0, n_var_total = 0, n_cnst_total = 0;
+    std::vector<int64_t> e_id, v_eb;
+    std::vector<int32_t> e_cnst, v_id, v_n, c_id;
+    std::vector<double> e_w, v_p, v_b, c_b;
+    std::vector<uint8_t> e_fl, c_fl;
+  };
+  void drain_deltas(ResPacked& p);
+
 private:
+  void touch_e(Id e);
+  void touch_v(Id v);
+  void touch_c(Id c);
+  void res_sync();
+  void prepare_resident();
+  void fetch_resident();
   // list helpers
   void en_push_front(Id c, Id e);
   void dis_push_back(Id c, Id e);
@@ -199,6 +232,11 @@ private:
   Id mod_head_ = kNone, mod_tail_ = kNone;
   int64_t n_live_vars_ = 0;
   std::vector<Id> modified_actions_;
+
+  // resident mode: delta log (dirty flags + lists of ids)
+  bool resident_ = false, res_full_ = true, res_prepared_ = false;
+  std::vector<uint8_t> res_de_, res_dv_, res_dc_;
+  std::vector<Id> res_le_, res_lv_, res_lc_;
 
   // device state
   lmmhip_ctx* ctx_ = nullptr;

@@ -82,6 +82,12 @@ SIGNATURES = {
     "lmm_device_solve": (I, [P]),
     "lmm_fetch": (I, [P]),
     "lmm_last_stats": (I, [P, PI64, PD]),
+    "lmm_set_resident": (I, [P, I]),
+    "lmm_is_resident": (I, [P]),
+    "lmm_pending_deltas": (I, [P, PI64]),
+    "lmm_last_delta_records": (ct.c_int64, [P]),
+    "lmm_table_sizes": (I, [P, PI64]),
+    "lmm_resident_drain": (I, [P, PI64, PI64, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8), ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD, PD, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8)]),
     "lmm_flat_export": (I, [P, PI64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8), PI64]),
     "lmm_solve_batch": (I, [ct.POINTER(P), I]),
     "lmm_system_device_ctx": (P, [P]),
@@ -98,6 +104,10 @@ SIGNATURES = {
     "lmmhip_upload": (I, [P, I64, I64, I64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
     "lmmhip_update_vars": (I, [P, PD, PD]),
     "lmmhip_update_cnsts": (I, [P, PD]),
+    "lmmhip_res_apply": (I, [P, I64, I64, I64, I64, PI64, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8), I64, ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD, PD, I64, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_res_flatten": (I, [P, I64, ct.POINTER(ct.c_int32), D, PI64]),
+    "lmmhip_res_values": (I, [P, I64, PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_flat_download": (I, [P, PI64, P, P, P, P, P, P, P, P, P, P]),
     "lmmhip_solve": (I, [P, I, D]),
     "lmmhip_get_values": (I, [P, PD]),
     "lmmhip_values_device_ptr": (I, [P, ct.POINTER(P)]),
@@ -151,6 +161,12 @@ def lib():
 def _check(rc):
     if rc != 0:
         raise LmmError(lib().lmm_last_error().decode())
+    return rc
+
+
+def _check_hip(rc):
+    if rc != 0:
+        raise LmmError(lib().lmmhip_last_error().decode())
     return rc
 
 
@@ -320,7 +336,51 @@ class System:
         c, m = (I64 * 4)(), (D * 4)()
         lib().lmm_last_stats(self.h, c, m)
         return dict(rounds=c[0], n_var=c[1], n_cnst=c[2], nnz=c[3], device_ms=m[0], flatten_ms=m[1],
-                    upload_ms=m[2], fetch_ms=m[3])
+                    upload_ms=m[2], fetch_ms=m[3], delta_records=lib().lmm_last_delta_records(self.h))
+
+    # resident mode (include/lmm/lmm_system.h, lmm_set_resident): HBM mirror + delta log + device flatten
+    def set_resident(self, on=True):
+        _check(lib().lmm_set_resident(self.h, int(bool(on))))
+
+    def resident(self):
+        return bool(lib().lmm_is_resident(self.h))
+
+    def drain_deltas(self):
+        """Drain the delta log without shipping it (test hook): dict of numpy arrays as lmmhip_res_apply
+        would receive them."""
+        ne, nv, nc = self.pending_deltas()
+        sz = (I64 * 6)(ne, nv, nc, 0, 0, 0)
+        if min(ne, nv, nc) < 0:  # whole system pending: every record
+            _check(lib().lmm_table_sizes(self.h, sz))
+        a = dict(e_id=np.zeros(sz[0], np.int64), e_cnst=np.zeros(sz[0], np.int32), e_w=np.zeros(sz[0]),
+                 e_fl=np.zeros(sz[0], np.uint8), v_id=np.zeros(sz[1], np.int32), v_eb=np.zeros(sz[1], np.int64),
+                 v_n=np.zeros(sz[1], np.int32), v_p=np.zeros(sz[1]), v_b=np.zeros(sz[1]),
+                 c_id=np.zeros(sz[2], np.int32), c_b=np.zeros(sz[2]), c_fl=np.zeros(sz[2], np.uint8))
+        ptr = lambda x: x.ctypes.data_as(ct.POINTER(np.ctypeslib.as_ctypes_type(x.dtype)))
+        _check(lib().lmm_resident_drain(self.h, sz, *(ptr(a[k]) for k in (
+            "e_id", "e_cnst", "e_w", "e_fl", "v_id", "v_eb", "v_n", "v_p", "v_b", "c_id", "c_b", "c_fl"))))
+        n = dict(e=sz[0], v=sz[1], c=sz[2])
+        out = {k: v[:n[k[0]]] for k, v in a.items()}
+        out["totals"] = (sz[3], sz[4], sz[5])
+        return out
+
+    def device_flat(self):
+        """The flattened system on the device (after prepare()): dict of numpy arrays."""
+        ctx = self.device_ctx()
+        n = (I64 * 3)()
+        _check_hip(lib().lmmhip_flat_download(ctx, n, *([None] * 10)))
+        nV, nC, nnz = n
+        a = dict(var_ptr=np.zeros(nV + 1, np.uint32), csr_c=np.zeros(nnz, np.int32), csr_w=np.zeros(nnz),
+                 cnst_ptr=np.zeros(nC + 1, np.uint32), csc_v=np.zeros(nnz, np.int32), csc_w=np.zeros(nnz),
+                 pen=np.zeros(nV), vbound=np.zeros(nV), cbound=np.zeros(nC), cflags=np.zeros(nC, np.uint8))
+        _check_hip(lib().lmmhip_flat_download(ctx, n, *(x.ctypes.data for x in a.values())))
+        return a
+
+    def pending_deltas(self):
+        """(elements, variables, constraints) logged since the last solve; (-1, -1, -1) = whole system."""
+        o = (I64 * 3)()
+        _check(lib().lmm_pending_deltas(self.h, o))
+        return tuple(o)
 
     def check_certificate(self, precision=None):
         """(max relative excess, #infeasible constraints, #variables without a bottleneck)."""

@@ -1,0 +1,130 @@
+"""Resident mode on the GPU: HBM mirror + delta log + device flatten.
+
+Parity bar: the device flatten must build, BIT FOR BIT, the very arrays the host flatten uploads (dense
+constraint ids in list order, dense variables ascending, CSC by a stable sort) — checked by downloading
+both flattened systems from HBM (lmmhip_flat_download) step after step of random mutations (flows
+ending and starting, penalty / bound moves, staging).  Values are then compared with the parity
+tolerance of tests/lmm_cases.py against the host-flatten solve and the oracle (the solver's fp64
+decrement atomics make the last bits run-to-run dependent, so bitwise value equality is not a property
+of either path), and in selective (Lazy) mode the modified-action lists must be identical.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from simgrid_amd import lmm as L
+from tests import lmm_cases as K
+from tests.test_resident import step_ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if L.device_count() == 0:
+        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X")
+
+
+def _values(vs):
+    return {k: v.get_value() for k, v in vs.items()}
+
+
+def _flat_equal(fa, fb):
+    for k in fb:
+        assert fa[k].dtype == fb[k].dtype and np.array_equal(fa[k], fb[k]), k
+
+
+def _split_solve(s):
+    s.prepare()
+    f = s.device_flat()
+    s.device_solve()
+    s.fetch()
+    return f
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("selective", [False, True])
+def test_resident_steps_bit_identical(seed, selective):
+    ops = K.random_script(seed, n_cnst=40, n_var=150, conc_limits=seed % 2 == 1, frees=10, penalty_updates=10,
+                          bound_updates=10)
+    a, csa, vsa = K.replay(L, ops, selective)
+    a.set_resident(True)
+    b, csb, vsb = K.replay(L, ops, selective)
+    o, cso, vso = K.replay(O, ops, selective)
+    rng = random.Random(7 + seed)
+    next_var = 10000
+    for step in range(6):
+        fa = _split_solve(a)
+        fb = _split_solve(b)
+        o.solve()
+        _flat_equal(fa, fb)
+        worst, bad = K.compare_values(vsa, vsb)
+        assert not bad, (step, worst, bad[:5])
+        worst, bad = K.compare_values(vsa, vso)
+        assert not bad, (step, worst, bad[:5])
+        if selective:
+            assert [v.h for v in a.modified_actions()] == [v.h for v in b.modified_actions()]
+            a.clear_modified_actions()
+            b.clear_modified_actions()
+        st = a.last_stats()
+        assert st["n_var"] == b.last_stats()["n_var"] and st["nnz"] == b.last_stats()["nnz"]
+        if step > 0:  # only the logged records travel after the first (full) ship
+            assert 0 < st["delta_records"] < len(vsa) * 4 + 200
+        more, next_var = step_ops(rng, csa, vsa, next_var)
+        K.replay(L, more, sys_=a, cs=csa, vs=vsa)
+        K.replay(L, more, sys_=b, cs=csb, vs=vsb)
+        K.replay(O, more, sys_=o, cs=cso, vs=vso)
+
+
+@pytest.mark.parametrize("klass,run", [(0, r) for r in range(10)] + [(1, r) for r in range(5)])
+def test_resident_maxmin_bench_goldens(klass, run):
+    """maxmin_bench small/medium (golden-pinned systems, heavy concurrency staging) through resident mode."""
+    a = L.System(False)
+    a.set_resident(True)
+    _, va, _, _ = a.gen_maxmin_bench(klass, run)
+    b = L.System(False)
+    _, vb, _, _ = b.gen_maxmin_bench(klass, run)
+    _flat_equal(_split_solve(a), _split_solve(b))
+    for x, y in zip(va, vb):
+        assert K.close(x.get_value(), y.get_value())
+
+
+def test_resident_synthetic_churn():
+    """A 2e4 x 2e5 x 8 synthetic system, then churn steps driven through the API: resident equals the
+    host flatten bit for bit and ships only the logged records."""
+    nC, nV = 20000, 200000
+    a = L.System(False)
+    a.set_resident(True)
+    va = a.gen_synthetic(nC, nV, k=8, seed=3, penalty_mix=1, bounded_permille=100, fatpipe_permille=50)
+    b = L.System(False)
+    vb = b.gen_synthetic(nC, nV, k=8, seed=3, penalty_mix=1, bounded_permille=100, fatpipe_permille=50)
+    rng = np.random.default_rng(5)
+    for step in range(3):
+        _flat_equal(_split_solve(a), _split_solve(b))
+        xa, xb = a.values_of(va), b.values_of(vb)
+        assert np.all(np.abs(xa - xb) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(xb))), step
+        if step:
+            assert a.last_stats()["delta_records"] < 20000
+        for i in rng.choice(nV, 500, replace=False):
+            p = float(rng.choice([0.0, 0.5, 1.0, 2.0]))
+            a.update_variable_penalty(L.Variable(a, int(va[i])), p)
+            b.update_variable_penalty(L.Variable(b, int(vb[i])), p)
+        for c in rng.choice(nC, 100, replace=False):
+            bnd = float(rng.uniform(0.5, 10.0))
+            a.update_constraint_bound(L.Constraint(a, int(c)), bnd)
+            b.update_constraint_bound(L.Constraint(b, int(c)), bnd)
+
+
+def test_resident_fair_bottleneck_keeps_host_flatten():
+    """FairBottleneck::solve is not served by the device flatten (max-min only); resident mode must not
+    change its result."""
+    ops = K.random_script(11, n_cnst=20, n_var=50)
+    a, _, vsa = K.replay(L, ops, kind=1)
+    a.set_resident(True)
+    b, _, vsb = K.replay(L, ops, kind=1)
+    a.solve()
+    b.solve()
+    worst, bad = K.compare_values(vsa, vsb)
+    assert not bad, (worst, bad[:5])
