@@ -167,6 +167,38 @@ int lmmhip_update_actions_full(lmmhip_ctx* ctx, int model, double delta, double 
 int lmmhip_actions_download(lmmhip_ctx* ctx, double* remains, double* max_duration, double* latency, double* penalty,
                             uint8_t* events);
 
+/* LAZY update models (the default for CPU and network, sg_config.cpp:252): the
+ * ActionHeap (Action.cpp:209-241) becomes per-action (date, type) arrays in HBM whose top is a grid
+ * min-reduction — no heap maintenance on the host.
+ * lmmhip_actions_lazy_upload (after lmmhip_actions_upload): Action::last_update_ / last_value_ /
+ *   start_time_, and each action's heap entry (date, heap_type LMMHIP_HEAP_*; UNSET = not in the heap,
+ *   e.g. NetworkCm02Model::communicate's latency event, network_cm02.cpp:215-225, is LATENCY).
+ *   flags bit2 (LMMHIP_ACT_NOT_STARTED) = not in the started set.
+ * lmmhip_actions_lazy_update: the loop of Model::next_occuring_event_lazy (Model.cpp:46-94) over the
+ *   modified actions of the last lmm_solve (action indices, each once): update_remains_lazy of the
+ *   CPU (cpu_interface.cpp:141-157) or CM02 (network_cm02.cpp:426-449) action, completion date, heap
+ *   update; *n_finished = actions update_remains_lazy finished (events[i] = LMMHIP_EV_FINISHED).
+ * lmmhip_next_event_lazy: heap top date - now, or -1 when the heap is empty (Model.cpp:97-100).
+ * lmmhip_actions_lazy_due: update_actions_state_lazy (cpu_interface.cpp:25-35, network_cm02.cpp:103-126):
+ *   pops every entry while double_equals(top_date, now, surf_precision); returns the popped actions in
+ *   ascending index order with their event (CM02 latency hat: LMMHIP_EV_LATENCY_PAID, the host restores
+ *   the penalty; otherwise LMMHIP_EV_FINISHED).  The reference pops by (date, Action*): same set.
+ * lmmhip_actions_lazy_download: inspection of the lazy state. */
+#define LMMHIP_HEAP_UNSET 0
+#define LMMHIP_HEAP_LATENCY 1
+#define LMMHIP_HEAP_MAX_DURATION 2
+#define LMMHIP_HEAP_NORMAL 3
+#define LMMHIP_ACT_NOT_STARTED 4
+int lmmhip_actions_lazy_upload(lmmhip_ctx* ctx, const double* last_update, const double* last_value,
+                               const double* start_time, const double* date, const uint8_t* heap_type);
+int lmmhip_actions_lazy_update(lmmhip_ctx* ctx, int model, double now, double maxmin_precision, double surf_precision,
+                               int64_t n_modified, const int32_t* modified, int64_t* n_finished);
+int lmmhip_next_event_lazy(lmmhip_ctx* ctx, double now, double* out);
+int lmmhip_actions_lazy_due(lmmhip_ctx* ctx, int model, double now, double surf_precision, int32_t* ids,
+                            uint8_t* events, int64_t cap, int64_t* n_due);
+int lmmhip_actions_lazy_download(lmmhip_ctx* ctx, double* last_update, double* last_value, double* date,
+                                 uint8_t* heap_type);
+
 /* Number of visible HIP devices (0 when none; never initialises a context). */
 int lmmhip_device_count(void);
 

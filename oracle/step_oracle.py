@@ -70,3 +70,97 @@ def update_actions_state_full(model, values, st, delta, maxmin_prec, surf_prec):
         events.append(ev)
     assert all(not math.isnan(x) for x in st["remains"])
     return events
+
+
+# ---- LAZY models: Model::next_occuring_event_lazy / update_actions_state_lazy with a real heap ----
+HEAP_UNSET, HEAP_LATENCY, HEAP_MAX_DURATION, HEAP_NORMAL = 0, 1, 2, 3  # ActionHeap::Type
+ACT_NOT_STARTED = 4
+
+
+class LazyModel:
+    """One LAZY model's actions with an ActionHeap kept as a binary heap (heapq, lazy deletion), as the
+    reference keeps a boost pairing heap of (date, Action*) (Action.cpp:209-241).  `st` holds lists:
+    remains, max_duration, penalty, flags, last_update, last_value, start_time, date, heap_type."""
+
+    def __init__(self, model, st):
+        import heapq
+
+        self.hq = heapq
+        self.model, self.st = model, st
+        self.heap, self.ver = [], [0] * len(st["remains"])
+        for i, h in enumerate(st["heap_type"]):
+            if h != HEAP_UNSET:
+                self._push(i, st["date"][i], h)
+
+    def _push(self, i, date, h):  # ActionHeap::update / insert
+        self.ver[i] += 1
+        self.st["date"][i], self.st["heap_type"][i] = date, h
+        self.hq.heappush(self.heap, (date, i, self.ver[i]))
+
+    def _remove(self, i):  # ActionHeap::remove
+        self.ver[i] += 1
+        self.st["heap_type"][i] = HEAP_UNSET
+        self.st["date"][i] = math.inf
+
+    def _top(self):
+        while self.heap and self.heap[0][2] != self.ver[self.heap[0][1]]:
+            self.hq.heappop(self.heap)
+        return self.heap[0] if self.heap else None
+
+    def _update_remains_lazy(self, i, value, now, rprec, sprec):
+        """CpuAction (cpu_interface.cpp:141-157) / NetworkCm02Action (network_cm02.cpp:426-449)."""
+        st = self.st
+        delta = now - st["last_update"][i]
+        if st["remains"][i] > 0:
+            st["remains"][i] = double_update(st["remains"][i], st["last_value"][i] * delta, rprec)
+        finished = False
+        if self.model != 0:
+            if st["max_duration"][i] != NO_MAX_DURATION:
+                st["max_duration"][i] = double_update(st["max_duration"][i], delta, sprec)
+            if (st["remains"][i] <= 0 and st["penalty"][i] > 0) or (
+                    st["max_duration"][i] != NO_MAX_DURATION and st["max_duration"][i] <= 0):
+                finished = True
+                self._remove(i)
+        st["last_update"][i] = now
+        st["last_value"][i] = value
+        return finished
+
+    def next_occuring_event_lazy(self, values, now, modified, maxmin_prec, sprec):
+        """Model.cpp:40-101 after lmm_solve: returns (top - now or -1, actions finished on the way)."""
+        st, rprec, finished = self.st, maxmin_prec * sprec, []
+        for i in modified:
+            if st["flags"][i] & ACT_NOT_STARTED:
+                continue
+            if st["penalty"][i] <= 0 or st["heap_type"][i] == HEAP_LATENCY:
+                continue
+            if self._update_remains_lazy(i, values[i], now, rprec, sprec):
+                finished.append(i)
+            # get_remains() re-runs update_remains_lazy at delta = 0 (Action.cpp:184-192): no change
+            mn, share = -1.0, values[i]
+            if share > 0:
+                mn = now + (st["remains"][i] / share if st["remains"][i] > 0 else 0.0)
+            flag = False
+            md = st["max_duration"][i]
+            if md != NO_MAX_DURATION and (mn <= -1 or st["start_time"][i] + md < mn):
+                mn, flag = st["start_time"][i] + md, True
+            assert mn > -1, "DIE_IMPOSSIBLE"
+            self._push(i, mn, HEAP_MAX_DURATION if flag else HEAP_NORMAL)
+        top = self._top()
+        return (top[0] - now if top else -1.0), finished
+
+    def update_actions_state_lazy(self, now, sprec):
+        """cpu_interface.cpp:25-35 / network_cm02.cpp:103-126: pop while double_equals(top, now)."""
+        out = []
+        while True:
+            top = self._top()
+            if top is None or not abs(top[0] - now) < sprec:
+                break
+            self.hq.heappop(self.heap)
+            i = top[1]
+            if self.model != 0 and self.st["heap_type"][i] == HEAP_LATENCY:
+                out.append((i, EV_LATENCY_PAID))
+                self.st["last_update"][i] = now
+            else:
+                out.append((i, EV_FINISHED))
+            self._remove(i)
+        return out

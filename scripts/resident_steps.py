@@ -61,9 +61,12 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pen", type=int, default=10000)
     ap.add_argument("--cb", type=int, default=1000)
+    ap.add_argument("--resident-only", action="store_true")
     a = ap.parse_args()
     res, xr = run(True, a)
     print(json.dumps(res), flush=True)
+    if a.resident_only:
+        return
     host, xh = run(False, a)
     print(json.dumps(host), flush=True)
     # parity tolerance of tests/lmm_cases.py (fp64 decrement atomics: last bits vary run to run)

@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -44,6 +45,15 @@ int fail(int code, const std::string& msg) {
 // =============================================================================================
 // context + C ABI
 // =============================================================================================
+// Device buffers of one flattened system: allocated by alloc_flat, filled by the host upload
+// (lmmhip_upload) or on the device by the resident flatten (lmmhip_res_flatten).
+struct FlatBufs {
+  uint32_t *vp, *cp, *chb;
+  int32_t *csr_c, *csc_v, *cvar0, *chc, *cch;
+  double *csr_w, *csc_w, *pen, *vb, *cb;
+  uint8_t* cf;
+};
+
 struct lmmhip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;      // the stream every launch and copy goes to
@@ -84,6 +94,8 @@ struct lmmhip_ctx {
   int64_t res_capE = 0, res_capV = 0, res_capC = 0;
   int64_t res_nE = 0, res_nV = 0, res_nC = 0;  // host table sizes of the last delta batch
   bool res_flat = false;                        // the uploaded system came from lmmhip_res_flatten
+  FlatBufs fb_last{};
+  int64_t fcap[4] = {0, 0, 0, 0};               // capacities of the flat-system buffers (nV, nC, nnz, nch)
   int64_t res_flat_nv = 0;                      // variable slots covered by that flatten
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp;
@@ -196,16 +208,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   return 0;
 }
 
-// Device buffers of one flattened system: allocated by alloc_flat, filled by the host upload
-// (lmmhip_upload) or on the device by the resident flatten (lmmhip_res_flatten).
-struct FlatBufs {
-  uint32_t *vp, *cp, *chb;
-  int32_t *csr_c, *csc_v, *cvar0, *chc, *cch;
-  double *csr_w, *csc_w, *pen, *vb, *cb;
-  uint8_t* cf;
-};
-
-static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_t nch, FlatBufs* o) {
+static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_t nch, FlatBufs* o) {
   free_all(c);
   Dev& d = c->d;
   d.nV = int32_t(nV);
@@ -302,6 +305,36 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
   d.crow[2] = crow2;
   d.ccol[2] = ccol2;
   *o = FlatBufs{vp, cp, chb, csr_c, csc_v, cvar0, chc, cch, csr_w, csc_w, pen, vb, cb, cf};
+  return 0;
+}
+
+// Buffers for a system of this shape, reusing the current ones when they are large enough (a
+// simulation re-solves systems of similar size every step: no hipMalloc / hipFree on that path);
+// otherwise reallocated with 25 % headroom over the previous capacity.
+static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_t nch, FlatBufs* o) {
+  const bool have = !c->allocs.empty();
+  const bool fits = have && nV <= c->fcap[0] && nC <= c->fcap[1] && nnz <= c->fcap[2] && nch <= c->fcap[3];
+  if (!fits) {
+    int64_t a[4] = {nV, nC, nnz, nch};
+    if (have)
+      for (int i = 0; i < 4; i++)
+        a[i] = std::max(a[i], c->fcap[i] + c->fcap[i] / 4);
+    if (a[2] > INT32_MAX)
+      a[2] = std::max(nnz, int64_t(INT32_MAX));
+    if (int rc = alloc_flat_exact(c, a[0], a[1], a[2], a[3], &c->fb_last))
+      return rc;
+    for (int i = 0; i < 4; i++)
+      c->fcap[i] = a[i];
+  } else {
+    c->uploaded = false;
+    c->res_flat = false;
+    c->fb_shard = false;
+  }
+  c->d.nV = int32_t(nV);
+  c->d.nC = int32_t(nC);
+  c->d.nnz = nnz;
+  c->d.nch = int32_t(nch);
+  *o = c->fb_last;
   return 0;
 }
 
@@ -1163,6 +1196,169 @@ int lmmhip_actions_download(lmmhip_ctx* c, double* remains, double* max_duration
       HIPCHK(hipMemcpyAsync(penalty, c->act.penalty, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (events)
       HIPCHK(hipMemcpyAsync(events, c->act.events, n, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_actions_lazy_upload(lmmhip_ctx* c, const double* last_update, const double* last_value,
+                               const double* start_time, const double* date, const uint8_t* heap_type) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (!c->act.nev)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_upload first");
+  const int64_t n = c->act.n;
+  if (n > 0 && (!last_update || !last_value || !start_time || !date || !heap_type))
+    return fail(LMMHIP_E_ARG, "null lazy action arrays");
+  if (n >= (int64_t(1) << 30))
+    return fail(LMMHIP_E_ARG, "too many actions for the lazy heap (< 2^30)");
+  for (int64_t i = 0; i < n; i++)
+    if (heap_type[i] > HEAP_NORMAL)
+      return fail(LMMHIP_E_ARG, "unknown heap type");
+  HIPCHK(hipSetDevice(c->device));
+  ActDev& a = c->act;
+  double* st;
+  std::vector<double> d(date, date + n);
+  for (int64_t i = 0; i < n; i++)
+    if (heap_type[i] == HEAP_UNSET)
+      d[size_t(i)] = __builtin_huge_val();
+  int rc = act_alloc(c, &a.last_update, n, last_update) | act_alloc(c, &a.last_value, n, last_value) |
+           act_alloc(c, &st, n, start_time) | act_alloc(c, &a.date, n, d.data()) |
+           act_alloc(c, &a.htype, n, heap_type) | act_alloc<int32_t>(c, &a.due, n, nullptr) |
+           act_alloc<int32_t>(c, &a.ndue, 1, nullptr) | act_alloc<int32_t>(c, &a.err, 1, nullptr);
+  if (rc)
+    return rc;
+  a.start_time = st;
+  HIPCHK(hipMemsetAsync(a.err, 0, sizeof(int32_t), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_actions_lazy_update(lmmhip_ctx* c, int model, double now, double maxmin_precision, double surf_precision,
+                               int64_t n_modified, const int32_t* modified, int64_t* n_finished) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (!c->act.htype)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_lazy_upload first");
+  if (model != MODEL_CPU && model != MODEL_CM02)
+    return fail(LMMHIP_E_ARG, "lazy update: CPU or CM02 model");
+  if (n_modified < 0 || (n_modified && !modified))
+    return fail(LMMHIP_E_ARG, "bad modified-action list");
+  {  // the modified set holds each action once (its hook): a duplicate would race on the action
+    std::vector<uint8_t> seen(size_t(c->act.n), 0);
+    for (int64_t j = 0; j < n_modified; j++) {
+      if (modified[j] < 0 || modified[j] >= c->act.n)
+        return fail(LMMHIP_E_ARG, "modified action out of range");
+      if (seen[size_t(modified[j])]++)
+        return fail(LMMHIP_E_ARG, "duplicate action in the modified list");
+    }
+  }
+  HIPCHK(hipSetDevice(c->device));
+  int32_t h[2] = {0, 0};
+  HIPCHK(hipMemsetAsync(c->act.nev, 0, sizeof(int32_t), c->stream));
+  if (n_modified) {
+    int32_t* dmod = nullptr;
+    if (int rc = scratch(c, c->rs_stage[0], n_modified, &dmod))
+      return rc;
+    HIPCHK(hipMemcpyAsync(dmod, modified, size_t(n_modified) * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    LAUNCH(7, -1, act_lazy_update, grid_for(n_modified, kBlock), kBlock, c->act, c->d.x, model, now,
+           maxmin_precision * surf_precision, surf_precision, n_modified, dmod);
+  }
+  HIPCHK(hipMemcpyAsync(&h[0], c->act.nev, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(&h[1], c->act.err, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (h[1])
+    return fail(LMMHIP_E_STATE, "next_occuring_event_lazy: an action got no date (DIE_IMPOSSIBLE, Model.cpp:96)");
+  if (n_finished)
+    *n_finished = h[0];
+  return 0;
+}
+
+static int lazy_top(lmmhip_ctx* c, bool* any, double* top) {
+  unsigned long long h = ~0ull;
+  HIPCHK(hipMemsetAsync(c->act.umin, 0xFF, sizeof(unsigned long long), c->stream));
+  if (c->act.n > 0)
+    LAUNCH(7, -1, act_lazy_min, grid_for(c->act.n, kBlock), kBlock, c->act);
+  HIPCHK(hipMemcpyAsync(&h, c->act.umin, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *any = h != ~0ull;
+  if (*any) {
+    const unsigned long long b = (h >> 63) ? (h & 0x7FFFFFFFFFFFFFFFull) : ~h;
+    std::memcpy(top, &b, sizeof(*top));
+  }
+  return 0;
+}
+
+int lmmhip_next_event_lazy(lmmhip_ctx* c, double now, double* out) {
+  if (!c || !out)
+    return fail(LMMHIP_E_ARG, "null argument");
+  if (!c->act.htype)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_lazy_upload first");
+  HIPCHK(hipSetDevice(c->device));
+  bool any = false;
+  double top = 0;
+  if (int rc = lazy_top(c, &any, &top))
+    return rc;
+  *out = any ? top - now : -1.0;  // Model.cpp:95-100
+  return 0;
+}
+
+int lmmhip_actions_lazy_due(lmmhip_ctx* c, int model, double now, double surf_precision, int32_t* ids,
+                            uint8_t* events, int64_t cap, int64_t* n_due) {
+  if (!c || !n_due)
+    return fail(LMMHIP_E_ARG, "null argument");
+  if (!c->act.htype)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_lazy_upload first");
+  if (model != MODEL_CPU && model != MODEL_CM02)
+    return fail(LMMHIP_E_ARG, "lazy update: CPU or CM02 model");
+  HIPCHK(hipSetDevice(c->device));
+  *n_due = 0;
+  bool any = false;
+  double top = 0;
+  if (int rc = lazy_top(c, &any, &top))
+    return rc;
+  if (!any || !(std::fabs(top - now) < surf_precision))  // the heap loop's first test
+    return 0;
+  int32_t h = 0;
+  HIPCHK(hipMemsetAsync(c->act.ndue, 0, sizeof(int32_t), c->stream));
+  LAUNCH(7, -1, act_lazy_due, grid_for(c->act.n, kBlock), kBlock, c->act, model, now, surf_precision);
+  HIPCHK(hipMemcpyAsync(&h, c->act.ndue, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (h > cap || (h && (!ids || !events)))
+    return fail(LMMHIP_E_ARG, "lazy due: output capacity too small (the heap entries are already popped)");
+  if (h) {
+    std::vector<int32_t> v(static_cast<size_t>(h));
+    std::vector<uint8_t> e(static_cast<size_t>(c->act.n));
+    HIPCHK(hipMemcpyAsync(v.data(), c->act.due, size_t(h) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(e.data(), c->act.events, size_t(c->act.n), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::sort(v.begin(), v.end());  // deterministic order (the reference pops by (date, Action*))
+    for (int32_t k = 0; k < h; k++) {
+      ids[k] = v[size_t(k)];
+      events[k] = e[size_t(v[size_t(k)])];
+    }
+  }
+  *n_due = h;
+  return 0;
+}
+
+int lmmhip_actions_lazy_download(lmmhip_ctx* c, double* last_update, double* last_value, double* date,
+                                 uint8_t* heap_type) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (!c->act.htype)
+    return fail(LMMHIP_E_STATE, "lmmhip_actions_lazy_upload first");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t n = size_t(c->act.n);
+  if (n) {
+    if (last_update)
+      HIPCHK(hipMemcpyAsync(last_update, c->act.last_update, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (last_value)
+      HIPCHK(hipMemcpyAsync(last_value, c->act.last_value, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (date)
+      HIPCHK(hipMemcpyAsync(date, c->act.date, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (heap_type)
+      HIPCHK(hipMemcpyAsync(heap_type, c->act.htype, n, hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;

@@ -124,6 +124,11 @@ SIGNATURES = {
     "lmmhip_next_event_full": (I, [P, I, PD]),
     "lmmhip_update_actions_full": (I, [P, I, D, D, D, PI64]),
     "lmmhip_actions_download": (I, [P, PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_actions_lazy_upload": (I, [P, PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_actions_lazy_update": (I, [P, I, D, D, D, I64, ct.POINTER(ct.c_int32), PI64]),
+    "lmmhip_next_event_lazy": (I, [P, D, PD]),
+    "lmmhip_actions_lazy_due": (I, [P, I, D, D, ct.POINTER(ct.c_int32), ct.POINTER(ct.c_uint8), I64, PI64]),
+    "lmmhip_actions_lazy_download": (I, [P, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
     "lmmhip_device_count": (I, []),
     "lmmhip_last_error": (ct.c_char_p, []),
 }

@@ -48,3 +48,54 @@ def test_step_glue_matches_oracle(model):
         assert list(dev["events"]) == ev
         for k in ("remains", "max_duration", "latency", "penalty"):
             assert np.array_equal(dev[k], np.array(ost[k])), (step, k)
+
+
+@pytest.mark.parametrize("model", [D.MODEL_CPU, D.MODEL_CM02])
+def test_lazy_glue_matches_heap_oracle(model):
+    """LAZY models: device (date, type) arrays + min-reduction vs the oracle's real heap, bit for bit,
+    over steps of modified sets, completion dates, pops and latency hats."""
+    rng = np.random.default_rng(11 + model)
+    s = L.System(False)
+    s.gen_maxmin_bench(2, 1)
+    f = M.export_flat(s)
+    s.solve()
+    x = np.array(s.values_of(f.var_ids))
+    n = 6000
+    vi, st = random_actions(rng, n, len(x))
+    st["flags"] = np.where(rng.random(n) < 0.05, S.ACT_NOT_STARTED, 0).astype(np.uint8)
+    lat_hat = (rng.random(n) < 0.2) if model == D.MODEL_CM02 else np.zeros(n, bool)
+    lz = dict(last_update=np.zeros(n), last_value=np.where(rng.random(n) < 0.5, rng.random(n), 0.0),
+              start_time=np.zeros(n), date=np.where(lat_hat, rng.random(n) * 1e-3, 0.0),
+              heap_type=np.where(lat_hat, S.HEAP_LATENCY, S.HEAP_UNSET).astype(np.uint8))
+    acts = D.DeviceActions(s.device_ctx(), vi, **st)
+    acts.lazy_init(**lz)
+    ost = {k: list(v) for k, v in st.items() if k in ("remains", "max_duration", "penalty", "flags")}
+    ost.update({k: list(v) for k, v in lz.items()})
+    ost["date"] = [d if h else float("inf") for d, h in zip(ost["date"], ost["heap_type"])]
+    O = S.LazyModel(model, ost)
+    values = [x[i] if i >= 0 else 0.0 for i in vi]
+    # a modified action the loop does not skip must get a date (else DIE_IMPOSSIBLE, Model.cpp:96):
+    # share > 0 or a max duration
+    dated = np.array([values[i] > 0 or st["max_duration"][i] != S.NO_MAX_DURATION or st["penalty"][i] <= 0
+                      or st["flags"][i] & S.ACT_NOT_STARTED or lat_hat[i] for i in range(n)])
+    now, pops = 0.0, 0
+    for step in range(10):
+        modified = rng.permutation(np.nonzero(dated)[0])[: n // 3]
+        nfin = acts.lazy_update(model, now, modified, 1e-5, 1e-5)
+        want_ev, want_fin = O.next_occuring_event_lazy(values, now, [int(i) for i in modified], 1e-5, 1e-5)
+        got_ev = acts.next_occuring_event_lazy(now)
+        assert nfin == len(want_fin) and got_ev == want_ev, (step, got_ev, want_ev)
+        if got_ev < 0:
+            break
+        now = now + got_ev
+        ids, evs = acts.lazy_due(model, now, 1e-5)
+        want = sorted(O.update_actions_state_lazy(now, 1e-5))
+        assert list(zip(ids.tolist(), evs.tolist())) == want, step
+        pops += len(want)
+        dev, lzs = acts.state(), acts.lazy_state()
+        for k in ("remains", "max_duration"):
+            assert np.array_equal(dev[k], np.array(ost[k])), (step, k)
+        for k in ("last_update", "last_value", "date"):
+            assert np.array_equal(lzs[k], np.array(ost[k])), (step, k)
+        assert np.array_equal(lzs["heap_type"], np.array(ost["heap_type"], np.uint8)), step
+    assert pops > 0
