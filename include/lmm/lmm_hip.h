@@ -93,6 +93,13 @@ int lmmhip_res_apply(lmmhip_ctx* ctx, int64_t n_elem_total, int64_t n_var_total,
                      const double* c_bound, const uint8_t* c_flags);
 int lmmhip_res_flatten(lmmhip_ctx* ctx, int64_t n_list, const int32_t* cnst_list, double precision, int64_t* counts3);
 int lmmhip_res_values(lmmhip_ctx* ctx, int64_t n, double* values, uint8_t* reset);
+/* Same, into context-owned pinned host buffers (valid until the next call / lmmhip_ctx_destroy): the
+ * D2H runs at full PCIe rate and the caller scatters from them without another copy. */
+int lmmhip_res_values_pinned(lmmhip_ctx* ctx, int64_t n, const double** values, const uint8_t** reset);
+/* Number of lmmhip_res_flatten calls served by the refresh path (same constraint list and precision,
+ * no element record / slab change / bound crossing the part test since the last flatten: only the
+ * dense penalties and bounds are rewritten). */
+int lmmhip_res_refreshes(lmmhip_ctx* ctx, int64_t* n);
 /* Inspection: download the flattened system the next lmmhip_solve runs on (from lmmhip_upload or
  * lmmhip_res_flatten).  counts3 = {n_var, n_cnst, nnz}; null arrays are skipped (sizes first). */
 int lmmhip_flat_download(lmmhip_ctx* ctx, int64_t* counts3, uint32_t* var_ptr, int32_t* csr_c, double* csr_w,

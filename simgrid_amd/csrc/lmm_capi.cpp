@@ -104,7 +104,7 @@ int lmm_constraint_elements(lmm_sys* s, int64_t c, int* var_rank, double* w, dou
       const auto& x = s->sys.elem(e);
       var_rank[n] = s->sys.var(x.var).rank;
       w[n] = x.weight;
-      val[n] = s->sys.var(x.var).value;
+      val[n] = s->sys.get_value(x.var);
       enabled[n] = x.where == 1;
     }
     n++;

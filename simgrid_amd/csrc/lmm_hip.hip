@@ -6,6 +6,7 @@
 // reference (the FairBottleneck `value == bound` test is exact).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
@@ -95,8 +96,19 @@ struct lmmhip_ctx {
   int64_t res_nE = 0, res_nV = 0, res_nC = 0;  // host table sizes of the last delta batch
   bool res_flat = false;                        // the uploaded system came from lmmhip_res_flatten
   FlatBufs fb_last{};
+  int tune_upd = 0, tune_rdy = 0, tune_sat = 0;
+  double* pin_vals = nullptr;  // pinned host staging of lmmhip_res_values_pinned
+  uint8_t* pin_rst = nullptr;
+  int64_t pin_cap = 0;  // launch-width caps of the round kernels (0 = none)
   int64_t fcap[4] = {0, 0, 0, 0};               // capacities of the flat-system buffers (nV, nC, nnz, nch)
   int64_t res_flat_nv = 0;                      // variable slots covered by that flatten
+  // refresh path of lmmhip_res_flatten: the last flatten's list and precision, host-side structural
+  // flag (element records shipped since), device flags of rs_apply_v / rs_apply_c (kResStruct / kResPenalty)
+  std::vector<int32_t> res_last_list;
+  double res_last_prec = -1.0;
+  bool res_struct_host = true;
+  int32_t* res_dirty = nullptr;
+  int64_t res_refreshes = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp;
 };
@@ -192,6 +204,12 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
       (void)hipFree(b.p);
   for (void* p : c->act_allocs)
     (void)hipFree(p);
+  if (c->res_dirty)
+    (void)hipFree(c->res_dirty);
+  if (c->pin_vals)
+    (void)hipHostFree(c->pin_vals);
+  if (c->pin_rst)
+    (void)hipHostFree(c->pin_rst);
   if (c->h_ctl)
     (void)hipHostFree(c->h_ctl);
   if (c->vstat)
@@ -603,6 +621,12 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
       return rc;
     c->res_capC = cap;
   }
+  if (!c->res_dirty) {
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
+  }
+  if (ne || n_var_total > c->res_nV || n_cnst_total > c->res_nC)
+    c->res_struct_host = true;
   c->res_nE = std::max(c->res_nE, n_elem_total);
   c->res_nV = std::max(c->res_nV, n_var_total);
   c->res_nC = std::max(c->res_nC, n_cnst_total);
@@ -626,7 +650,7 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
              stage(c, 7, v_penalty, nv, &dp) | stage(c, 8, v_bound, nv, &db);
     if (rc)
       return rc;
-    RS_LAUNCH(rs_apply_v, nv, nv, did, deb, dn, dp, db, r);
+    RS_LAUNCH(rs_apply_v, nv, nv, did, deb, dn, dp, db, r, c->res_dirty);
   }
   if (nc) {
     const int32_t* did;
@@ -635,7 +659,7 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
     int rc = stage(c, 9, c_id, nc, &did) | stage(c, 10, c_bound, nc, &db) | stage(c, 11, c_flags, nc, &dfl);
     if (rc)
       return rc;
-    RS_LAUNCH(rs_apply_c, nc, nc, did, db, dfl, r);
+    RS_LAUNCH(rs_apply_c, nc, nc, did, db, dfl, r, c->res_last_prec < 0 ? 1e-5 : c->res_last_prec, c->res_dirty);
   }
   HIPCHK(hipStreamSynchronize(c->stream));  // host delta arrays are borrowed for the call only
   return 0;
@@ -653,6 +677,37 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
   HIPCHK(hipStreamSynchronize(c->stream));
   const ResDev& r = c->res;
   const int64_t nl = n_list, nvs = c->res_nV;
+  // Refresh path: same list, same precision, no element record and no slab / part change since the
+  // last flatten -> the structure (CSR/CSC, dense maps, reset mask) stands; only penalties, variable
+  // bounds and constraint bounds / policies are rewritten in dense order.
+  if (c->res_flat && c->uploaded && !c->res_struct_host && c->res_dirty && precision == c->res_last_prec &&
+      nvs == c->res_flat_nv && size_t(nl) == c->res_last_list.size() &&
+      (nl == 0 || std::memcmp(c->res_last_list.data(), cnst_list, size_t(nl) * sizeof(int32_t)) == 0)) {
+    int32_t flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, c->res_dirty, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!(flags & kResStruct)) {
+      Dev& d = c->d;
+      const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
+      const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
+      const int32_t* list = static_cast<const int32_t*>(c->rs_list.p);
+      const int64_t* lany = static_cast<const int64_t*>(c->rs_lany.p);
+      const int64_t* dcl = static_cast<const int64_t*>(c->rs_dcl.p);
+      RS_LAUNCH(rs_refresh_v, nvs, nvs, r, vm, dv, const_cast<double*>(d.pen), const_cast<double*>(d.vbound));
+      RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, const_cast<double*>(d.cbound), const_cast<uint8_t*>(d.cflags));
+      if ((flags & kResPenalty) && d.nnz > 0)
+        RS_LAUNCH(mm_elem_usage, d.nnz, d);
+      HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      c->res_refreshes++;
+      if (counts3) {
+        counts3[0] = d.nV;
+        counts3[1] = d.nC;
+        counts3[2] = d.nnz;
+      }
+      return 0;
+    }
+  }
   int32_t *pos, *list;
   uint8_t *lpart, *vrst;
   int64_t *lany, *dcl, *cdeg, *cptr, *vm, *dv, *rl, *ro;
@@ -716,11 +771,59 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
   HIPCHK(hipStreamSynchronize(c->stream));  // before the host's list buffer is released
   if ((rc = finish_flat(c, nV, nC, nnz)))
     return rc;
+  c->res_last_list.assign(cnst_list, cnst_list + nl);
+  c->res_last_prec = precision;
+  c->res_struct_host = false;
+  if (c->res_dirty)
+    HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   if (counts3) {
     counts3[0] = nV;
     counts3[1] = nC;
     counts3[2] = nnz;
   }
+  return 0;
+}
+
+int lmmhip_res_refreshes(lmmhip_ctx* c, int64_t* n) {
+  if (!c || !n)
+    return fail(LMMHIP_E_ARG, "null argument");
+  *n = c->res_refreshes;
+  return 0;
+}
+
+int lmmhip_res_values_pinned(lmmhip_ctx* c, int64_t n, const double** values, const uint8_t** reset) {
+  if (!c || !c->uploaded || !c->res_flat)
+    return fail(LMMHIP_E_STATE, "no resident flatten to read values from");
+  if (n != c->res_flat_nv || !values || !reset)
+    return fail(LMMHIP_E_ARG, "values: n must be the variable slot count of the last resident flatten");
+  HIPCHK(hipSetDevice(c->device));
+  if (n > c->pin_cap) {
+    if (c->pin_vals)
+      HIPCHK(hipHostFree(c->pin_vals));
+    if (c->pin_rst)
+      HIPCHK(hipHostFree(c->pin_rst));
+    c->pin_vals = nullptr;
+    c->pin_rst = nullptr;
+    c->pin_cap = 0;
+    const int64_t cap = std::max(n, c->pin_cap + c->pin_cap / 4);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_vals), size_t(cap) * sizeof(double), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_rst), size_t(cap), hipHostMallocDefault));
+    c->pin_cap = cap;
+  }
+  double* vout = nullptr;
+  if (int rc = scratch(c, c->rs_vout, n, &vout))
+    return rc;
+  if (n) {
+    const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
+    const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
+    RS_LAUNCH(rs_values, n, n, vm, dv, c->d.x, vout);
+    HIPCHK(hipMemcpyAsync(c->pin_vals, vout, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->pin_rst, c->rs_vrst.p, size_t(n), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *values = c->pin_vals;
+  *reset = c->pin_rst;
   return 0;
 }
 
@@ -902,6 +1005,11 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
 
 // Slots: 0 mm_init_cnsts, 1 mm_init_vars, 2 mm_vote, 3 mm_ready, 4 mm_saturate, 5 mm_update,
 // 6 compaction.
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
@@ -910,23 +1018,29 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   LAUNCH(1, -1, mm_init_vars, grid_for(d.nV, kBlock), kBlock, d);
   LAUNCH(1, -1, mm_clist, gC, kBlock, d, 0, 0, 1);
   HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
-  const int gU = gC;  // mm_update: thread per constraint, identity order
+  // Launch-width caps (tuning knobs, environment; 0 = uncapped): fewer blocks cut the fixed per-round
+  // cost of the grid-stride round kernels once the alive set is small.
+  const int cap_upd = env_int("LMMHIP_UPD_BLOCKS", c->tune_upd);
+  const int cap_rdy = env_int("LMMHIP_READY_BLOCKS", c->tune_rdy);
+  const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat);
+  auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
+  const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
   int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
   int buf = 0, cb = 0, chunk = 2;
   for (;;) {
-    const int gL = grid_for(ncl, kBlock);
+    const int gL = capped(grid_for(ncl, kBlock), cap_rdy);
     for (int k = 0; k < chunk; k++, r++) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
       if (c->sat_waves == 1)
-        LAUNCH(4, r, mm_saturate<1>, gL, kBlock, d, int(r), cb, gL);
+        LAUNCH(4, r, mm_saturate<1>, capped(gL, cap_sat), kBlock, d, int(r), cb, gL);
       else if (c->sat_waves == 2)
-        LAUNCH(4, r, mm_saturate<2>, grid_for(2 * ncl, kBlock), kBlock, d, int(r), cb, gL);
+        LAUNCH(4, r, mm_saturate<2>, capped(grid_for(2 * ncl, kBlock), cap_sat), kBlock, d, int(r), cb, gL);
       else
-        LAUNCH(4, r, mm_saturate<4>, grid_for(4 * ncl, kBlock), kBlock, d, int(r), cb, gL);
+        LAUNCH(4, r, mm_saturate<4>, capped(grid_for(4 * ncl, kBlock), cap_sat), kBlock, d, int(r), cb, gL);
       LAUNCH(5, r, mm_update, gU, kBlock, d, int(r), prec);
     }
     LAUNCH(6, r, mm_done, 1, kBlock, d, gU);

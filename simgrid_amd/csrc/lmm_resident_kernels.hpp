@@ -50,26 +50,44 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// Structural-change flags of a delta batch (read by lmmhip_res_flatten's refresh path): bit0 = the
+// system's structure may have changed (slab moved / resized, a constraint's bound crossed the "part"
+// test at the last flatten's precision), bit1 = a penalty changed (per-element usage w/p is stale).
+constexpr int kResStruct = 1, kResPenalty = 2;
+
 __global__ void __launch_bounds__(kBlock)
     rs_apply_v(int64_t n, const int32_t* __restrict__ id, const int64_t* __restrict__ eb,
                const int32_t* __restrict__ ne, const double* __restrict__ pen, const double* __restrict__ bnd,
-               ResDev r) {
+               ResDev r, int32_t* dirty) {
+  int f = 0;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
     const int32_t v = id[i];
+    if (r.v_ebase[v] != eb[i] || r.v_n[v] != ne[i])
+      f |= kResStruct;
+    if (r.v_pen[v] != pen[i])
+      f |= kResPenalty;
     r.v_ebase[v] = eb[i];
     r.v_n[v] = ne[i];
     r.v_pen[v] = pen[i];
     r.v_bound[v] = bnd[i];
   }
+  if (f)
+    atomicOr(dirty, f);
 }
 
 __global__ void __launch_bounds__(kBlock)
     rs_apply_c(int64_t n, const int32_t* __restrict__ id, const double* __restrict__ b,
-               const uint8_t* __restrict__ fl, ResDev r) {
+               const uint8_t* __restrict__ fl, ResDev r, double prec, int32_t* dirty) {
+  int f = 0;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-    r.c_bound[id[i]] = b[i];
+    const double ob = r.c_bound[id[i]], nb = b[i];
+    if ((ob > ob * prec) != (nb > nb * prec))
+      f |= kResStruct;
+    r.c_bound[id[i]] = nb;
     r.c_fl[id[i]] = fl[i];
   }
+  if (f)
+    atomicOr(dirty, f);
 }
 
 // pos[c] = list position of listed constraint c (pos pre-set to -1); lpart[i] = bound > bound * prec
@@ -186,6 +204,18 @@ __global__ void __launch_bounds__(kBlock)
         k++;
       }
     }
+  }
+}
+
+// Refresh path (no structural change since the last flatten): the dense per-variable arrays only.
+__global__ void __launch_bounds__(kBlock)
+    rs_refresh_v(int64_t nv, ResDev r, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv, double* pen,
+                 double* vbound) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
+    if (!vm[v])
+      continue;
+    pen[dv[v]] = r.v_pen[v];
+    vbound[dv[v]] = r.v_bound[v];
   }
 }
 

@@ -264,10 +264,12 @@ Id System::variable_new(void* id, double penalty, double bound, size_t n_cnst) {
   } else {
     check(vars_.size() < size_t(std::numeric_limits<Id>::max()), "too many variables");
     vars_.emplace_back();
+    values_.push_back(0.0);
     v = Id(vars_.size() - 1);
   }
   VarRec& r = vars_[v];
   r = VarRec();
+  values_[v] = 0.0;
   r.id = id;
   r.rank = next_var_rank_++;
   r.penalty = penalty;
@@ -460,7 +462,7 @@ void System::disable_var(Id v) {
   }
   r.penalty = 0.0;
   r.staged = 0.0;
-  r.value = 0.0;
+  values_[v] = 0.0;
   touch_v(v);
   flat_valid_ = false;
 }
@@ -588,7 +590,7 @@ double System::get_usage(Id c) const {
     const ElemRec& x = elems_[e];
     if (x.weight <= 0)
       continue;
-    double u = x.weight * vars_[x.var].value;
+    double u = x.weight * values_[x.var];
     r = fat ? std::max(r, u) : r + u;
   }
   return r;
@@ -631,9 +633,9 @@ void System::check_certificate(double prec, double* max_excess, int64_t* n_infea
       if (x.weight <= 0)
         continue;
       const VarRec& r = vars_[x.var];
-      const double u = x.weight * r.value;
+      const double u = x.weight * values_[x.var];
       usage[c] = fat ? std::max(usage[c], u) : usage[c] + u;
-      top[c] = std::max(top[c], r.value * r.penalty);
+      top[c] = std::max(top[c], values_[x.var] * r.penalty);
     }
   }
   double worst = -1e300;
@@ -651,11 +653,12 @@ void System::check_certificate(double prec, double* max_excess, int64_t* n_infea
   }
   for (Id v = 0; v < Id(vars_.size()); v++) {
     const VarRec& r = vars_[v];
-    if (!r.live || !(r.penalty > 0) || !(r.value > 0))
+    const double rv = values_[v];
+    if (!r.live || !(r.penalty > 0) || !(rv > 0))
       continue;
-    if (r.bound > 0 && std::fabs(r.value - r.bound) <= std::max(prec, 1e-9 * r.bound))
+    if (r.bound > 0 && std::fabs(rv - r.bound) <= std::max(prec, 1e-9 * r.bound))
       continue;  // at its bound
-    const double lvl = r.value * r.penalty;
+    const double lvl = rv * r.penalty;
     bool ok = false;
     for (int i = 0; i < r.n_elems && !ok; i++) {
       const ElemRec& x = elems_[r.ebase + i];
@@ -698,7 +701,7 @@ void System::flatten_maxmin(Flat& f, const std::vector<Id>& list) {
     bool any = false;
     for (Id e = k.en_head; e != kNone; e = elems_[e].next) {
       const ElemRec& x = elems_[e];
-      vars_[x.var].value = 0.0;
+      values_[x.var] = 0.0;
       if (part && x.weight > 0) {
         any = true;
         vmark[x.var] = 1;
@@ -740,7 +743,7 @@ void System::flatten_fair(Flat& f) {
   std::vector<int32_t> dense_c(cnsts_.size(), -1);
   for (Id v = vset_head_; v != kNone; v = vars_[v].next) {
     VarRec& r = vars_[v];
-    r.value = 0.0;
+    values_[v] = 0.0;
     if (r.penalty > 0.0) {
       bool any_nz = false, any_pos = false;
       for (int i = 0; i < r.n_elems; i++) {
@@ -748,7 +751,7 @@ void System::flatten_fair(Flat& f) {
         any_pos |= elems_[r.ebase + i].weight > 0.0;
       }
       if (!any_nz)
-        r.value = 1.0;
+        values_[v] = 1.0;
       else
         check(any_pos, "FairBottleneck: negative consumption weights are not supported");
     }
@@ -799,7 +802,7 @@ void System::flatten_into(Flat& f) {
 
 void System::scatter_values(const double* x) {
   for (size_t i = 0; i < flat_.dense_vars.size(); i++)
-    vars_[flat_.dense_vars[i]].value = x[i];
+    values_[flat_.dense_vars[i]] = x[i];
 }
 
 void System::finish_solve() {
@@ -1030,14 +1033,15 @@ void System::prepare_resident() {
 void System::fetch_resident() {
   auto t0 = std::chrono::steady_clock::now();
   const size_t n = vars_.size();
-  std::vector<double> vals(n);
-  std::vector<uint8_t> rst(n);
-  int rc = lmmhip_res_values(ctx(), int64_t(n), vals.data(), rst.data());
+  const double* vals = nullptr;
+  const uint8_t* rst = nullptr;
+  int rc = lmmhip_res_values_pinned(ctx(), int64_t(n), &vals, &rst);
   if (rc)
     fatal(std::string("resident fetch failed: ") + lmmhip_last_error());
-  for (size_t v = 0; v < n; v++)
+  double* out = values_.data();
+  for (size_t v = 0; v < n; v++)  // two streams over pinned memory, one over the value column
     if (rst[v])
-      vars_[v].value = vals[v];
+      out[v] = vals[v];
   res_prepared_ = false;
   stats_.fetch_ms = ms_since(t0);
   finish_solve();

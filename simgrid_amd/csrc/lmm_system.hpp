@@ -55,7 +55,7 @@ struct CnstRec {
 };
 
 struct VarRec {
-  double penalty = 0.0, staged = 0.0, bound = -1.0, value = 0.0;
+  double penalty = 0.0, staged = 0.0, bound = -1.0;  // value: System::values_ (a column of its own)
   int share = 1;
   int rank = 0;
   unsigned visited = 0;
@@ -109,7 +109,7 @@ public:
   void fetch();
 
   // read API (maxmin.hpp:296-331, :188-247)
-  double get_value(Id v) const { return vars_[v].value; }
+  double get_value(Id v) const { return values_[v]; }
   double get_bound(Id v) const { return vars_[v].bound; }
   double get_penalty(Id v) const { return vars_[v].penalty; }
   int number_of_constraints(Id v) const { return vars_[v].n_elems; }
@@ -120,7 +120,7 @@ public:
   const CnstRec& cnst(Id c) const { return cnsts_[c]; }
   const VarRec& var(Id v) const { return vars_[v]; }
   void reset_concurrency_maximum(Id c) { cnsts_[c].conc_maximum = 0; }
-  void set_value(Id v, double x) { vars_[v].value = x; }
+  void set_value(Id v, double x) { values_[v] = x; }
   // elements of c in print order (enabled list, then disabled list), as element ids
   std::vector<Id> constraint_elements(Id c) const;
   const ElemRec& elem(Id e) const { return elems_[e]; }
@@ -224,6 +224,7 @@ private:
 
   std::vector<CnstRec> cnsts_;
   std::vector<VarRec> vars_;
+  std::vector<double> values_;  // Variable::value_, kept as a column: the solve writes it as a stream
   std::vector<Id> free_var_ids_;
   std::vector<ElemRec> elems_;
   std::vector<std::vector<int64_t>> free_slabs_;  // by capacity (small caps only)

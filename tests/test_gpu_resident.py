@@ -128,3 +128,45 @@ def test_resident_fair_bottleneck_keeps_host_flatten():
     b.solve()
     worst, bad = K.compare_values(vsa, vsb)
     assert not bad, (worst, bad[:5])
+
+
+def test_resident_refresh_path_bounds_and_penalties():
+    """Steps that only move penalties (staying > 0), variable bounds and constraint bounds (staying > 0)
+    keep the structure: the device flatten takes the refresh path (dense penalties / bounds rewritten,
+    structure reused) and must still equal the host flatten bit for bit."""
+    import ctypes as ct
+
+    ops = K.random_script(21, n_cnst=50, n_var=300, conc_limits=False)
+    a, csa, vsa = K.replay(L, ops)
+    a.set_resident(True)
+    b, csb, vsb = K.replay(L, ops)
+    rng = random.Random(4)
+    _flat_equal(_split_solve(a), _split_solve(b))
+    nref = ct.c_int64()
+    for step in range(4):
+        live = [k for k in sorted(vsa) if vsa[k].get_penalty() > 0]
+        for k in rng.sample(live, 20):
+            p = rng.choice([0.5, 1.5, 3.0])
+            a.update_variable_penalty(vsa[k], p)
+            b.update_variable_penalty(vsb[k], p)
+        for k in rng.sample(live, 10):
+            bd = round(rng.uniform(0.05, 3.0), 3)
+            a.update_variable_bound(vsa[k], bd)
+            b.update_variable_bound(vsb[k], bd)
+        for k in rng.sample([k for k in sorted(csa) if csa[k].get_bound() > 0], 5):
+            bd = round(rng.uniform(0.5, 20.0), 3)
+            a.update_constraint_bound(csa[k], bd)
+            b.update_constraint_bound(csb[k], bd)
+        _flat_equal(_split_solve(a), _split_solve(b))
+        worst, bad = K.compare_values(vsa, vsb)
+        assert not bad, (step, worst, bad[:5])
+        L._check_hip(L.lib().lmmhip_res_refreshes(a.device_ctx(), ct.byref(nref)))
+        assert nref.value == step + 1
+    # a structural step (a new flow) goes back to the full rebuild
+    v = a.variable_new(None, 1.0, -1.0, 2)
+    a.expand(csa[0], v, 1.0)
+    w = b.variable_new(None, 1.0, -1.0, 2)
+    b.expand(csb[0], w, 1.0)
+    _flat_equal(_split_solve(a), _split_solve(b))
+    L._check_hip(L.lib().lmmhip_res_refreshes(a.device_ctx(), ct.byref(nref)))
+    assert nref.value == 4
