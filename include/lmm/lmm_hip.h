@@ -78,7 +78,7 @@ int lmmhip_update_cnsts(lmmhip_ctx* ctx, const double* cnst_bound);
  *
  * lmmhip_res_apply: one delta batch.  *_total = sizes of the host tables (the mirror grows to them,
  *   keeping its contents).  Element e: constraint id (-1 = unused), weight, flags bit0 = in its
- *   constraint's enabled list.  Variable v: slab base (first element id), elements in use (0 = dead),
+ *   constraint's enabled list.  Variable v: slab base (first element id), elements in use (-1 = dead),
  *   penalty, bound.  Constraint c: bound, flags bit0 = FATPIPE.  Host arrays are borrowed.
  * lmmhip_res_flatten: build the max-min system of the listed constraints (list order = dense order:
  *   the active set, or the modified set in selective mode) from the mirror; then lmmhip_solve(MAXMIN)
@@ -92,6 +92,11 @@ int lmmhip_res_apply(lmmhip_ctx* ctx, int64_t n_elem_total, int64_t n_var_total,
                      const double* v_penalty, const double* v_bound, int64_t nc, const int32_t* c_id,
                      const double* c_bound, const uint8_t* c_flags);
 int lmmhip_res_flatten(lmmhip_ctx* ctx, int64_t n_list, const int32_t* cnst_list, double precision, int64_t* counts3);
+/* FairBottleneck flavour (System::flatten_fair, fair_bottleneck.cpp:29-50): every active constraint with
+ * an enabled element of weight > 0 (cflags bit1 = one of weight 0), every live variable with penalty > 0
+ * and such an element; values of the other live variables reset to 0, or 1.0 when penalised with no
+ * non-zero weight; CSC chunks built on the device.  Then lmmhip_solve(FAIR_BOTTLENECK). */
+int lmmhip_res_flatten_fair(lmmhip_ctx* ctx, int64_t n_list, const int32_t* cnst_list, int64_t* counts3);
 int lmmhip_res_values(lmmhip_ctx* ctx, int64_t n, double* values, uint8_t* reset);
 /* Same, into context-owned pinned host buffers (valid until the next call / lmmhip_ctx_destroy): the
  * D2H runs at full PCIe rate and the caller scatters from them without another copy. */

@@ -109,8 +109,9 @@ struct lmmhip_ctx {
   bool res_struct_host = true;
   int32_t* res_dirty = nullptr;
   int64_t res_refreshes = 0;
+  int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
-      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp;
+      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
 
 static void free_all(lmmhip_ctx* c) {
@@ -196,7 +197,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
       (void)hipFree(p);
   for (lmmhip_ctx::Scr* b : {&c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
-                             &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp})
+                             &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
+                             &c->rs_nck, &c->rs_cch})
     if (b->p)
       (void)hipFree(b->p);
   for (lmmhip_ctx::Scr& b : c->rs_stage)
@@ -590,8 +592,8 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
     if (e_id[i] < 0 || e_id[i] >= n_elem_total || e_cnst[i] < -1 || e_cnst[i] >= n_cnst_total)
       return fail(LMMHIP_E_ARG, "element delta out of range");
   for (int64_t i = 0; i < nv; i++)
-    if (v_id[i] < 0 || v_id[i] >= n_var_total || v_nelem[i] < 0 || v_ebase[i] < 0 ||
-        v_ebase[i] + v_nelem[i] > n_elem_total)
+    if (v_id[i] < 0 || v_id[i] >= n_var_total || v_nelem[i] < -1 || v_ebase[i] < 0 ||
+        v_ebase[i] + std::max(v_nelem[i], 0) > n_elem_total)
       return fail(LMMHIP_E_ARG, "variable delta out of range");
   for (int64_t i = 0; i < nc; i++)
     if (c_id[i] < 0 || c_id[i] >= n_cnst_total)
@@ -622,8 +624,8 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
     c->res_capC = cap;
   }
   if (!c->res_dirty) {
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), sizeof(int32_t)));
-    HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 2 * sizeof(int32_t)));  // flags, fair error
+    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 2 * sizeof(int32_t), c->stream));
   }
   if (ne || n_var_total > c->res_nV || n_cnst_total > c->res_nC)
     c->res_struct_host = true;
@@ -665,7 +667,10 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
   return 0;
 }
 
-int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, double precision, int64_t* counts3) {
+}  // extern "C"
+
+static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* cnst_list, double precision,
+                       int64_t* counts3) {
   if (!c)
     return fail(LMMHIP_E_ARG, "null context");
   if (n_list < 0 || (n_list && !cnst_list))
@@ -680,7 +685,8 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
   // Refresh path: same list, same precision, no element record and no slab / part change since the
   // last flatten -> the structure (CSR/CSC, dense maps, reset mask) stands; only penalties, variable
   // bounds and constraint bounds / policies are rewritten in dense order.
-  if (c->res_flat && c->uploaded && !c->res_struct_host && c->res_dirty && precision == c->res_last_prec &&
+  if (!fair && c->res_flat && c->res_flat_kind == LMMHIP_KIND_MAXMIN && c->uploaded && !c->res_struct_host &&
+      c->res_dirty && precision == c->res_last_prec &&
       nvs == c->res_flat_nv && size_t(nl) == c->res_last_list.size() &&
       (nl == 0 || std::memcmp(c->res_last_list.data(), cnst_list, size_t(nl) * sizeof(int32_t)) == 0)) {
     int32_t flags = 0;
@@ -694,7 +700,8 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
       const int64_t* lany = static_cast<const int64_t*>(c->rs_lany.p);
       const int64_t* dcl = static_cast<const int64_t*>(c->rs_dcl.p);
       RS_LAUNCH(rs_refresh_v, nvs, nvs, r, vm, dv, const_cast<double*>(d.pen), const_cast<double*>(d.vbound));
-      RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, const_cast<double*>(d.cbound), const_cast<uint8_t*>(d.cflags));
+      RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, nullptr, const_cast<double*>(d.cbound),
+                const_cast<uint8_t*>(d.cflags));
       if ((flags & kResPenalty) && d.nnz > 0)
         RS_LAUNCH(mm_elem_usage, d.nnz, d);
       HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
@@ -709,9 +716,10 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
     }
   }
   int32_t *pos, *list;
-  uint8_t *lpart, *vrst;
+  uint8_t *lpart, *vrst, *lzero;
   int64_t *lany, *dcl, *cdeg, *cptr, *vm, *dv, *rl, *ro;
   int rc = scratch(c, c->rs_pos, c->res_nC, &pos) | scratch(c, c->rs_list, nl, &list) |
+           scratch(c, c->rs_lzero, nl, &lzero) |
            scratch(c, c->rs_lpart, nl, &lpart) | scratch(c, c->rs_lany, nl + 1, &lany) |
            scratch(c, c->rs_dcl, nl + 1, &dcl) | scratch(c, c->rs_cdeg, nl + 1, &cdeg) |
            scratch(c, c->rs_cptr, nl + 1, &cptr) | scratch(c, c->rs_vrst, nvs, &vrst) |
@@ -724,11 +732,23 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
   if (c->res_nC)
     HIPCHK(hipMemsetAsync(pos, 0xFF, size_t(c->res_nC) * sizeof(int32_t), c->stream));
   HIPCHK(hipMemsetAsync(cdeg, 0, size_t(nl + 1) * sizeof(int64_t), c->stream));
-  RS_LAUNCH(rs_pos, nl, nl, list, r, precision, pos, lpart, lany);
-  RS_LAUNCH(rs_mark, nvs, nvs, r, pos, lpart, lany, vrst, vm);
+  if (!c->res_dirty) {
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 2 * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 2 * sizeof(int32_t), c->stream));
+  }
+  RS_LAUNCH(rs_pos, nl, nl, list, r, precision, int(fair), pos, lpart, lany, lzero);
+  if (fair) {
+    HIPCHK(hipMemsetAsync(c->res_dirty + 1, 0, sizeof(int32_t), c->stream));
+    RS_LAUNCH(rs_mark_fair, nvs, nvs, r, pos, lany, lzero, vrst, vm, c->res_dirty + 1);
+  } else {
+    RS_LAUNCH(rs_mark, nvs, nvs, r, pos, lpart, lany, vrst, vm);
+  }
   if ((rc = dev_scan(c, lany, dcl, nl + 1)))
     return rc;
-  RS_LAUNCH(rs_rowlen, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
+  if (fair)
+    RS_LAUNCH(rs_rowlen_fair, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
+  else
+    RS_LAUNCH(rs_rowlen, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
   if ((rc = dev_scan(c, vm, dv, nvs + 1)) || (rc = dev_scan(c, rl, ro, nvs + 1)) ||
       (rc = dev_scan(c, cdeg, cptr, nl + 1)))
     return rc;
@@ -739,23 +759,44 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
     return rc;
   if (nnz > INT32_MAX)
     return fail(LMMHIP_E_ARG, "resident flatten: more than 2^31 active elements");
+  int64_t nch = 0;
+  int64_t *nck = nullptr, *cch = nullptr;
+  if (fair) {  // chunk counts before the allocation (lmm_fb_kernels.hpp)
+    int32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, c->res_dirty + 1, sizeof(err), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (err)
+      return fail(LMMHIP_E_ARG, "FairBottleneck: negative consumption weights are not supported");
+    if ((rc = scratch(c, c->rs_nck, nC + 1, &nck) | scratch(c, c->rs_cch, nC + 1, &cch)))
+      return rc;
+    RS_LAUNCH(rs_nchunks, nC, nC, cdeg, kFbChunk, nck);
+    if ((rc = dev_scan(c, nck, cch, nC + 1)))
+      return rc;
+    nch = read_i64(c, cch + nC, &rc);
+    if (rc)
+      return rc;
+  }
   FlatBufs fb;
-  if ((rc = alloc_flat(c, nV, nC, nnz, 0, &fb)))
+  if ((rc = alloc_flat(c, nV, nC, nnz, nch, &fb)))
     return rc;
   c->res_flat = true;
+  c->res_flat_kind = fair ? LMMHIP_KIND_FAIR_BOTTLENECK : LMMHIP_KIND_MAXMIN;
   c->res_flat_nv = nvs;
   int32_t *rowid, *kidx, *skey, *sval;
   rc = scratch(c, c->rs_rowid, nnz, &rowid) | scratch(c, c->rs_kidx, nnz, &kidx) |
        scratch(c, c->rs_skey, nnz, &skey) | scratch(c, c->rs_sval, nnz, &sval);
   if (rc)
     return rc;
-  RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, fb.cb, fb.cf);
+  RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, fair ? lzero : nullptr, fb.cb, fb.cf);
   RS_LAUNCH(rs_write, nvs, nvs, r, pos, lany, dcl, vm, dv, ro, fb.vp, fb.csr_c, fb.csr_w, fb.pen, fb.vb, fb.cvar0,
             rowid, kidx);
   const uint32_t nnz32 = uint32_t(nnz);
   HIPCHK(hipMemcpyAsync(fb.vp + nV, &nnz32, sizeof(nnz32), hipMemcpyHostToDevice, c->stream));
   RS_LAUNCH(rs_ptr32, nC, nC, cptr, fb.cp);
-  HIPCHK(hipMemsetAsync(fb.cch, 0, size_t(nC + 1) * sizeof(int32_t), c->stream));  // no FB chunks
+  if (fair)
+    RS_LAUNCH(rs_chunks, nC, nC, cptr, nck, cch, kFbChunk, fb.cch, fb.chc, fb.chb);
+  else
+    HIPCHK(hipMemsetAsync(fb.cch, 0, size_t(nC + 1) * sizeof(int32_t), c->stream));  // no FB chunks
   if (nnz) {
     int bits = 1;
     while (bits < 31 && (int64_t(1) << bits) < nC)
@@ -783,6 +824,16 @@ int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, 
     counts3[2] = nnz;
   }
   return 0;
+}
+
+extern "C" {
+
+int lmmhip_res_flatten(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, double precision, int64_t* counts3) {
+  return res_flatten(c, false, n_list, cnst_list, precision, counts3);
+}
+
+int lmmhip_res_flatten_fair(lmmhip_ctx* c, int64_t n_list, const int32_t* cnst_list, int64_t* counts3) {
+  return res_flatten(c, true, n_list, cnst_list, 0.0, counts3);
 }
 
 int lmmhip_res_refreshes(lmmhip_ctx* c, int64_t* n) {
@@ -817,7 +868,7 @@ int lmmhip_res_values_pinned(lmmhip_ctx* c, int64_t n, const double** values, co
   if (n) {
     const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
     const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
-    RS_LAUNCH(rs_values, n, n, vm, dv, c->d.x, vout);
+    RS_LAUNCH(rs_values, n, n, vm, dv, static_cast<const uint8_t*>(c->rs_vrst.p), c->d.x, vout);
     HIPCHK(hipMemcpyAsync(c->pin_vals, vout, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->pin_rst, c->rs_vrst.p, size_t(n), hipMemcpyDeviceToHost, c->stream));
   }
@@ -868,7 +919,7 @@ int lmmhip_res_values(lmmhip_ctx* c, int64_t n, double* values, uint8_t* reset) 
   const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
   const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
   if (n) {
-    RS_LAUNCH(rs_values, n, n, vm, dv, c->d.x, vout);
+    RS_LAUNCH(rs_values, n, n, vm, dv, static_cast<const uint8_t*>(c->rs_vrst.p), c->d.x, vout);
     HIPCHK(hipMemcpyAsync(values, vout, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(reset, c->rs_vrst.p, size_t(n), hipMemcpyDeviceToHost, c->stream));
   }
@@ -892,8 +943,8 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
     return fail(LMMHIP_E_STATE, "solve before upload");
   if (kind != LMMHIP_KIND_MAXMIN && kind != LMMHIP_KIND_FAIR_BOTTLENECK)
     return fail(LMMHIP_E_ARG, "unknown solver kind");
-  if (kind == LMMHIP_KIND_FAIR_BOTTLENECK && c->res_flat)
-    return fail(LMMHIP_E_STATE, "a resident flatten builds a max-min system (no fair-bottleneck chunks)");
+  if (c->res_flat && kind != c->res_flat_kind)
+    return fail(LMMHIP_E_STATE, "the resident flatten was built for the other solver kind");
   HIPCHK(hipSetDevice(c->device));
   for (int i = 0; i < 8; i++) {
     c->stats.kernel_ms[i] = 0;

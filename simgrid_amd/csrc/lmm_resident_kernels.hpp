@@ -92,17 +92,20 @@ __global__ void __launch_bounds__(kBlock)
 
 // pos[c] = list position of listed constraint c (pos pre-set to -1); lpart[i] = bound > bound * prec
 // (maxmin.cpp:523-525).  lany[i] (int64, scanned later) is cleared here.
+// FairBottleneck (fair_bottleneck.cpp:29-50) lists every active constraint without a bound test; lzero
+// (cleared here) then marks the ones with an enabled zero-weight element (cflags bit1).
 __global__ void __launch_bounds__(kBlock)
-    rs_pos(int64_t nl, const int32_t* __restrict__ list, ResDev r, double prec, int32_t* pos, uint8_t* lpart,
-           int64_t* lany) {
+    rs_pos(int64_t nl, const int32_t* __restrict__ list, ResDev r, double prec, int fair, int32_t* pos,
+           uint8_t* lpart, int64_t* lany, uint8_t* lzero) {
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i <= nl; i += int64_t(gridDim.x) * kBlock) {
     lany[i] = 0;
     if (i == nl)
       break;
+    lzero[i] = 0;
     const int32_t c = list[i];
     pos[c] = int32_t(i);
     const double b = r.c_bound[c];
-    lpart[i] = b > b * prec;
+    lpart[i] = fair ? 1 : b > b * prec;
   }
 }
 
@@ -164,16 +167,102 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-// Dense constraint records in list order.
+// FairBottleneck membership pass (System::flatten_fair, fair_bottleneck.cpp:29-50), per variable slot:
+// every live variable is reset (vrst = 1), to 1.0 when it has a positive penalty and no non-zero weight
+// (vrst = 3); constraints with an enabled element of weight > 0 are listed (lany), those with an
+// enabled zero-weight one get the FATPIPE quirk flag (lzero); membership itself needs the final lany
+// and is decided by rs_rowlen_fair.  A penalised variable with non-zero but no positive weight is the
+// host's "negative consumption weights" error (*err).
+__global__ void __launch_bounds__(kBlock)
+    rs_mark_fair(int64_t nv, ResDev r, const int32_t* __restrict__ pos, int64_t* lany, uint8_t* lzero,
+                 uint8_t* vrst, int64_t* vm, int32_t* err) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
+    if (v == nv) {
+      vm[v] = 0;
+      break;
+    }
+    const int n = r.v_n[v];
+    const int64_t b = r.v_ebase[v];
+    bool nz = false, posw = false;
+    for (int i = 0; i < n; i++) {
+      const double w = r.e_w[b + i];
+      nz |= w != 0.0;
+      posw |= w > 0.0;
+      if (!(r.e_fl[b + i] & kResElemEnabled))
+        continue;
+      const int32_t p = pos[r.e_cnst[b + i]];
+      if (p < 0)
+        continue;
+      if (w > 0)
+        lany[p] = 1;
+      else if (w == 0.0)
+        lzero[p] = 1;
+    }
+    const bool pen = r.v_pen[v] > 0.0;
+    vrst[v] = n < 0 ? 0 : (pen && !nz) ? 3 : 1;
+    vm[v] = 0;
+    if (n >= 0 && pen && nz && !posw)
+      atomicOr(err, 1);
+  }
+}
+
+// Row lengths + membership (live, penalty > 0, an element of weight > 0 on a listed constraint).
+__global__ void __launch_bounds__(kBlock)
+    rs_rowlen_fair(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
+                   const int64_t* __restrict__ dcl, int64_t* vm, int64_t* rl, int64_t* cdeg) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
+    if (v == nv) {
+      rl[v] = 0;
+      break;
+    }
+    int64_t cnt = 0;
+    if (r.v_pen[v] > 0.0) {
+      const int64_t b = r.v_ebase[v];
+      const int n = r.v_n[v];
+      for (int i = 0; i < n; i++) {
+        const int32_t p = pos[r.e_cnst[b + i]];
+        if (p >= 0 && lany[p] && r.e_w[b + i] > 0) {
+          cnt++;
+          atomicAdd(reinterpret_cast<unsigned long long*>(cdeg + dcl[p]), 1ull);
+        }
+      }
+    }
+    rl[v] = cnt;
+    vm[v] = cnt > 0;
+  }
+}
+
+// Dense constraint records in list order (fair: cflags bit1 = enabled zero-weight element).
 __global__ void __launch_bounds__(kBlock)
     rs_cmeta(int64_t nl, const int32_t* __restrict__ list, ResDev r, const int64_t* __restrict__ lany,
-             const int64_t* __restrict__ dcl, double* cbound, uint8_t* cflags) {
+             const int64_t* __restrict__ dcl, const uint8_t* __restrict__ lzero, double* cbound, uint8_t* cflags) {
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nl; i += int64_t(gridDim.x) * kBlock) {
     if (!lany[i])
       continue;
     const int32_t c = list[i];
     cbound[dcl[i]] = r.c_bound[c];
-    cflags[dcl[i]] = (r.c_fl[c] & kResCnstFatpipe) ? 1 : 0;
+    cflags[dcl[i]] = uint8_t(((r.c_fl[c] & kResCnstFatpipe) ? 1 : 0) | (lzero && lzero[i] ? 2 : 0));
+  }
+}
+
+// FairBottleneck CSC chunks (lmm_fb_kernels.hpp): nck[j] chunks of kChunk elements per constraint.
+__global__ void __launch_bounds__(kBlock)
+    rs_nchunks(int64_t nc, const int64_t* __restrict__ cdeg, int chunk, int64_t* nck) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j <= nc; j += int64_t(gridDim.x) * kBlock)
+    nck[j] = j < nc ? (cdeg[j] + chunk - 1) / chunk : 0;
+}
+
+__global__ void __launch_bounds__(kBlock)
+    rs_chunks(int64_t nc, const int64_t* __restrict__ cptr, const int64_t* __restrict__ nck,
+              const int64_t* __restrict__ cch, int chunk, int32_t* c_ch, int32_t* ch_cnst, uint32_t* ch_beg) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j <= nc; j += int64_t(gridDim.x) * kBlock) {
+    c_ch[j] = int32_t(cch[j]);
+    if (j == nc)
+      break;
+    for (int64_t k = 0; k < nck[j]; k++) {
+      ch_cnst[cch[j] + k] = int32_t(j);
+      ch_beg[cch[j] + k] = uint32_t(cptr[j] + k * chunk);
+    }
   }
 }
 
@@ -238,9 +327,9 @@ __global__ void __launch_bounds__(kBlock) rs_ptr32(int64_t n, const int64_t* __r
 // vrst set are written back by the host).
 __global__ void __launch_bounds__(kBlock)
     rs_values(int64_t nv, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
-              const double* __restrict__ x, double* out) {
+              const uint8_t* __restrict__ vrst, const double* __restrict__ x, double* out) {
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock)
-    out[v] = vm[v] ? x[dv[v]] : 0.0;
+    out[v] = vm[v] ? x[dv[v]] : vrst[v] == 3 ? 1.0 : 0.0;
 }
 
 }  // namespace lmmdev

@@ -819,7 +819,7 @@ void System::finish_solve() {
 // solve
 // ------------------------------------------------------------------------------------------
 void System::prepare() {
-  if (resident_ && kind_ == SolverKind::MAXMIN) {
+  if (resident_) {
     prepare_resident();
     return;
   }
@@ -951,7 +951,7 @@ void System::drain_deltas(ResPacked& p) {
   for (size_t i = 0; i < nv; i++) {
     const VarRec& r = vars_[res_lv_[i]];
     p.v_eb[i] = r.ebase;
-    p.v_n[i] = r.live ? r.n_elems : 0;
+    p.v_n[i] = r.live ? r.n_elems : -1;
     p.v_p[i] = r.penalty;
     p.v_b[i] = r.bound;
   }
@@ -993,14 +993,15 @@ void System::prepare_resident() {
   // The active set rarely changes between simulation steps: its list (a pointer chase over the
   // constraint records, ~0.1 s at 1e6 constraints) is cached until make_cnst_(in)active.
   std::vector<Id> mod_list;
-  if (selective_)
+  if (selective_ && kind_ == SolverKind::MAXMIN)
     mod_list = solve_constraint_list();
   else if (!act_cache_ok_) {
     act_cache_ = solve_constraint_list();
     act_cache_ok_ = true;
   }
-  const std::vector<Id>& list = selective_ ? mod_list : act_cache_;
-  if (selective_) {  // Lazy side effect, maxmin.cpp:536-538 (the walk the reference does at init)
+  const std::vector<Id>& list = selective_ && kind_ == SolverKind::MAXMIN ? mod_list : act_cache_;
+  const bool fair = kind_ == SolverKind::FAIR_BOTTLENECK;
+  if (selective_ && !fair) {  // Lazy side effect, maxmin.cpp:536-538 (the walk the reference does at init)
     const double prec = maxmin_precision;
     for (Id c : list) {
       const CnstRec& k = cnsts_[c];
@@ -1018,7 +1019,8 @@ void System::prepare_resident() {
   stats_.flatten_ms = ms_since(t0);
   auto t1 = std::chrono::steady_clock::now();
   int64_t cnt[3] = {0, 0, 0};
-  int rc = lmmhip_res_flatten(ctx(), int64_t(list.size()), list.data(), maxmin_precision, cnt);
+  int rc = fair ? lmmhip_res_flatten_fair(ctx(), int64_t(list.size()), list.data(), cnt)
+                : lmmhip_res_flatten(ctx(), int64_t(list.size()), list.data(), maxmin_precision, cnt);
   if (rc)
     fatal(std::string("resident flatten failed: ") + lmmhip_last_error());
   stats_.upload_ms = ms_since(t1);

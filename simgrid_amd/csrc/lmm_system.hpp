@@ -165,8 +165,8 @@ public:
   // The element / variable / constraint records are mirrored in HBM (lmmhip_res_apply); every
   // mutation logs the records it touched, the log is shipped at the next max-min solve, and the
   // solver's CSR/CSC is rebuilt on the device (lmmhip_res_flatten) instead of flatten_maxmin + a full
-  // upload.  Same results bit for bit (tests/test_gpu_resident.py).  FairBottleneck::solve keeps the
-  // host flatten.  Turning it on ships the whole system at the next solve.
+  // upload.  Same results bit for bit (tests/test_gpu_resident.py), for lmm_solve and for
+  // FairBottleneck::solve (flatten_fair's rules).  Turning it on ships the whole system at the next solve.
   void set_resident(bool on);
   bool resident() const { return resident_; }
   // Pending delta-log sizes (elements, variables, constraints; -1 each = full re-ship pending).

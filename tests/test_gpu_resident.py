@@ -117,17 +117,59 @@ def test_resident_synthetic_churn():
             b.update_constraint_bound(L.Constraint(b, int(c)), bnd)
 
 
-def test_resident_fair_bottleneck_keeps_host_flatten():
-    """FairBottleneck::solve is not served by the device flatten (max-min only); resident mode must not
-    change its result."""
-    ops = K.random_script(11, n_cnst=20, n_var=50)
+@pytest.mark.parametrize("seed", range(4))
+def test_resident_fair_bottleneck_flatten(seed):
+    """FairBottleneck inputs built on the device (flatten_fair's rules: no bound test, zero-weight FATPIPE
+    flag, CSC chunks) equal the host flatten's bit for bit, over mutation steps.  Flatten only: these
+    systems mix zero weights, zero bounds and FATPIPE, on which the reference's bottleneck_solve need not
+    terminate (tests/test_gpu_parity.py)."""
+    ops = K.random_script(100 + seed, n_cnst=40, n_var=150, zero_w_p=0.1, fatpipe_p=0.2)
+    a, csa, vsa = K.replay(L, ops, kind=1)
+    a.set_resident(True)
+    b, csb, vsb = K.replay(L, ops, kind=1)
+    rng = random.Random(seed)
+    next_var = 5000
+    for step in range(4):
+        a.prepare()
+        b.prepare()
+        _flat_equal(a.device_flat(), b.device_flat())
+        more, next_var = step_ops(rng, csa, vsa, next_var)
+        K.replay(L, more, sys_=a, cs=csa, vs=vsa)
+        K.replay(L, more, sys_=b, cs=csb, vs=vsb)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_resident_fair_bottleneck_steps(seed):
+    """FairBottleneck::solve through the device flatten on terminating systems (no FATPIPE, no zero
+    weight; zero bounds allowed): flattened inputs bit-identical, values within tolerance, steps."""
+    ops = K.random_script(200 + seed, n_cnst=40, n_var=150, zero_w_p=0.0, fatpipe_p=0.0, zero_bound_p=0.05)
+    a, csa, vsa = K.replay(L, ops, kind=1)
+    a.set_resident(True)
+    b, csb, vsb = K.replay(L, ops, kind=1)
+    rng = random.Random(seed)
+    next_var = 5000
+    for step in range(4):
+        _flat_equal(_split_solve(a), _split_solve(b))
+        worst, bad = K.compare_values(vsa, vsb)
+        assert not bad, (step, worst, bad[:5])
+        more, next_var = step_ops(rng, csa, vsa, next_var, unshare_p=0.0)
+        more = [op for op in more if not (op[0] == "expand_add" and op[3] == 0.0)]
+        K.replay(L, more, sys_=a, cs=csa, vs=vsa)
+        K.replay(L, more, sys_=b, cs=csb, vs=vsb)
+
+
+def test_resident_switches_solver_kind():
+    """lmm_solve() on a FairBottleneck system is the max-min solver (maxmin.hpp:447): the device flatten
+    follows the kind of each call."""
+    ops = K.random_script(7, n_cnst=20, n_var=60, zero_w_p=0.0, fatpipe_p=0.0)
     a, _, vsa = K.replay(L, ops, kind=1)
     a.set_resident(True)
     b, _, vsb = K.replay(L, ops, kind=1)
-    a.solve()
-    b.solve()
-    worst, bad = K.compare_values(vsa, vsb)
-    assert not bad, (worst, bad[:5])
+    for call in ("solve", "lmm_solve", "solve"):
+        getattr(a, call)()
+        getattr(b, call)()
+        worst, bad = K.compare_values(vsa, vsb)
+        assert not bad, (call, worst, bad[:5])
 
 
 def test_resident_refresh_path_bounds_and_penalties():

@@ -71,7 +71,7 @@ def assert_same_device_view(a, b):
     np.testing.assert_array_equal(a.v_b, b.v_b)
     np.testing.assert_array_equal(a.c_b, b.c_b)
     np.testing.assert_array_equal(a.c_fl, b.c_fl)
-    for v in np.nonzero(b.v_n)[0]:
+    for v in np.nonzero(b.v_n > 0)[0]:  # the slabs the device reads (-1 = dead)
         assert a.v_eb[v] == b.v_eb[v]
         sl = slice(int(b.v_eb[v]), int(b.v_eb[v] + b.v_n[v]))
         np.testing.assert_array_equal(a.e_cnst[sl], b.e_cnst[sl])
@@ -79,7 +79,7 @@ def assert_same_device_view(a, b):
         np.testing.assert_array_equal(a.e_fl[sl], b.e_fl[sl])
 
 
-def step_ops(rng, cs, vs, next_var, n_new=8, n_free=6, n_pen=6, n_bound=6, max_el=5):
+def step_ops(rng, cs, vs, next_var, n_new=8, n_free=6, n_pen=6, n_bound=6, max_el=5, unshare_p=0.3):
     """One simulation step's worth of mutations on an existing replayed system (op tuples of
     tests/lmm_cases.replay): flows end, flows start, penalties / bounds move."""
     ops = []
@@ -106,7 +106,7 @@ def step_ops(rng, cs, vs, next_var, n_new=8, n_free=6, n_pen=6, n_bound=6, max_e
             ops.append(("vbound", rng.choice(alive), round(rng.uniform(0.05, 3.0), 3)))
         else:
             ops.append(("cbound", rng.choice(ckeys), round(rng.uniform(0.5, 20.0), 3)))
-    if rng.random() < 0.3:
+    if rng.random() < unshare_p:
         ops.append(("unshare", rng.choice(ckeys)))
     return ops, next_var + n_new
 
