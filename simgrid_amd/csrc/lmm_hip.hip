@@ -1076,6 +1076,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat);
   auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
+  // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
+  // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
+  const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 16);
+  const int cmp_pct = env_int("LMMHIP_COMPACT_PCT", 75);
+  const int cl_every = env_int("LMMHIP_CLIST_EVERY", 8);
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
   int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
@@ -1101,7 +1106,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       break;
     if (r > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
-    if (r - last_clist >= 8 && ncl > 4096) {  // alive-constraint list (order not preserved)
+    if (r - last_clist >= cl_every && ncl > 4096) {  // alive-constraint list (order not preserved)
       const int out = cb ^ 1;
       HIPCHK(hipMemsetAsync(d.ctl + CTL_NCL0 + out, 0, sizeof(int32_t), c->stream));
       LAUNCH(6, r, mm_clist, gL, kBlock, d, cb, out, 0);
@@ -1111,7 +1116,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         return rc;
       ncl = c->h_ctl[CTL_NCL0 + cb];
     }
-    if (r - last_compact >= 16 && nrows > 4096) {  // order-preserving compaction of the alive rows
+    if (r - last_compact >= cmp_every && nrows > 4096) {  // order-preserving compaction of the alive rows
       const int out = buf == 1 ? 2 : 1;
       const int nblk = int((nrows + kCompactRows - 1) / kCompactRows);
       LAUNCH(6, r, cmp_count, nblk, kBlock, d, buf);
@@ -1119,7 +1124,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = poll_ctl(c))
         return rc;
       const int64_t alive_rows = c->h_ctl[CTL_NROWS + out];
-      if (alive_rows < nrows * 3 / 4) {  // worth rewriting
+      if (alive_rows * 100 < nrows * cmp_pct) {  // worth rewriting
         LAUNCH(6, r, cmp_write, nblk, kBlock, d, buf, out);
         nrows = alive_rows;
         buf = out;
