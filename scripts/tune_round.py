@@ -19,7 +19,7 @@ from simgrid_amd import lmm as L  # noqa: E402
 
 KNOBS = ("LMMHIP_UPD_BLOCKS", "LMMHIP_READY_BLOCKS", "LMMHIP_SAT_BLOCKS", "LMMHIP_COMPACT_EVERY",
          "LMMHIP_COMPACT_PCT", "LMMHIP_CLIST_EVERY")
-DEFAULT = (0, 0, 0, 16, 75, 8)
+DEFAULT = (0, 0, 0, 32, 75, 8)
 WIDTHS = [(0, 0, 0), (1024, 0, 0), (512, 0, 0), (0, 0, 1024), (0, 0, 512), (0, 1024, 0), (0, 512, 0),
           (1024, 1024, 1024), (512, 512, 512), (0, 0, 256)]
 CADENCE = [(16, 75, 8), (32, 75, 8), (16, 50, 8), (32, 50, 8), (8, 75, 8), (24, 60, 8), (16, 75, 16),

@@ -1078,7 +1078,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
   // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
   // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
-  const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 16);
+  const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 32);
   const int cmp_pct = env_int("LMMHIP_COMPACT_PCT", 75);
   const int cl_every = env_int("LMMHIP_CLIST_EVERY", 8);
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
