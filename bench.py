@@ -344,6 +344,18 @@ def run_config(args):
     else:
         alg = 56 * tot[1] + 24 * tot[0] + 32 * tot[2]
     ach = alg / (ms_per_step * 1e-3) / 1e9
+    if args.profile_json and rank == 0 and shards is None:  # per-launch HIP events of one extra solve
+        s.set_profiling(True)
+        s.device_solve()
+        s.set_profiling(False)
+        slot, rnd, ms = s.launch_profile()
+        per_kernel = {SLOT_NAMES[int(k)]: dict(launches=int((slot == k).sum()), total_ms=float(ms[slot == k].sum()),
+                                               avg_us=float(1000 * ms[slot == k].mean()))
+                      for k in sorted(set(slot.tolist()))}
+        with open(args.profile_json, "w") as f:
+            json.dump(dict(per_kernel=per_kernel, rounds=s.last_stats()["rounds"],
+                           device_ms=s.last_stats()["device_ms"], launch_slot=slot.tolist(),
+                           launch_round=rnd.tolist(), launch_ms=ms.tolist()), f)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = config_cpu_baseline(args.workload, args.flows)

@@ -254,6 +254,19 @@ def solve_batch_block(build, n_systems, weights, exchange, solve=None):
     return mine
 
 
+_FB_STREAMS = {}
+
+
+def _fb_stream():
+    """The process's FairBottleneck shard stream on the current device (created once)."""
+    import torch
+
+    dev = torch.cuda.current_device()
+    if dev not in _FB_STREAMS:
+        _FB_STREAMS[dev] = torch.cuda.Stream(dev)
+    return _FB_STREAMS[dev]
+
+
 class DeviceFbShard:
     """One rank's part of a variable-sharded FairBottleneck solve on the current HIP device: its block
     of variables and every constraint, the three phases of lmmhip_fb_shard_step, and the exchange
@@ -273,13 +286,19 @@ class DeviceFbShard:
             return a.ctypes.data_as(ct.POINTER(t))
 
         nc = len(f.cbound)
-        self._check(L.lmmhip_ctx_set_stream(self.ctx, ct.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        # One torch stream shared by every shard of the process: the context's kernels and the torch-side
+        # reductions / all-reduces of the exchange buffers (fb_solve_sharded runs them on it) are then
+        # stream-ordered.  Torch's default stream has handle 0, which lmmhip_ctx_set_stream would map to
+        # the context's own non-blocking stream -- unordered with the torch work.
+        self.stream = _fb_stream()
+        self._check(L.lmmhip_ctx_set_stream(self.ctx, ct.c_void_p(self.stream.cuda_stream)))
         self._check(L.lmmhip_upload(self.ctx, self.n, nc, len(f.cnst_idx), p(f.var_ptr, ct.c_int64),
                                     p(f.cnst_idx, ct.c_int32), p(f.weight, ct.c_double), p(f.penalty, ct.c_double),
                                     p(f.vbound, ct.c_double), p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8)))
-        self.xnb = torch.zeros(nc + 1, dtype=torch.int32, device="cuda")
-        self.xsum = torch.zeros(nc, dtype=torch.float64, device="cuda")
-        self.xmin = torch.zeros(nc, dtype=torch.float64, device="cuda")
+        with torch.cuda.stream(self.stream):
+            self.xnb = torch.zeros(nc + 1, dtype=torch.int32, device="cuda")
+            self.xsum = torch.zeros(nc, dtype=torch.float64, device="cuda")
+            self.xmin = torch.zeros(nc, dtype=torch.float64, device="cuda")
         self.prec = lmm.get_precision() if precision is None else precision
         self.begin()
 
@@ -347,6 +366,16 @@ def fb_solve_sharded(shards, exchange, n_var_total, n_cnst, poll_every=16):
     rank) with the exchange buffers reduced over the local shards, then over the ranks.  Returns the
     round count.  All ranks stop in the same round: `done` comes from the reduced counts, and the stop
     decision itself is all-reduced."""
+    stream = getattr(shards[0], "stream", None) if shards else None
+    if stream is not None:  # device shards: the exchange-buffer reductions run on the shards' stream
+        import torch
+
+        with torch.cuda.stream(stream):
+            return _fb_rounds(shards, exchange, n_var_total, n_cnst, poll_every)
+    return _fb_rounds(shards, exchange, n_var_total, n_cnst, poll_every)
+
+
+def _fb_rounds(shards, exchange, n_var_total, n_cnst, poll_every):
     max_rounds = 64 * (n_var_total + n_cnst) + 4096
     rounds = 0
     while True:
