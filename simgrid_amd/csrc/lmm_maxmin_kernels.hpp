@@ -41,9 +41,16 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
     const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
     const bool fat = s.cflags[c] & 1;
     double acc = 0.0;
-    for (uint32_t j = b + lane; j < e; j += kWave) {
-      const double u = s.csc_u[j];
-      acc = fat ? fmax(acc, u) : acc + u;
+    // four loads in flight per lane, accumulated in the same order as a one-at-a-time loop (a missing
+    // term adds 0.0 / max's 0.0 to a non-negative acc: bit-identical)
+    for (uint32_t j0 = b + lane; j0 < e; j0 += 4 * kWave) {
+      double u[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        u[k] = j0 + k * kWave < e ? s.csc_u[j0 + k * kWave] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        acc = fat ? fmax(acc, u[k]) : acc + u[k];
     }
     acc = fat ? wave_max(acc) : wave_sum(acc);
     if (lane == 0) {
