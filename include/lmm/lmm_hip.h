@@ -133,9 +133,11 @@ int lmmhip_round_profile(lmmhip_ctx* ctx, int64_t* alive_vars, int64_t* alive_el
  * elements.  Returns the number of rounds. */
 int lmmhip_vote_profile(lmmhip_ctx* ctx, int64_t* reeval_vars, int64_t* reeval_elems, int cap);
 
-/* Launch on `hip_stream` (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream) instead of the
+/* Launch on `hip_stream` (a hipStream_t, e.g. a torch.cuda.Stream's cuda_stream) instead of the
  * context's own stream; null restores the own stream.  Lets a caller order its collectives and the
- * solver's kernels on one stream without host synchronisation. */
+ * solver's kernels on one stream without host synchronisation.  The legacy null stream cannot be
+ * selected: its handle is 0, which means "own stream" here.  So torch's default stream is not a valid
+ * argument.  Use a dedicated stream (simgrid_amd/multi.py _fb_stream). */
 int lmmhip_ctx_set_stream(lmmhip_ctx* ctx, void* hip_stream);
 
 /* FairBottleneck with the variables sharded over ranks (simgrid_amd/multi.py).  The
