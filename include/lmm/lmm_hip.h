@@ -116,6 +116,17 @@ int lmmhip_solve(lmmhip_ctx* ctx, int kind, double precision);
 
 /* Copy the solved values (n_var doubles, CSR variable order) to host memory. */
 int lmmhip_get_values(lmmhip_ctx* ctx, double* values_out);
+/* Saturated set of the last solve, one byte per constraint of the solved system (dense order):
+ *   MAXMIN: sat(c) = NOT double_positive(bound - U_c, bound * precision), U_c = Constraint::get_usage()
+ *           (maxmin.cpp:948-961) from the solved values — the saturated_constraint_set the reference
+ *           leaves behind (maxmin.cpp:397-409), recomputed the way SURVEY.md A.6 compares it;
+ *   FAIR_BOTTLENECK: c was erased (remaining <= 0, fair_bottleneck.cpp:129-140). */
+int lmmhip_get_saturated(lmmhip_ctx* ctx, uint8_t* saturated_out);
+/* Variables the last flatten put in the system — the Lazy models' modified_set_ side effect of the
+ * solve (every variable of an active element of a listed constraint, maxmin.cpp:536-538) — in the
+ * caller's id space: dense CSR indices after lmmhip_upload, host variable slots after
+ * lmmhip_res_flatten (ascending).  *n = count; ids == NULL = size query; cap must be >= *n. */
+int lmmhip_get_touched_vars(lmmhip_ctx* ctx, int32_t* ids, int64_t cap, int64_t* n);
 /* Device pointer of the values (for device-resident consumers, e.g. model update kernels). */
 int lmmhip_values_device_ptr(lmmhip_ctx* ctx, const double** dptr);
 
@@ -134,11 +145,22 @@ int lmmhip_round_profile(lmmhip_ctx* ctx, int64_t* alive_vars, int64_t* alive_el
 int lmmhip_vote_profile(lmmhip_ctx* ctx, int64_t* reeval_vars, int64_t* reeval_elems, int cap);
 
 /* Launch on `hip_stream` (a hipStream_t, e.g. a torch.cuda.Stream's cuda_stream) instead of the
- * context's own stream; null restores the own stream.  Lets a caller order its collectives and the
- * solver's kernels on one stream without host synchronisation.  The legacy null stream cannot be
- * selected: its handle is 0, which means "own stream" here.  So torch's default stream is not a valid
- * argument.  Use a dedicated stream (simgrid_amd/multi.py _fb_stream). */
+ * context's own stream.  Lets a caller order its collectives and the solver's kernels on one stream
+ * without host synchronisation.  Every handle means that stream: 0 is the legacy null stream (torch's
+ * default stream), ordered with the caller's work on it.  lmmhip_ctx_use_own_stream returns to the
+ * context's own non-blocking stream (the state after lmmhip_ctx_create). */
 int lmmhip_ctx_set_stream(lmmhip_ctx* ctx, void* hip_stream);
+int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
+
+/* Max-min engine (the round loop of maxmin.cpp:560-680):
+ *   LMMHIP_ENGINE_PERSISTENT (default) — ONE cooperative launch per solve: the rounds' phases separated
+ *     by grid barriers, termination decided on the device, no host round-trip;
+ *   LMMHIP_ENGINE_ROUNDS — one launch per phase per round, the host polling termination every few
+ *     rounds (also the engine of the profiling mode, which times every phase launch).
+ * Both give bit-identical results.  The environment variable LMMHIP_ENGINE=rounds|persistent overrides. */
+#define LMMHIP_ENGINE_PERSISTENT 0
+#define LMMHIP_ENGINE_ROUNDS 1
+int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
 
 /* FairBottleneck with the variables sharded over ranks (simgrid_amd/multi.py).  The
  * context holds this rank's variables and EVERY constraint (constraint indices are global).  A round

@@ -28,6 +28,9 @@ enum : int {
   CTL_NTOUCH0 = 12,  // maxmin: touched-list lengths, per round parity (2 words)
   CTL_NCL0 = 14,     // maxmin: alive-constraint list lengths (2 buffers)
   CTL_LASTR = 16,    // maxmin: last round that fixed a variable (+1 = rounds)
+  CTL_PALIVE0 = 17,  // persistent maxmin: constraints alive after round r's update, per round parity (2 words)
+  CTL_ERR = 19,      // persistent kernels: 1 = grid-barrier timeout, 2 = round guard
+  CTL_RESEVAL = 20,  // persistent maxmin (profiling): rows re-evaluated by the vote, summed over the solve
   CTL_WORDS = 32
 };
 
@@ -36,14 +39,47 @@ enum : int {
 // at the kernel boundary), and the first three fields are the decrement record: the three pushes of
 // one element, issued by the 4 lanes of a quad in ONE wave instruction, are one memory-side atomic
 // request (scripts/ubench_atomic.hip: 2.9x the rate of three separate arrays).
+//
+// Determinism: the decrements are summed as 64-bit FIXED-POINT integers (w*x scaled by 2^srem, w/p by
+// 2^suse, per-constraint powers of two chosen at init so that a round's sum stays below 2^61, see
+// dec_scale), so the sum is the same whatever order the atomics land in: a solve is bit-reproducible
+// run to run, like the reference's sequential loop (maxmin.cpp:601-606).  Each term is rounded once
+// to 2^-61 of the constraint's bound / initial usage (256x finer than one fp64 ulp of it).
 struct alignas(64) CstRec {
-  double drem, duse, dcnt;  // decrements pushed this round (atomics; dcnt = fixed elements)
+  unsigned long long drem, duse, dcnt;  // fixed-point decrements pushed this round; dcnt = fixed elements
   int64_t pad;
   double rem, use;          // remaining, usage (maxmin.cpp:520-535, 603-658)
   double ratio;             // rem / use; +inf when out of the light table
   double bound;             // constraint bound
 };
 static_assert(sizeof(CstRec) == 64, "CstRec must be one 64-B line");
+
+// Scale exponent of a non-negative magnitude bound m: 2^s * m < 2^61 (headroom 4x below int64).
+__device__ __forceinline__ int dec_scale(double m) {
+  if (!(m > 0) || !(m < __builtin_huge_val()))
+    return 0;
+  int s = 61 - __builtin_amdgcn_frexp_exp(m);  // m < 2^frexp_exp(m)
+  return s < -1000 ? -1000 : (s > 1000 ? 1000 : s);
+}
+// One decrement as a fixed-point integer (the multiply by 2^s is exact; one rounding to integer).
+__device__ __forceinline__ unsigned long long dec_q(double d, int s) {
+  return (unsigned long long)__double2ll_rn(__builtin_amdgcn_ldexp(d, s));
+}
+__device__ __forceinline__ double dec_val(unsigned long long q, int s) {
+  return __builtin_amdgcn_ldexp(double((long long)q), -s);
+}
+// packed per-constraint scale exponents: low 16 bits srem, high 16 bits suse
+__device__ __forceinline__ int cexp_rem(int32_t e) { return int(int16_t(e & 0xFFFF)); }
+__device__ __forceinline__ int cexp_use(int32_t e) { return int(int16_t(uint32_t(e) >> 16)); }
+
+// Relaxed agent-scope load: always a vector (global) load, never the scalar cache — for words other
+// workgroups write inside a persistent launch (MI355X_MICROARCH.md, inter-workgroup visibility).
+template <class T> __device__ __forceinline__ T ld_rlx(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T> __device__ __forceinline__ void st_rlx(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 struct Dev {
   int32_t nV, nC;
@@ -72,6 +108,7 @@ struct Dev {
   double* rem;      // [nC]
   double* use;      // [nC]
   CstRec* cst;      // [nC] maxmin: per-constraint record (one 64-B line, see CstRec)
+  int32_t* cexp;    // [nC] maxmin: fixed-point scale exponents of the decrements (cexp_rem / cexp_use)
   // [nC] maxmin: alive elements whose variable votes for ANOTHER constraint (dense: mm_ready reads it
   // for every alive constraint each round); ready iff 0.  Vote moves add/subtract the moving
   // variable's multiplicity, fixed elements leave through the record's count in mm_update.

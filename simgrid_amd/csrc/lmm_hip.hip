@@ -19,6 +19,7 @@
 #include "lmm_fb_kernels.hpp"
 #include "lmm_step_kernels.hpp"
 #include "lmm_maxmin_kernels.hpp"
+#include "lmm_persist_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
 #include "lmm_scan.hpp"
 
@@ -76,7 +77,15 @@ struct lmmhip_ctx {
   std::vector<float> launch_ms;
   lmmhip_stats stats{};
   int last_kind = LMMHIP_KIND_MAXMIN;
+  double last_prec = 1e-5;  // precision of the last solve (lmmhip_get_saturated)
+  bool solved = false;      // a solve completed since the last upload / flatten
   int32_t* vstat = nullptr;  // profiling counters of mm_vote ([round][block] x 2)
+  // maxmin engine (lmmhip_ctx_set_engine): one persistent launch per solve (default) or the
+  // multi-launch round chain; grid-barrier words of the persistent launch
+  int engine = LMMHIP_ENGINE_PERSISTENT;
+  unsigned* pbar = nullptr;
+  int persist_grid = 0;  // workgroups of the persistent launch (one per CU, checked at first use)
+  bool ev1_done = false;  // the solve recorded ev1 itself (right behind its last kernel)
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
   int64_t fb_round = 0;
   double fb_prec = 0;
@@ -110,6 +119,7 @@ struct lmmhip_ctx {
   int32_t* res_dirty = nullptr;
   int64_t res_refreshes = 0;
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
+  Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
@@ -195,7 +205,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch})
@@ -216,6 +226,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipHostFree(c->h_ctl);
   if (c->vstat)
     (void)hipFree(c->vstat);
+  if (c->pbar)
+    (void)hipFree(c->pbar);
   if (c->ev0)
     (void)hipEventDestroy(c->ev0);
   if (c->ev1)
@@ -260,6 +272,7 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   rc |= dalloc(c, &d.rem, nC);
   rc |= dalloc(c, &d.use, nC);
   rc |= dalloc(c, &d.cst, nC);
+  rc |= dalloc(c, &d.cexp, nC);
   rc |= dalloc(c, &d.nvote, nC);
   rc |= dalloc(c, &cvar0, nV);
   rc |= dalloc(c, &cvar1, nV);
@@ -371,6 +384,7 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
     HIPCHK(hipStreamSynchronize(c->stream));
   }
   c->uploaded = true;
+  c->solved = false;
   c->stats = lmmhip_stats{};
   c->stats.n_var = nV;
   c->stats.n_cnst = nC;
@@ -935,7 +949,9 @@ int lmmhip_set_profiling(lmmhip_ctx* c, int on) {
 }
 
 static int solve_maxmin(lmmhip_ctx* c, double prec);
+static int solve_maxmin_persist(lmmhip_ctx* c, double prec);
 static int solve_fair(lmmhip_ctx* c, double prec);
+static int engine_of(const lmmhip_ctx* c);
 static int resolve_profile(lmmhip_ctx* c);
 
 int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
@@ -963,14 +979,21 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
     HIPCHK(hipMemsetAsync(c->vstat, 0, stat_bytes, c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   c->last_kind = kind;
-  int rc = kind == LMMHIP_KIND_MAXMIN ? solve_maxmin(c, precision) : solve_fair(c, precision);
+  c->last_prec = precision;
+  c->solved = false;
+  c->ev1_done = false;
+  int rc = kind == LMMHIP_KIND_FAIR_BOTTLENECK ? solve_fair(c, precision)
+           : engine_of(c) == LMMHIP_ENGINE_PERSISTENT ? solve_maxmin_persist(c, precision)
+                                                     : solve_maxmin(c, precision);
   if (rc)
     return rc;
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  HIPCHK(hipEventSynchronize(c->ev1));
+  if (!c->ev1_done)
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->stats.device_ms = ms;
+  c->solved = true;
   c->stats.rounds = c->h_ctl[CTL_ROUNDS];
   if (kind == LMMHIP_KIND_MAXMIN && c->stats.rounds > 0)  // launched rounds include empty tail rounds
     c->stats.rounds = c->h_ctl[CTL_LASTR] + 1;
@@ -1137,6 +1160,52 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   return 0;
 }
 
+static int engine_of(const lmmhip_ctx* c) {
+  // the profiling mode times every phase launch: it runs the multi-launch engine
+  if (c->profiling)
+    return LMMHIP_ENGINE_ROUNDS;
+  const char* e = std::getenv("LMMHIP_ENGINE");
+  if (e && *e)
+    return std::strcmp(e, "rounds") == 0 ? LMMHIP_ENGINE_ROUNDS : LMMHIP_ENGINE_PERSISTENT;
+  return c->engine;
+}
+
+// One cooperative launch per solve (lmm_persist_kernels.hpp): one 1024-thread workgroup per CU, all
+// resident (hipLaunchCooperativeKernel checks the grid against the occupancy query); every barrier
+// wait is bounded, so a fault in the protocol ends the launch with CTL_ERR instead of hanging the GPU.
+static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
+  Dev d = c->d;
+  d.vstat = nullptr;
+  const bool bits = int64_t(d.nC) <= int64_t(kPBitWords) * 64;
+  const void* kern = bits ? reinterpret_cast<const void*>(&mm_persist<true>)
+                          : reinterpret_cast<const void*>(&mm_persist<false>);
+  if (!c->pbar)
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->pbar), BAR_WORDS * sizeof(unsigned)));
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPB, 0));
+  if (per_cu < 1)
+    return fail(LMMHIP_E_HIP, "persistent maxmin kernel: not one workgroup per CU (occupancy query)");
+  const int grid = c->n_cu;
+  c->persist_grid = grid;
+  HIPCHK(hipMemsetAsync(c->pbar, 0, BAR_WORDS * sizeof(unsigned), c->stream));
+  HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
+  const int max_rounds = int(std::min<int64_t>(int64_t(d.nV) + 2, INT32_MAX - 1));
+  const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 16);
+  unsigned* barw = c->pbar;
+  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every)};
+  HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
+  c->stats.kernel_launches[2] += 1;
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->ev1_done = true;
+  if (int rc = poll_ctl(c))
+    return rc;
+  if (c->h_ctl[CTL_ERR] == 1)
+    return fail(LMMHIP_E_HIP, "persistent maxmin kernel: a grid-barrier wait timed out");
+  if (c->h_ctl[CTL_ERR] == 2)
+    return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
+  return 0;
+}
+
 static int fb_begin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
   c->fb_round = 0;
@@ -1208,7 +1277,25 @@ int lmmhip_ctx_set_stream(lmmhip_ctx* c, void* stream) {
     return fail(LMMHIP_E_ARG, "null context");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  c->stream = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+  c->stream = static_cast<hipStream_t>(stream);  // 0 = the legacy null stream, like any other handle
+  return 0;
+}
+
+int lmmhip_ctx_use_own_stream(lmmhip_ctx* c) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->stream = c->own_stream;
+  return 0;
+}
+
+int lmmhip_ctx_set_engine(lmmhip_ctx* c, int engine) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (engine != LMMHIP_ENGINE_PERSISTENT && engine != LMMHIP_ENGINE_ROUNDS)
+    return fail(LMMHIP_E_ARG, "unknown maxmin engine");
+  c->engine = engine;
   return 0;
 }
 
@@ -1614,6 +1701,55 @@ int lmmhip_get_values(lmmhip_ctx* c, double* out) {
   HIPCHK(hipSetDevice(c->device));
   if (c->d.nV)
     HIPCHK(hipMemcpyAsync(out, c->d.x, sizeof(double) * c->d.nV, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_get_saturated(lmmhip_ctx* c, uint8_t* sat) {
+  if (!c || !c->uploaded || !c->solved)
+    return fail(LMMHIP_E_STATE, "no solved system");
+  if (!sat && c->d.nC)
+    return fail(LMMHIP_E_ARG, "null output");
+  HIPCHK(hipSetDevice(c->device));
+  if (c->d.nC) {
+    uint8_t* o = nullptr;
+    if (int rc = scratch(c, c->sat_out, c->d.nC, &o))
+      return rc;
+    hipLaunchKernelGGL(mm_saturated, dim3(grid_for(c->d.nC, kBlock / kWave)), dim3(kBlock), 0, c->stream, c->d,
+                       c->last_prec, int(c->last_kind == LMMHIP_KIND_FAIR_BOTTLENECK), o);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(sat, o, size_t(c->d.nC), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_get_touched_vars(lmmhip_ctx* c, int32_t* ids, int64_t cap, int64_t* n) {
+  if (!c || !c->uploaded || !n)
+    return fail(LMMHIP_E_STATE, "no system uploaded / null count");
+  const int64_t nv = c->d.nV;
+  *n = nv;
+  if (!ids)
+    return 0;  // size query
+  if (cap < nv)
+    return fail(LMMHIP_E_ARG, "touched vars: output capacity below the system's variable count");
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->res_flat) {  // lmmhip_upload: the caller's ids are the dense CSR indices
+    for (int64_t v = 0; v < nv; v++)
+      ids[v] = int32_t(v);
+    return 0;
+  }
+  int32_t* o = nullptr;
+  if (int rc = scratch(c, c->tv_out, nv, &o))
+    return rc;
+  const int64_t ns = c->res_flat_nv;
+  if (ns) {
+    hipLaunchKernelGGL(rs_touched, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, c->stream, ns,
+                       static_cast<const int64_t*>(c->rs_vm.p), static_cast<const int64_t*>(c->rs_dv.p), o);
+    HIPCHK(hipGetLastError());
+  }
+  if (nv)
+    HIPCHK(hipMemcpyAsync(ids, o, size_t(nv) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }

@@ -33,11 +33,11 @@ __global__ void __launch_bounds__(kBlock) mm_elem_usage(Dev s) {
 
 // Init, one wave per constraint: maxmin.cpp:520-555.  remaining = bound; skipped when
 // bound <= bound*prec; usage = sum (SHARED) or max (FATPIPE) of w/p over the active elements.
-__global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
+// Waves `wave`, `wave + nwaves`, ... of the grid; returns (on lane 0) the constraints made alive.
+__device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64_t wave, int64_t nwaves) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int wpb = kBlock / kWave;
   int alive_cnt = 0;
-  for (int64_t c = int64_t(blockIdx.x) * wpb + threadIdx.x / kWave; c < s.nC; c += int64_t(gridDim.x) * wpb) {
+  for (int64_t c = wave; c < s.nC; c += nwaves) {
     const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
     const bool fat = s.cflags[c] & 1;
     double acc = 0.0;
@@ -60,13 +60,16 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
       const bool alive = part && usage > 0;
       const double r = bound / usage;
       CstRec rec;
-      rec.drem = rec.duse = rec.dcnt = 0.0;
+      rec.drem = rec.duse = rec.dcnt = 0;
       rec.pad = 0;
       rec.rem = bound;
       rec.use = usage;
       rec.ratio = alive ? r : dinf();
       rec.bound = bound;
       s.cst[c] = rec;
+      // fixed-point scales of this solve's decrements (CstRec): a round never removes more than the
+      // remaining (<= bound) or the usage (<= initial usage) from a constraint
+      s.cexp[c] = alive ? int32_t((uint32_t(uint16_t(dec_scale(usage))) << 16) | uint16_t(dec_scale(bound))) : 0;
       s.touched[c] = 0;
       s.nvote[c] = int32_t(e - b);  // no element votes yet
       s.chg[c] = uint16_t(0xFFFF);
@@ -74,35 +77,46 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
       alive_cnt += alive;
     }
   }
-  if (lane == 0 && alive_cnt)
+  return alive_cnt;
+}
+
+__global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int alive_cnt = init_cnsts_waves(s, prec, wave, int64_t(gridDim.x) * (kBlock / kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0 && alive_cnt)
     atomicAdd(&s.ctl[CTL_ALIVE_C], alive_cnt);
 }
 
-__global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
+__device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t nthreads) {
+  for (int64_t v = t; v < s.nV; v += nthreads) {
     s.x[v] = 0.0;
     s.vstate[v] = 0;
     s.rtgt[0][v] = kUnvoted;
   }
+}
+
+__global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
+  init_vars_range(s, int64_t(blockIdx.x) * kBlock + threadIdx.x, int64_t(gridDim.x) * kBlock);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_NROWS + 0] = s.nV;
     s.ctl[CTL_NELEM + 0] = int32_t(s.nnz);
   }
 }
 
-// Decrements of a fixed variable's element j (maxmin.cpp:601-606) into the constraint's record;
-// FATPIPE constraints only count.  One lane issues all three (rare paths).
+// Decrements of a fixed variable's element j (maxmin.cpp:601-606) into the constraint's record, as
+// fixed-point integers (CstRec); FATPIPE constraints only count.  One lane issues all three (rare paths).
 __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double xv, double p) {
   const int32_t c = s.csr_c[j];
   if (s.key[c] == kDeadKey)
     return;
-  double* r = &s.cst[c].drem;
+  unsigned long long* r = &s.cst[c].drem;
   s.touched[c] = 1;
-  unsafeAtomicAdd(&r[2], 1.0);
+  atomicAdd(&r[2], 1ull);
   if (!(s.cflags[c] & 1)) {
     const double w = s.csr_w[j];
-    unsafeAtomicAdd(&r[0], w * xv);
-    unsafeAtomicAdd(&r[1], w / p);
+    const int32_t ce = s.cexp[c];
+    atomicAdd(&r[0], dec_q(w * xv, cexp_rem(ce)));
+    atomicAdd(&r[1], dec_q(w / p, cexp_use(ce)));
   }
 }
 
@@ -210,8 +224,8 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
           sk = min(sk, (unsigned)key[c]);
       }
       sk = grp_umin<G>(sk);
-      if (live && !bounded && g == 0)
-        s.skey[buf][row] = vb > 0 ? 0 : uint16_t(sk);
+      if (live && !bounded && g == 0)  // 0 = "sensitive" row (bounded, or key-level tie: see vote_row)
+        s.skey[buf][row] = (vb > 0 || sk == mk) ? 0 : uint16_t(sk);
       int mult_new = h0 && c0 == newt, mult_old = h0 && c0 == t;
       for (uint32_t j = j0 + G; j < e; j += G) {
         const int32_t c = ccol[j];
@@ -369,7 +383,11 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     if (c != newt)
       sk = min(sk, (unsigned)key[c]);
   }
-  skey[row] = vb > 0 ? 0 : uint16_t(sk);
+  // skey = the row's floor: the min key over its OTHER constraints (keys never decrease, so while the
+  // target's key stays below it the vote stands even if the target's ratio moved).  0 marks a
+  // "sensitive" row whose vote depends on the target's exact ratio — a bounded variable (the bound test
+  // reads it) or a key-level tie broken by exact ratios — re-evaluated whenever the target is touched.
+  skey[row] = (vb > 0 || sk == mk) ? 0 : uint16_t(sk);
   if (newt == t)
     return;
   int mult_new = 0;
@@ -432,15 +450,17 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
       else
         ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
     }
-    unsigned kt[kFilt], sk[kFilt];  // target key and the row's other-key floor, gathered together
+    // With the bitmap, a set bit means the target's KEY changed (or it died) last round; a sensitive
+    // row (skey 0: bounded variable or key-level tie) also re-votes when its target was merely touched
+    // (chg stamp).  Without it, chg marks every touched target.
+    unsigned kt[kFilt], sk[kFilt], cg[kFilt];
 #pragma unroll
-    for (int u = 0; u < kFilt; u++) {
-      kt[u] = 0;
-      sk[u] = 0;
-      if (ch[u]) {
-        kt[u] = key[tt[u]];
-        sk[u] = skey[base + u * B + threadIdx.x];
-      }
+    for (int u = 0; u < kFilt; u++)
+      sk[u] = (kBits ? tt[u] >= 0 : ch[u]) ? skey[base + u * B + threadIdx.x] : 1u;
+#pragma unroll
+    for (int u = 0; u < kFilt; u++) {  // target key (changed targets) / stamp (sensitive rows), together
+      kt[u] = ch[u] ? key[tt[u]] : 0u;
+      cg[u] = (kBits && !ch[u] && tt[u] >= 0 && sk[u] == 0) ? unsigned(s.chg[tt[u]]) : 0x10000u;
     }
 #pragma unroll
     for (int u = 0; u < kFilt; u++) {
@@ -448,6 +468,8 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
       bool need = tt[u] == kUnvoted;
       if (ch[u])  // target changed last round: does the vote still stand?
         need = !(kt[u] < sk[u]);
+      else if (kBits && cg[u] == prev)
+        need = true;
       const unsigned long long m = __ballot(need);  // one LDS atomic per wave
       const int lane = threadIdx.x & (kWave - 1);
       const int leader = m ? __ffsll((long long)m) - 1 : 0;
@@ -567,21 +589,22 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       kk[u] = uint32_t(__shfl(int(rb), o, kWave)) + uint32_t(f - pre[o]);
       cc[u] = f < total ? s.csr_c[kk[u]] : -1;
     }
-    double a0[kSatU], a1[kSatU];
+    long long a0[kSatU], a1[kSatU];  // fixed-point decrements (CstRec)
     bool fat[kSatU];
 #pragma unroll
     for (int u = 0; u < kSatU; u++) {
       const double ox = __shfl(lx, ol[u], kWave);
       const double op = __shfl(lp, ol[u], kWave);
       fat[u] = false;
-      a0[u] = a1[u] = 0.0;
+      a0[u] = a1[u] = 0;
       if (cc[u] >= 0 && (cc[u] == c || s.key[cc[u]] == kDeadKey))
         cc[u] = -1;
       if (cc[u] >= 0) {
         fat[u] = s.cflags[cc[u]] & 1;
         const double w = s.csr_w[kk[u]];
-        a0[u] = w * ox;
-        a1[u] = w / op;
+        const int32_t ce = s.cexp[cc[u]];
+        a0[u] = (long long)dec_q(w * ox, cexp_rem(ce));
+        a1[u] = (long long)dec_q(w / op, cexp_use(ce));
       }
     }
 #pragma unroll
@@ -594,10 +617,10 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
         const int e = t * 16 + (lane >> 2);
         const int ec = __shfl(cc[u], e, kWave);
         const int ef = __shfl(int(fat[u]), e, kWave);
-        const double e0 = __shfl(a0[u], e, kWave);
-        const double e1 = __shfl(a1[u], e, kWave);
+        const long long e0 = __shfl(a0[u], e, kWave);
+        const long long e1 = __shfl(a1[u], e, kWave);
         if (ec >= 0 && q < 3 && (!ef || q == 2))
-          unsafeAtomicAdd(&s.cst[ec].drem + q, q == 0 ? e0 : q == 1 ? e1 : 1.0);
+          atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
         if (ec >= 0 && q == 3)
           s.touched[ec] = 1;  // plain byte store: mm_update reads 1 B per constraint, not the record
       }
@@ -608,7 +631,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
 
 template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int k, int round, int lane,
                                                               int* pre) {
-  const double r = s.cst[c].ratio;
+  const double r = ld_rlx(&s.cst[c].ratio);  // wave-uniform address: keep it off the scalar cache
   const uint32_t ce = s.cnst_ptr[c + 1];
   for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
     saturate_chunk(s, c, r, base, ce, round, lane, pre);
@@ -676,10 +699,92 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
   }
 }
 
-// Round phase 4 — constraint update: maxmin.cpp:603-658.  Thread per constraint in identity order
-// (a wave = 64 consecutive constraints), so the changed-constraint bitmap the next vote reads is one
-// ballot per wave.  balive[block] = constraints of the block's range still in the light table (read
-// by mm_done; plain stores, no global atomic).
+// Round phase 4 — constraint update: maxmin.cpp:603-658, one wave = 64 consecutive constraints (identity
+// order), so the changed-constraint bitmap the next vote reads is one ballot per wave.  A bit is set when
+// the constraint's 16-bit KEY changed or it left the light table (the only events that can move a
+// non-sensitive vote, vote_row); chg[c] = round marks every touched constraint (sensitive rows).
+// FATPIPE usage is recomputed wave-cooperatively: max w/p over the elements whose variable is still at
+// 0 (maxmin.cpp:625-658), 64 elements per step.  Returns (per lane) alive constraints; *touch = some
+// constraint of the wave was touched.
+__device__ __forceinline__ int update_wave(const Dev& s, int64_t base, int round, double prec, bool* touch) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t c = base + lane;
+  bool changed = false, live = false, tch = false, fat = false;
+  unsigned okey = kDeadKey;
+  if (c < s.nC) {
+    okey = s.key[c];
+    if (okey == kDeadKey) {
+      changed = s.chg[c] == uint16_t(round);  // saturated by mm_saturate this round
+    } else {
+      live = true;
+      tch = s.touched[c];
+      fat = tch && (s.cflags[c] & 1);
+    }
+  }
+  double fuse = 0.0;
+  unsigned long long fm = __ballot(fat);
+  while (fm) {  // wave-uniform
+    const int l = __ffsll((long long)fm) - 1;
+    fm &= fm - 1;
+    const int64_t cl = base + l;
+    const uint32_t b = s.cnst_ptr[cl], e = s.cnst_ptr[cl + 1];
+    double m = 0.0;
+    for (uint32_t j = b + lane; j < e; j += kWave)
+      if (!(s.x[s.csc_v[j]] > 0))
+        m = fmax(m, s.csc_u[j]);
+    m = wave_max(m);
+    if (lane == l)
+      fuse = m;
+  }
+  int alive = 0;
+  if (live) {
+    if (!tch) {  // untouched: ratio unchanged
+      alive = 1;
+    } else {
+      *touch = true;
+      s.touched[c] = 0;
+      CstRec* rec = s.cst + c;
+      const unsigned long long qx = rec->drem, qy = rec->duse, qz = rec->dcnt;
+      rec->drem = rec->duse = rec->dcnt = 0;
+      s.nvote[c] -= int(qz);  // fixed elements leave (voters of c were compensated)
+      s.chg[c] = uint16_t(round);
+      const double bound = rec->bound;
+      double rem = rec->rem, use;
+      if (!fat) {
+        const int32_t ce = s.cexp[c];
+        use = rec->use - dec_val(qy, cexp_use(ce));
+        rem -= dec_val(qx, cexp_rem(ce));
+        if (rem < bound * prec)
+          rem = 0.0;
+        if (use < prec)
+          use = 0.0;
+      } else {
+        use = fuse;
+      }
+      rec->rem = rem;
+      rec->use = use;
+      if (!(use > prec) || !(rem > bound * prec)) {
+        rec->ratio = dinf();
+        s.key[c] = kDeadKey;
+        changed = true;
+      } else {
+        const double r = rem / use;
+        rec->ratio = r;
+        const unsigned nk = ratio_key(r);
+        s.key[c] = uint16_t(nk);
+        changed = nk != okey;
+        alive = 1;
+      }
+    }
+  }
+  const unsigned long long word = __ballot(changed);
+  if (lane == 0)
+    s.chgbits[base >> 6] = word;
+  return alive;
+}
+
+// balive[block] = constraints of the block's range still in the light table (read by mm_done; plain
+// stores, no global atomic).
 __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
     return;
@@ -689,63 +794,11 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   if (threadIdx.x == 0)
     alive_cnt = 0;
   __syncthreads();
-  const int lane = threadIdx.x & (kWave - 1);
-  int alive = 0, any_touch = 0;
+  int alive = 0;
+  bool any_touch = false;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
-       base += int64_t(gridDim.x) * kBlock) {  // wave-uniform
-    const int64_t c = base + lane;
-    bool changed = false;
-    if (c < s.nC) {
-      if (s.key[c] == kDeadKey) {
-        changed = s.chg[c] == uint16_t(round);  // saturated by mm_saturate this round
-      } else {
-        if (!s.touched[c]) {  // untouched: ratio unchanged
-          alive++;
-        } else {
-          changed = true;
-          any_touch = 1;
-          s.touched[c] = 0;
-          CstRec* rec = s.cst + c;
-          const double dx = rec->drem, dy = rec->duse, dz = rec->dcnt;
-          rec->drem = rec->duse = rec->dcnt = 0.0;
-          s.nvote[c] -= int(dz);  // fixed elements leave (voters of c were compensated)
-          s.chg[c] = uint16_t(round);
-          const double bound = rec->bound;
-          double rem = rec->rem, use;
-          if (!(s.cflags[c] & 1)) {
-            use = rec->use - dy;
-            rem -= dx;
-            if (rem < bound * prec)
-              rem = 0.0;
-            if (use < prec)
-              use = 0.0;
-          } else {  // FATPIPE: usage = max w/p over enabled elements whose variable is still at 0
-            use = 0.0;
-            for (uint32_t j = s.cnst_ptr[c]; j < s.cnst_ptr[c + 1]; j++) {
-              const int32_t v = s.csc_v[j];
-              if (s.x[v] > 0)
-                continue;
-              use = fmax(use, s.csc_u[j]);
-            }
-          }
-          rec->rem = rem;
-          rec->use = use;
-          if (!(use > prec) || !(rem > bound * prec)) {
-            s.cst[c].ratio = dinf();
-            s.key[c] = kDeadKey;
-          } else {
-            const double r = rem / use;
-            s.cst[c].ratio = r;
-            s.key[c] = ratio_key(r);
-            alive++;
-          }
-        }
-      }
-    }
-    const unsigned long long word = __ballot(changed);
-    if (lane == 0)
-      s.chgbits[base >> 6] = word;
-  }
+       base += int64_t(gridDim.x) * kBlock)  // wave-uniform
+    alive += update_wave(s, base, round, prec, &any_touch);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
@@ -753,6 +806,42 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
     s.balive[blockIdx.x] = alive_cnt;
   if (__syncthreads_or(any_touch) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
+}
+
+// Saturated set of the solved system: sat(c) = NOT double_positive(bound - U_c,
+// bound * prec) with U_c = Constraint::get_usage() (maxmin.cpp:948-961: sum, or max for FATPIPE, of
+// w * x over the enabled elements of weight > 0 — exactly the flattened CSC of c).  One wave per
+// constraint.  FairBottleneck: sat(c) = c was erased (fair_bottleneck.cpp:129-140, ratio = +inf).
+__global__ void __launch_bounds__(kBlock) mm_saturated(Dev s, double prec, int fair, uint8_t* out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int64_t c = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; c < s.nC;
+       c += int64_t(gridDim.x) * (kBlock / kWave)) {
+    if (fair) {
+      if (lane == 0)
+        out[c] = s.ratio[c] != 0.0;
+      continue;
+    }
+    const bool fat = s.cflags[c] & 1;
+    double u = 0.0;
+    for (uint32_t j = s.cnst_ptr[c] + lane; j < s.cnst_ptr[c + 1]; j += kWave) {
+      const double t = s.csc_w[j] * s.x[s.csc_v[j]];
+      u = fat ? fmax(u, t) : u + t;
+    }
+    u = fat ? wave_max(u) : wave_sum(u);
+    if (lane == 0) {
+      const double b = s.cbound[c];
+      out[c] = !((b - u) > b * prec);
+    }
+  }
+}
+
+// Variables of the solved system in the caller's id space: dense index d -> host slot (resident
+// flatten: dv = exclusive scan of the membership mask vm), written at out[d] (ascending slots).
+__global__ void __launch_bounds__(kBlock) rs_touched(int64_t nslots, const int64_t* vm, const int64_t* dv,
+                                                     int32_t* out) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nslots; v += int64_t(gridDim.x) * kBlock)
+    if (vm[v])
+      out[dv[v]] = int32_t(v);
 }
 
 // Termination (maxmin.cpp:680): no constraint left in the light table after the last update.

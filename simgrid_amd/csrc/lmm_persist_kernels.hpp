@@ -1,0 +1,366 @@
+// lmm_persist_kernels.hpp — System::lmm_solve as ONE persistent launch per solve (gfx950).
+//
+// The round loop of maxmin.cpp:560-680 (local-minimum progressive filling, lmm_maxmin_kernels.hpp) with
+// every round's phases inside one cooperative launch, separated by XCD-hierarchical grid barriers, and
+// the termination test (maxmin.cpp:680: the light table is empty) decided on the device — no host
+// round-trips, no per-round launches.  One 1024-thread workgroup per CU (16 waves), so the vote phase
+// can hold the changed-constraint bitmap (up to 2^20 constraints) in LDS.
+//
+//   init            mm_init_cnsts / mm_init_vars bodies (maxmin.cpp:509-555)
+//   round r:  V     filter + re-vote of the rows whose target's key changed (vote_row)
+//             |     grid barrier
+//             S     ready test (nvote == 0) fused with saturation: the wave that finds a ready
+//             |     constraint saturates it (saturate_one), maxmin.cpp:578-606
+//             |     grid barrier
+//             U     constraint update (update_wave), maxmin.cpp:603-658; alive count
+//             |     grid barrier; alive == 0 -> done (every block reads the same count)
+//             [C]   every cmp_every rounds: compaction of the alive rows (one pass, one barrier)
+//
+// Results are bit-identical to the multi-launch engine (same phase bodies, integer / fixed-point
+// atomics only): tests/test_gpu_engines.py.
+#pragma once
+#include "lmm_maxmin_kernels.hpp"
+
+namespace lmmdev {
+
+constexpr int kPB = 1024;            // threads per workgroup (one workgroup per CU)
+constexpr int kPW = kPB / kWave;     // waves per workgroup
+constexpr int kPBitWords = 16384;    // LDS bitmap: 2^20 constraints (128 KB)
+constexpr int kPFilt = 4;            // rows per thread per filter step
+constexpr long long kSpinTicks = 400000000;  // 4 s of the 100 MHz wall clock: a barrier wait gives up
+
+// Grid-barrier words (zeroed by the host before every launch), each counter on its own 64-B line.
+enum : int {
+  BAR_XCNT = 0,     // [8 x 16] arrivals per XCC (monotonic: gen * blocks-on-the-XCC)
+  BAR_TOP = 128,    // arrivals of the XCC leaders (monotonic: gen * XCCs)
+  BAR_GEN = 144,    // chip generation (released by the last leader)
+  BAR_XGEN = 160,   // [8 x 16] per-XCC generation (released by the XCC's leader)
+  BAR_XSIZE = 288,  // [8 x 16] workgroups on each XCC (counted at launch)
+  BAR_FLAT = 416,   // launch rendezvous
+  BAR_ALLOC = 432,  // u64 (2 words, 8-B aligned): compaction allocator (rows << 32 | elements)
+  BAR_WORDS = 448
+};
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v & 7u;
+}
+
+// Relaxed poll of one word until it reaches `target`; gives up (error word 1) after kSpinTicks.
+__device__ __forceinline__ bool spin_geq(unsigned* w, unsigned target, int32_t* err) {
+  const long long t0 = wall_clock64();
+  while (ld_rlx(w) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > kSpinTicks) {
+      st_rlx(err, 1);
+      return false;
+    }
+  }
+  return true;
+}
+
+struct PBar {
+  unsigned* w;
+  int32_t* err;
+  unsigned xcc, xsize, nx;  // meaningful in thread 0 only
+};
+
+// Launch rendezvous: count the workgroups per XCC (for the hierarchical barrier) and wait for all.
+__device__ bool bar_init(PBar& b) {
+  __shared__ int ok_sh;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    b.xcc = xcc_id();
+    __hip_atomic_fetch_add(&b.w[BAR_XSIZE + 16 * b.xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(&b.w[BAR_FLAT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ok = spin_geq(&b.w[BAR_FLAT], gridDim.x, b.err);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    b.xsize = ld_rlx(&b.w[BAR_XSIZE + 16 * b.xcc]);
+    b.nx = 0;
+    for (int i = 0; i < 8; i++)
+      b.nx += ld_rlx(&b.w[BAR_XSIZE + 16 * i]) != 0;
+    ok_sh = ok;
+  }
+  __syncthreads();
+  return ok_sh;
+}
+
+// Grid barrier number `gen` (1, 2, ...): every wave drains its stores to L2; the last workgroup of
+// each XCC writes that XCC's L2 back (agent release) and arrives at the chip counter; the last XCC
+// leader releases the generation; every workgroup acquires (MI355X_MICROARCH.md, barrier-xcd and
+// the valid producer / consumer forms).  Returns false when a wait timed out (the kernel then ends).
+__device__ bool grid_sync(const PBar& b, unsigned gen) {
+  __shared__ int ok_sh;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    const unsigned a =
+        __hip_atomic_fetch_add(&b.w[BAR_XCNT + 16 * b.xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a == gen * b.xsize - 1) {  // XCC leader
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(&b.w[BAR_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == gen * b.nx - 1)
+        st_rlx(&b.w[BAR_GEN], gen);
+      else
+        ok = spin_geq(&b.w[BAR_GEN], gen, b.err);
+      if (ok)
+        st_rlx(&b.w[BAR_XGEN + 16 * b.xcc], gen);
+    } else {
+      ok = spin_geq(&b.w[BAR_XGEN + 16 * b.xcc], gen, b.err);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ok_sh = ok;
+  }
+  __syncthreads();
+  return ok_sh;
+}
+
+template <bool kBits> struct PVoteLds {
+  uint64_t bits[kBits ? kPBitWords : 2];
+  int q[kPB * (kPFilt + 1)];  // queued rows (global row ids)
+  int qn, nq, st0, st1;
+};
+template <bool kBits> union PLds {
+  PVoteLds<kBits> v;
+  int pre[kPW][kWave];  // saturate_chunk's per-wave row-length prefix
+  int cnt;              // update: alive constraints of the workgroup
+};
+
+// V: the rows of buffer `buf` in tiles of kPB * kPFilt (tile t -> workgroup t mod grid).  A row re-votes
+// when it never voted, when its target's key changed or the target died last round (bitmap bit), unless
+// the target is still strictly below the row's other keys (skey), or — sensitive rows (skey 0) — when
+// its target was touched last round (chg stamp).  Queued rows are resolved kPB at a time (vote_row).
+template <bool kBits>
+__device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds<kBits>& L) {
+  if (kBits) {
+    const int n16 = (s.nC + 127) / 128;
+    const uint4* src = reinterpret_cast<const uint4*>(s.chgbits);
+    uint4* dst = reinterpret_cast<uint4*>(L.bits);
+    for (int i = threadIdx.x; i < n16; i += kPB)
+      dst[i] = src[i];
+  }
+  if (threadIdx.x == 0)
+    L.qn = L.nq = 0;
+  __syncthreads();
+  const int32_t* rtgt = s.rtgt[buf];
+  const uint16_t* skey = s.skey[buf];
+  const uint16_t prev = uint16_t(round - 1);
+  const int lane = threadIdx.x & (kWave - 1);
+  constexpr int64_t kStep = int64_t(kPB) * kPFilt;
+  for (int64_t base = int64_t(blockIdx.x) * kStep; base < nrows; base += int64_t(gridDim.x) * kStep) {
+    int tt[kPFilt];
+#pragma unroll
+    for (int u = 0; u < kPFilt; u++) {
+      const int64_t row = base + u * kPB + threadIdx.x;
+      tt[u] = row < nrows ? rtgt[row] : kRetired;
+    }
+    bool ch[kPFilt];
+    unsigned sk[kPFilt], kt[kPFilt], cg[kPFilt];
+#pragma unroll
+    for (int u = 0; u < kPFilt; u++) {
+      if (kBits)
+        ch[u] = tt[u] >= 0 && ((L.bits[tt[u] >> 6] >> (tt[u] & 63)) & 1);
+      else
+        ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
+      sk[u] = (kBits ? tt[u] >= 0 : ch[u]) ? skey[base + u * kPB + threadIdx.x] : 1u;
+    }
+#pragma unroll
+    for (int u = 0; u < kPFilt; u++) {
+      kt[u] = ch[u] ? s.key[tt[u]] : 0u;
+      cg[u] = (kBits && !ch[u] && tt[u] >= 0 && sk[u] == 0) ? unsigned(s.chg[tt[u]]) : 0x10000u;
+    }
+#pragma unroll
+    for (int u = 0; u < kPFilt; u++) {
+      const int64_t row = base + u * kPB + threadIdx.x;
+      bool need = tt[u] == kUnvoted;
+      if (ch[u])
+        need = !(kt[u] < sk[u]);
+      else if (kBits && cg[u] == prev)
+        need = true;
+      const unsigned long long m = __ballot(need);  // one LDS atomic per wave
+      const int leader = m ? __ffsll((long long)m) - 1 : 0;
+      int at = 0;
+      if (m && lane == leader)
+        at = atomicAdd(&L.qn, __popcll(m));
+      at = __shfl(at, leader, kWave);
+      if (need)
+        L.q[at + __popcll(m & ((1ull << lane) - 1))] = int(row);
+    }
+    __syncthreads();
+    int n = L.qn;
+    while (n >= kPB) {  // resolve full queues: the last kPB entries each time
+      vote_row(s, buf, round, L.q[n - kPB + threadIdx.x], &L.st0, &L.st1);
+      n -= kPB;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      L.nq += L.qn - n;
+      L.qn = n;
+    }
+    __syncthreads();
+  }
+  const int n = L.qn;
+  if (threadIdx.x < n)
+    vote_row(s, buf, round, L.q[threadIdx.x], &L.st0, &L.st1);
+  if (threadIdx.x == 0 && L.nq + n)
+    atomicAdd(&s.ctl[CTL_RESEVAL], L.nq + n);
+}
+
+// S: identity-order scan of the constraints, 64 per wave step; a ready constraint (every alive element
+// votes for it, nvote == 0) is saturated by the wave that found it.  Ready constraints share no alive
+// variable (each alive variable votes for exactly one constraint), so the claims never race across waves.
+__device__ bool p_saturate(const Dev& s, int round, int* pre) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kPW;
+  bool any = false;
+  for (int64_t base = wave * kWave; base < s.nC; base += nwaves * kWave) {  // wave-uniform
+    const int64_t c = base + lane;
+    const bool rdy = c < s.nC && s.key[c] != kDeadKey && s.nvote[c] == 0;
+    unsigned long long m = __ballot(rdy);
+    any |= m != 0;
+    while (m) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      saturate_one<1>(s, int32_t(base + l), 0, round, lane, pre);
+    }
+  }
+  return any;
+}
+
+// C: order-free compaction of the alive rows of buffer `in` into `out`: per wave ONE 64-bit atomic
+// allocates its rows AND their elements (rows << 32 | elements), so consecutive allocations stay
+// consistent in both (row k's end = row k+1's start).  Row order does not matter: every vote, claim
+// and fixed-point sum is order-independent.
+__device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned long long* alloc) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kPW;
+  int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
+  uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
+  int32_t* ocol = const_cast<int32_t*>(s.ccol[out]);
+  for (int64_t base = wave * kWave; base < nrows; base += nwaves * kWave) {  // wave-uniform
+    const int64_t row = base + lane;
+    int32_t v = -1;
+    uint32_t b = 0, e = 0;
+    if (row < nrows) {
+      v = s.cvar[in][row];
+      if (s.vstate[v] == 0) {
+        b = s.crow[in][row];
+        e = s.crow[in][row + 1];
+      } else {
+        v = -1;
+      }
+    }
+    const int len = int(e - b);
+    int incl = len;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int t = __shfl_up(incl, o, kWave);
+      if (lane >= o)
+        incl += t;
+    }
+    const unsigned total = unsigned(__shfl(incl, kWave - 1, kWave));
+    const unsigned long long m = __ballot(v >= 0);
+    if (!m)
+      continue;
+    const unsigned k = unsigned(__popcll(m));
+    unsigned long long old = 0;
+    if (lane == 0)
+      old = atomicAdd(alloc, (static_cast<unsigned long long>(k) << 32) | total);
+    old = __shfl(old, 0, kWave);
+    const uint32_t r0 = uint32_t(old >> 32), e0 = uint32_t(old);
+    if (v >= 0) {
+      const uint32_t o = r0 + uint32_t(__popcll(m & ((1ull << lane) - 1)));
+      const uint32_t dst = e0 + uint32_t(incl - len);
+      ovar[o] = v;
+      s.rtgt[out][o] = s.rtgt[in][row];
+      s.skey[out][o] = s.skey[in][row];
+      orow[o] = dst;
+      for (uint32_t j = 0; j < uint32_t(len); j++)
+        ocol[dst + j] = s.ccol[in][b + j];
+    }
+    if (lane == 63 - __clzll(m))  // the wave's last row also writes the end of its elements
+      orow[r0 + k] = e0 + total;
+  }
+}
+
+template <bool kBits>
+__global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double prec, int max_rounds,
+                                                  int cmp_every) {
+  __shared__ PLds<kBits> L;
+  PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0};
+  unsigned long long* alloc = reinterpret_cast<unsigned long long*>(barw + BAR_ALLOC);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  // init (maxmin.cpp:509-555) overlapped with the rendezvous
+  init_cnsts_waves(s, prec, (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave, int64_t(gridDim.x) * kPW);
+  init_vars_range(s, int64_t(blockIdx.x) * kPB + threadIdx.x, int64_t(gridDim.x) * kPB);
+  if (!bar_init(b))
+    return;
+  unsigned gen = 0;
+  int buf = 0;
+  int64_t nrows = s.nV;
+  for (int r = 0;; r++) {
+    p_vote<kBits>(s, buf, r, nrows, L.v);
+    if (!grid_sync(b, ++gen))
+      return;
+    if (lead) {  // words first used later in this round, last read before the previous barrier
+      st_rlx(&s.ctl[CTL_PALIVE0 + ((r + 1) & 1)], 0);
+      st_rlx(alloc, 0ull);
+    }
+    if (p_saturate(s, r, L.pre[w]) && lane == 0)
+      atomicMax(&s.ctl[CTL_LASTR], r);
+    if (!grid_sync(b, ++gen))
+      return;
+    if (threadIdx.x == 0)
+      L.cnt = 0;
+    __syncthreads();
+    {
+      int alive = 0;
+      bool touch = false;
+      const int64_t wave = (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave;
+      for (int64_t base = wave * kWave; base < s.nC; base += int64_t(gridDim.x) * kPB)  // wave-uniform
+        alive += update_wave(s, base, r, prec, &touch);
+      alive = grp_isum<kWave>(alive);
+      if (lane == 0 && alive)
+        atomicAdd(&L.cnt, alive);
+      if (__any(touch) && lane == 0)
+        atomicMax(&s.ctl[CTL_LASTR], r);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && L.cnt)
+      atomicAdd(&s.ctl[CTL_PALIVE0 + (r & 1)], L.cnt);
+    if (!grid_sync(b, ++gen))
+      return;
+    if (ld_rlx(&s.ctl[CTL_PALIVE0 + (r & 1)]) == 0) {  // light table empty (maxmin.cpp:680)
+      if (lead)
+        s.ctl[CTL_ROUNDS] = r + 1;
+      return;
+    }
+    if (r + 1 >= max_rounds) {  // every round fixes a variable: a solver bug
+      if (lead)
+        st_rlx(&s.ctl[CTL_ERR], 2);
+      return;
+    }
+    if (cmp_every > 0 && r % cmp_every == cmp_every - 1 && nrows > kPB) {
+      const int out = buf == 1 ? 2 : 1;
+      p_compact(s, buf, out, nrows, alloc);
+      if (!grid_sync(b, ++gen))
+        return;
+      nrows = int64_t(ld_rlx(alloc) >> 32);
+      buf = out;
+    }
+  }
+}
+
+}  // namespace lmmdev

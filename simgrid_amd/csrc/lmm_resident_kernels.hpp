@@ -29,7 +29,7 @@ struct ResDev {
   double* e_w;       // [capE] consumption weight
   uint8_t* e_fl;     // [capE] bit0: in its constraint's enabled list
   int64_t* v_ebase;  // [capV] first element slot of the variable's slab
-  int32_t* v_n;      // [capV] elements in use (0 for a dead variable)
+  int32_t* v_n;      // [capV] elements in use; -1 = dead variable (lmm_system.cpp; loops `i < n` skip it, rs_apply_v validates it)
   double* v_pen;     // [capV] sharing penalty
   double* v_bound;   // [capV] bound (-1 = none)
   double* c_bound;   // [capC]

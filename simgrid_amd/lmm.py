@@ -114,12 +114,16 @@ SIGNATURES = {
     "lmmhip_solve": (I, [P, I, D]),
     "lmmhip_get_values": (I, [P, PD]),
     "lmmhip_values_device_ptr": (I, [P, ct.POINTER(P)]),
+    "lmmhip_get_saturated": (I, [P, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_get_touched_vars": (I, [P, ct.POINTER(ct.c_int32), I64, PI64]),
     "lmmhip_get_stats": (I, [P, P]),
     "lmmhip_set_profiling": (I, [P, I]),
     "lmmhip_launch_profile": (I, [P, PI, PI, ct.POINTER(ct.c_float), I]),
     "lmmhip_round_profile": (I, [P, PI64, PI64, I]),
     "lmmhip_vote_profile": (I, [P, PI64, PI64, I]),
     "lmmhip_ctx_set_stream": (I, [P, P]),
+    "lmmhip_ctx_use_own_stream": (I, [P]),
+    "lmmhip_ctx_set_engine": (I, [P, I]),
     "lmmhip_fb_shard_begin": (I, [P, D, P, P, P]),
     "lmmhip_fb_shard_step": (I, [P, I]),
     "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
@@ -403,6 +407,36 @@ class System:
         if not c:
             raise LmmError(lib().lmm_last_error().decode())
         return c
+
+    ENGINE_PERSISTENT, ENGINE_ROUNDS = 0, 1
+
+    def set_engine(self, engine):
+        """Max-min engine of this system's device context (lmmhip_ctx_set_engine): ENGINE_PERSISTENT (one
+        launch per solve, default) or ENGINE_ROUNDS (one launch per phase per round)."""
+        _check_hip(lib().lmmhip_ctx_set_engine(self.device_ctx(), int(engine)))
+
+    def device_values(self):
+        """Values of the last solve in the device's dense (CSR) order (lmmhip_get_values)."""
+        n = self.last_stats()["n_var"]
+        x = np.empty(n, np.float64)
+        _check_hip(lib().lmmhip_get_values(self.device_ctx(), x.ctypes.data_as(PD)))
+        return x
+
+    def device_saturated(self):
+        """Saturated set of the last solve, dense constraint order (lmmhip_get_saturated)."""
+        out = np.empty(self.last_stats()["n_cnst"], np.uint8)
+        _check_hip(lib().lmmhip_get_saturated(self.device_ctx(), out.ctypes.data_as(ct.POINTER(ct.c_uint8))))
+        return out.astype(bool)
+
+    def device_touched_vars(self):
+        """Variables of the solved system in the context's id space (lmmhip_get_touched_vars)."""
+        n = I64()
+        ctx = self.device_ctx()
+        _check_hip(lib().lmmhip_get_touched_vars(ctx, None, 0, ct.byref(n)))
+        out = np.empty(n.value, np.int32)
+        _check_hip(lib().lmmhip_get_touched_vars(ctx, out.ctypes.data_as(ct.POINTER(ct.c_int32)), n.value,
+                                                 ct.byref(n)))
+        return out
 
     def set_profiling(self, on):
         if lib().lmmhip_set_profiling(self.device_ctx(), int(on)) != 0:

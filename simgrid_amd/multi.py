@@ -210,12 +210,17 @@ class DistExchange:
         import torch
 
         rop = self.dist.ReduceOp.SUM if op == "sum" else self.dist.ReduceOp.MIN
-        if isinstance(buf, torch.Tensor) and buf.device.type == self.device.type:
-            self.dist.all_reduce(buf, op=rop, group=self.group)
+        if isinstance(buf, torch.Tensor):
+            if buf.device.type == self.device.type:
+                self.dist.all_reduce(buf, op=rop, group=self.group)
+            else:  # e.g. device shards over gloo: reduce a copy on the backend's device
+                t = buf.to(self.device)
+                self.dist.all_reduce(t, op=rop, group=self.group)
+                buf.copy_(t)
         else:
             t = torch.as_tensor(np.asarray(buf)).to(self.device)
             self.dist.all_reduce(t, op=rop, group=self.group)
-            buf[...] = t.cpu().numpy() if not isinstance(buf, torch.Tensor) else t.to(buf.device)
+            buf[...] = t.cpu().numpy()
 
 
 def next_event_date(local_min, exchange):
@@ -271,9 +276,10 @@ class DeviceFbShard:
     """One rank's part of a variable-sharded FairBottleneck solve on the current HIP device: its block
     of variables and every constraint, the three phases of lmmhip_fb_shard_step, and the exchange
     buffers as torch tensors on the device (so RCCL all-reduces them in place, stream-ordered with the
-    solver's kernels: the context launches on torch's current stream)."""
+    solver's kernels: the context launches on `stream`, by default the process's dedicated shard stream
+    `_fb_stream()`, on which fb_solve_sharded also runs the reductions)."""
 
-    def __init__(self, f, precision=None):
+    def __init__(self, f, precision=None, stream=None):
         import torch
 
         L = lmm.lib()
@@ -288,9 +294,8 @@ class DeviceFbShard:
         nc = len(f.cbound)
         # One torch stream shared by every shard of the process: the context's kernels and the torch-side
         # reductions / all-reduces of the exchange buffers (fb_solve_sharded runs them on it) are then
-        # stream-ordered.  Torch's default stream has handle 0, which lmmhip_ctx_set_stream would map to
-        # the context's own non-blocking stream -- unordered with the torch work.
-        self.stream = _fb_stream()
+        # stream-ordered.  Any torch stream works, torch's default stream (handle 0) included.
+        self.stream = _fb_stream() if stream is None else stream
         self._check(L.lmmhip_ctx_set_stream(self.ctx, ct.c_void_p(self.stream.cuda_stream)))
         self._check(L.lmmhip_upload(self.ctx, self.n, nc, len(f.cnst_idx), p(f.var_ptr, ct.c_int64),
                                     p(f.cnst_idx, ct.c_int32), p(f.weight, ct.c_double), p(f.penalty, ct.c_double),

@@ -132,6 +132,119 @@ MAXMIN_TEST_KATS = [kat_shared_penalty, kat_shared_weight, kat_shared_weight_pen
 # teshsuite/surf/lmm_usage/lmm_usage.cpp — values are not printed by the tesh (DEBUG level), so
 # the expected answers below are derived analytically.
 # ---------------------------------------------------------------------------------------------
+# ---------------------------------------------------------------------------------------------
+# FairBottleneck known answers pinned by the reference's own L07 (ptask) tesh outputs.  Each builds
+# the system the L07 model builds for one parallel task (L07Action, ptask_L07.cpp:143-207: one
+# variable of penalty 1 and bound -1; expand() on every host's CPU constraint with its flops, 0 when
+# there is no computation; expand_add() of the bytes on every link of every (i, j) route; latencies
+# already paid), on the platform of the test (CPU bound = speed, ptask_L07.cpp:239-241; link bound =
+# bandwidth, :247-249; FATPIPE links unshared), solves it with FairBottleneck::bottleneck_solve, and
+# returns [(variable, expected value, scale, printed value, tolerance)]: value * scale is what the
+# tesh prints (%f -> +-5e-7 rounding, %g -> 6 significant digits).
+# ---------------------------------------------------------------------------------------------
+def _l07_task(M, s, host_cnsts, flops, routes):
+    """One L07Action: routes = [(bytes, [link constraints])] per (i, j) with bytes > 0."""
+    links = {id(c) for _, r in routes for c in r}
+    v = s.variable_new(None, 1.0, -1.0, len(host_cnsts) + len(links))
+    for c, f in zip(host_cnsts, flops if flops is not None else [0.0] * len(host_cnsts)):
+        s.expand(c, v, f)
+    for b, r in routes:
+        for c in r:
+            s.expand_add(c, v, b)
+    return v
+
+
+def fb_exec_ptask_comm(M):
+    """examples/s4u/exec-ptask/s4u-exec-ptask.tesh:9-12 on examples/platforms/energy_platform.xml:
+    3 x 1 Gflop on 100 Mf hosts, 10 MB between each pair over the 100 kBps 'bus' -> x = 1e5 / 3e7,
+    'speed_used 3333333.333333' per host and 'bus bandwidth_used 100000.000000' (x * weight,
+    instr_platform.cpp:254-260)."""
+    s = M.System(False, M.System.FAIR_BOTTLENECK)
+    hosts = [s.constraint_new(None, 100e6) for _ in range(3)]
+    bus = s.constraint_new(None, 100e3)
+    v = _l07_task(M, s, hosts, [1e9] * 3, [(1e7, [bus]) for i in range(3) for j in range(i + 1, 3)])
+    s.solve()
+    return s, [(v, 3333333.333333, 1e9, 5e-7), (v, 100000.0, 3e7, 5e-7)]
+
+
+def fb_exec_ptask_comp(M):
+    """s4u-exec-ptask.tesh:17-19: computation only, 3e8 / 6e8 / 1e9 flops on the three 100 Mf hosts ->
+    x = 0.1, 'speed_used 30000000 / 60000000 / 100000000'."""
+    s = M.System(False, M.System.FAIR_BOTTLENECK)
+    hosts = [s.constraint_new(None, 100e6) for _ in range(3)]
+    s.constraint_new(None, 100e3)  # the bus, unused
+    v = _l07_task(M, s, hosts, [3e8, 6e8, 1e9], [])
+    s.solve()
+    return s, [(v, 30000000.0, 3e8, 5e-7), (v, 60000000.0, 6e8, 5e-7), (v, 100000000.0, 1e9, 5e-7)]
+
+
+def _platform_4p_1switch(M, s):
+    """teshsuite/simdag/platforms/platform_4p_1switch.xml: 4 hosts of 1 flop/s, link_k 1 Bps SHARED,
+    'switch' 2 Bps FATPIPE, route i->j = link_i, switch, link_j (latency 0.5 + 1 + 0.5 = 2 s)."""
+    cpus = [s.constraint_new(None, 1.0) for _ in range(4)]
+    sw = s.constraint_new(None, 2.0)
+    sw.unshare()
+    links = [s.constraint_new(None, 1.0) for _ in range(4)]
+    return cpus, links, sw
+
+
+def _fb_mxn(M, amounts):
+    s = M.System(False, M.System.FAIR_BOTTLENECK)
+    cpus, links, sw = _platform_4p_1switch(M, s)
+    routes = [(amounts[i][j], [links[i], sw, links[j]]) for i in range(4) for j in range(4) if amounts[i][j] > 0]
+    v = _l07_task(M, s, cpus, None, routes)
+    s.solve()
+    return s, v
+
+
+def fb_mxn_all2all(M):
+    """teshsuite/simdag/comm-mxn-all2all.tesh: 1 B between every ordered pair; the task ends at 8 s =
+    2 s latency + 6 s of transfer -> x = 1/6 (each link carries 6 B at 1 Bps; the FATPIPE switch takes
+    the max, 1 B, maxmin.cpp:301-304)."""
+    s, v = _fb_mxn(M, [[0, 1, 1, 1], [1, 0, 1, 1], [1, 1, 0, 1], [1, 1, 1, 0]])
+    return s, [(v, 1.0 / 6.0, 1.0, 1e-12)]
+
+
+def fb_mxn_scatter(M):
+    """teshsuite/simdag/comm-mxn-scatter.tesh: 1 / 2 / 3 B from cpu0 to cpu1..3; ends at 8 s -> x = 1/6
+    (link0 carries 6 B)."""
+    s, v = _fb_mxn(M, [[0, 1, 2, 3], [0] * 4, [0] * 4, [0] * 4])
+    return s, [(v, 1.0 / 6.0, 1.0, 1e-12)]
+
+
+def fb_mxn_independent(M):
+    """teshsuite/simdag/comm-mxn-independent.tesh: cpu0->cpu1 and cpu2->cpu3, 1 B each; ends at 3 s ->
+    x = 1 (every link carries 1 B at 1 Bps, the switch max 1 B at 2 Bps)."""
+    s, v = _fb_mxn(M, [[0, 1, 0, 0], [0] * 4, [0, 0, 0, 1], [0] * 4])
+    return s, [(v, 1.0, 1.0, 1e-12)]
+
+
+def fb_p2p_latency_bound(M):
+    """teshsuite/simdag/comm-p2p-latency-bound.tesh on platform_2p_1bb.xml: three concurrent 1-B comms
+    cpu0->cpu1 over link0 (2 Bps, 10000 s latency) plus the root task's zero-cost host elements; the
+    simulation ends at 10001.5 -> each comm gets x = 2/3 (1.5 s for 1 B)."""
+    s = M.System(False, M.System.FAIR_BOTTLENECK)
+    cpus = [s.constraint_new(None, 1.0) for _ in range(2)]
+    link = s.constraint_new(None, 2.0)
+    vs = [_l07_task(M, s, cpus, [0.0, 0.0], [(1.0, [link])]) for _ in range(3)]
+    s.solve()
+    return s, [(v, 2.0 / 3.0, 1.0, 1e-12) for v in vs]
+
+
+FB_TESH_KATS = [fb_exec_ptask_comm, fb_exec_ptask_comp, fb_mxn_all2all, fb_mxn_scatter, fb_mxn_independent,
+                fb_p2p_latency_bound]
+
+
+def check_fb_kat(expect):
+    """[(variable, printed value, scale, tol)]: |x * scale - printed| <= tol (+ a 1e-12 relative slack)."""
+    bad = []
+    for v, want, scale, tol in expect:
+        got = v.get_value() * scale
+        if not abs(got - want) <= tol + 1e-12 * abs(want):
+            bad.append((got, want))
+    return bad
+
+
 def lmm_usage_test1(M):  # lmm_usage.cpp:28-68
     s = M.System(False)
     L1 = s.constraint_new(None, 1.0)

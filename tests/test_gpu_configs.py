@@ -1,0 +1,176 @@
+"""Parity at the BASELINE.json configurations' own sizes, not scaled-down stand-ins.
+
+* C3: all 4096 maxmin_bench "medium" systems (maxmin_bench.cpp:110-116, seeds 1..4096), both as one
+  disjoint-union system (bench.py --workload c3) and as 4096 systems through lmm_solve_batch, against
+  the oracle system by system (seeds 1..5 are also golden-pinned in test_gpu_parity.py).
+* C4: 1e5 LV08 flows on the 4096-host fat tree 3;16,16,16;1,16,16;1,1,1 against the oracle.
+* C5: FairBottleneck with L07 flows on the dragonfly 8,4;16,3;8,2;4 — 1e6 flows against the oracle, and
+  at the full 1e7 flows the size-independent properties of bottleneck_solve's fixed point
+  (fair_bottleneck.cpp:59-145): every value finite and > 0, every shared constraint feasible, every
+  variable stopped by an erased constraint or its bound; plus agreement with the variable-sharded
+  device solve (multi.py), which reduces in a different order.
+Tolerances: tests/lmm_cases.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from simgrid_amd import lmm as L
+from simgrid_amd import multi as M
+from tests import lmm_cases as K
+
+pytestmark = pytest.mark.gpu
+
+C4_PLATFORM = dict(topology=L.FAT_TREE, topo_parameters="3;16,16,16;1,16,16;1,1,1", loopback_bw=1e8)
+C5_PLATFORM = dict(topology=L.DRAGONFLY, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if L.device_count() == 0:
+        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X")
+
+
+@pytest.fixture(scope="module")
+def c3_oracle():
+    """Oracle values of the 4096 medium systems (one disjoint-union system: identical per system)."""
+    o = O.System(False)
+    vs = []
+    for i in range(4096):
+        vs.extend(o.gen_maxmin_bench(1, i)[1])
+    o.solve()
+    return np.array([v.get_value() for v in vs])
+
+
+def _close(x, y):
+    tol = np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(y))
+    bad = np.nonzero(~(np.abs(x - y) <= tol))[0]
+    return bad, (float(np.max(np.abs(x - y))) if len(x) else 0.0)
+
+
+def test_c3_disjoint_union_vs_oracle(c3_oracle):
+    s = L.System(False)
+    ids = []
+    for i in range(4096):
+        ids.extend(v.h for v in s.gen_maxmin_bench(1, i)[1])
+    s.solve()
+    x = s.values_of(np.array(ids, np.int64))
+    bad, worst = _close(x, c3_oracle)
+    assert len(bad) == 0, (len(bad), worst)
+    assert s.last_stats()["n_var"] > 100_000
+
+
+def test_c3_solve_batch_vs_oracle(c3_oracle):
+    ps = [L.System(False) for _ in range(4096)]
+    ids = [np.array([v.h for v in p.gen_maxmin_bench(1, i)[1]], np.int64) for i, p in enumerate(ps)]
+    L.solve_batch(ps)
+    x = np.concatenate([p.values_of(i) for p, i in zip(ps, ids)])
+    bad, worst = _close(x, c3_oracle)
+    assert len(bad) == 0, (len(bad), worst)
+
+
+def test_c4_full_size_vs_oracle():
+    p = dict(model=L.LV08, n_flows=100_000, seed=1, **C4_PLATFORM)
+    s, o = L.System(False), O.System(False)
+    _, vs = s.gen_platform_flows(L.platform_params(**p))
+    _, ov = o.gen_platform_flows(O.platform_params(**p))
+    s.solve()
+    o.solve()
+    x, y = s.values_of(vs), o.values_of(ov, len(vs))
+    bad, worst = _close(x, y)
+    assert len(bad) == 0, (len(bad), worst)
+    assert np.all(y > 0)
+    excess, infeasible, unbottlenecked = s.check_certificate()
+    assert infeasible == 0 and unbottlenecked == 0, (excess, infeasible, unbottlenecked)
+
+
+def test_c5_1e6_flows_vs_oracle():
+    p = dict(model=L.L07, n_flows=1_000_000, seed=1, **C5_PLATFORM)
+    s, o = L.System(False, L.System.FAIR_BOTTLENECK), O.System(False, O.System.FAIR_BOTTLENECK)
+    _, vs = s.gen_platform_flows(L.platform_params(**p))
+    _, ov = o.gen_platform_flows(O.platform_params(**p))
+    s.solve()
+    o.solve()
+    x, y = s.values_of(vs), o.values_of(ov, len(vs))
+    bad, worst = _close(x, y)
+    assert len(bad) == 0, (len(bad), worst)
+
+
+def fb_fixed_point_violations(flat, x, erased, prec=1e-5):
+    """Size-independent properties of bottleneck_solve's result on the solved (flattened) system.
+    Returns (non-finite / non-positive values, infeasible shared constraints, unstopped variables)."""
+    nv, nc = len(flat["pen"]), len(flat["cbound"])
+    vp = flat["var_ptr"].astype(np.int64)
+    rows = np.repeat(np.arange(nv), np.diff(vp))
+    bad_x = int(np.count_nonzero(~np.isfinite(x) | ~(x > 0)))
+    use = np.bincount(flat["csr_c"], weights=flat["csr_w"] * x[rows], minlength=nc)
+    shared = (flat["cflags"] & 1) == 0
+    b = flat["cbound"]
+    # consumption is over-counted by the frozen variables' stale increments (fair_bottleneck.cpp:111-116),
+    # so the real usage stays within the bound up to the double_update clamp (sg_maxmin_precision)
+    infeasible = int(np.count_nonzero(shared & (use > b + np.maximum(prec, 1e-9 * b))))
+    stopped_by_cnst = np.zeros(nv, bool)
+    np.logical_or.at(stopped_by_cnst, rows, erased[flat["csr_c"]])
+    vb = flat["vbound"]
+    at_bound = (vb > 0) & (x == vb)  # fair_bottleneck.cpp:101: exact
+    unstopped = int(np.count_nonzero(~(stopped_by_cnst | at_bound)))
+    return bad_x, infeasible, unstopped
+
+
+@pytest.mark.slow
+def test_c5_full_size_fixed_point_properties():
+    s = L.System(False, L.System.FAIR_BOTTLENECK)
+    s.gen_platform_flows(L.platform_params(model=L.L07, n_flows=10_000_000, seed=1, **C5_PLATFORM),
+                         want_vars=False)
+    s.solve()
+    st = s.last_stats()
+    assert st["n_var"] == 10_000_000 and st["rounds"] > 0
+    flat = s.device_flat()
+    x = s.device_values()
+    erased = s.device_saturated()
+    bad_x, infeasible, unstopped = fb_fixed_point_violations(flat, x, erased)
+    assert (bad_x, infeasible, unstopped) == (0, 0, 0)
+
+
+def test_c5_fixed_point_properties_hold_on_the_oracle_solution():
+    """The property check itself, validated where the oracle runs: the oracle's values pass it."""
+    p = dict(model=L.L07, n_flows=20_000, seed=3, **C5_PLATFORM)
+    s, o = L.System(False, L.System.FAIR_BOTTLENECK), O.System(False, O.System.FAIR_BOTTLENECK)
+    _, vs = s.gen_platform_flows(L.platform_params(**p))
+    _, ov = o.gen_platform_flows(O.platform_params(**p))
+    s.solve()
+    o.solve()
+    flat = s.device_flat()
+    erased = s.device_saturated()
+    assert fb_fixed_point_violations(flat, s.device_values(), erased) == (0, 0, 0)
+    # the oracle's values in the device's dense order (host ids of the dense variables: lmm_flat_export)
+    pos = {int(h): k for k, h in enumerate(vs)}
+    y = o.values_of(ov, len(vs))
+    y_dense = y[[pos[int(h)] for h in M.export_flat(s).var_ids]]
+    assert fb_fixed_point_violations(flat, y_dense, erased) == (0, 0, 0)
+    bad, worst = _close(s.values_of(vs), y)
+    assert len(bad) == 0, (len(bad), worst)
+
+
+def test_c5_sharded_matches_single_context():
+    """The variable-sharded FairBottleneck (per-round exchange of counts and sums, multi.py) against the
+    single-context solve of the same system, at 1e6 flows."""
+    s = L.System(False, L.System.FAIR_BOTTLENECK)
+    _, vs = s.gen_platform_flows(L.platform_params(model=L.L07, n_flows=1_000_000, seed=2, **C5_PLATFORM))
+    f = M.export_flat(s)
+    s.solve()
+    want = s.values_of(f.var_ids)
+    shards = []
+
+    def make(sub):
+        sh = M.DeviceFbShard(sub)
+        shards.append(sh)
+        return sh
+
+    from tests.test_multi import sharded_fb_values
+
+    x = sharded_fb_values(f, M.LocalExchange(), 3, make)
+    for sh in shards:
+        sh.close()
+    bad, worst = _close(x, want)
+    assert len(bad) == 0, (len(bad), worst)

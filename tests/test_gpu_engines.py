@@ -1,0 +1,173 @@
+"""Max-min engines and determinism on the device.
+
+* The persistent engine (ONE cooperative launch per solve, lmm_persist_kernels.hpp) and the multi-launch
+  round engine run the same phase bodies: their values must be identical bit for bit.
+* System::lmm_solve is sequential and bit-reproducible in the reference (maxmin.cpp:601-606); the device
+  sums a round's decrements as fixed-point integers (CstRec in lmm_dev.hpp), so two solves of the same
+  system must give identical bytes too.
+* The stream ABI: lmmhip_ctx_set_stream(0) is the legacy null stream (torch's default stream), so a
+  FairBottleneck solve sharded on torch's default stream is ordered and correct.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from simgrid_amd import lmm as L
+from simgrid_amd import multi as M
+from tests import lmm_cases as K
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if L.device_count() == 0:
+        pytest.fail("no HIP device visible: the GPU tests must run on the MI355X")
+
+
+def _synthetic(nc, nv, seed, stress):
+    kw = dict(penalty_mix=1, bounded_permille=100, fatpipe_permille=50) if stress else {}
+
+    def build(s):
+        return s.gen_synthetic(nc, nv, 8, seed=seed, **kw)
+    return build
+
+
+def _bench(klass, run):
+    def build(s):
+        return np.array([v.h for v in s.gen_maxmin_bench(klass, run)[1]], dtype=np.int64)
+    return build
+
+
+def _platform(n_flows, seed):
+    def build(s):
+        _, vs = s.gen_platform_flows(L.platform_params(topology=L.FAT_TREE, topo_parameters="3;8,8,8;1,8,4;1,1,2",
+                                                       loopback_bw=1e9, model=L.LV08, n_flows=n_flows, seed=seed))
+        return vs
+    return build
+
+
+def _values(build, engine):
+    s = L.System(False)
+    ids = build(s)
+    s.set_engine(engine)
+    s.solve()
+    return s.values_of(ids), s.last_stats()["rounds"]
+
+
+CASES = {
+    "synthetic_2e3x2e4": _synthetic(2000, 20000, 3, False),
+    "synthetic_2e3x2e4_stress": _synthetic(2000, 20000, 3, True),
+    "synthetic_2e4x2e5": _synthetic(20000, 200000, 7, False),
+    "synthetic_1e5x1e6_stress": _synthetic(100000, 1000000, 11, True),
+    "medium_run3": _bench(1, 3),
+    "small_run7": _bench(0, 7),
+    "big_run0": _bench(2, 0),
+    "fattree_lv08_5000": _platform(5000, 2),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_engines_bit_identical(name):
+    xp, rp = _values(CASES[name], L.System.ENGINE_PERSISTENT)
+    xr, rr = _values(CASES[name], L.System.ENGINE_ROUNDS)
+    assert rp == rr
+    assert xp.tobytes() == xr.tobytes(), float(np.max(np.abs(xp - xr)))
+
+
+@pytest.mark.parametrize("engine", [0, 1])
+def test_persistent_engine_vs_oracle(engine):
+    ps, os_ = L.System(False), O.System(False)
+    pv = ps.gen_synthetic(2000, 20000, 8, seed=9, penalty_mix=1, bounded_permille=100, fatpipe_permille=50)
+    ov = os_.gen_synthetic(2000, 20000, 8, seed=9, penalty_mix=1, bounded_permille=100, fatpipe_permille=50)
+    ps.set_engine(engine)
+    ps.solve()
+    os_.solve()
+    x, y = ps.values_of(pv), os_.values_of(ov, len(pv))
+    assert np.all(np.abs(x - y) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(y))), float(np.max(np.abs(x - y)))
+
+
+@pytest.mark.parametrize("engine", [0, 1])
+def test_run_to_run_identical_stress(engine):
+    """The 2e3 x 2e4 stress system (penalties {1,2,4}, 10 % bounded, 5 % FATPIPE) solved twice."""
+    a, _ = _values(_synthetic(2000, 20000, 3, True), engine)
+    b, _ = _values(_synthetic(2000, 20000, 3, True), engine)
+    assert a.tobytes() == b.tobytes()
+
+
+def test_run_to_run_identical_resolve_same_system():
+    s = L.System(False)
+    ids = s.gen_synthetic(20000, 200000, 8, seed=5, penalty_mix=1, bounded_permille=100, fatpipe_permille=50)
+    s.solve()
+    a = s.values_of(ids)
+    for _ in range(3):
+        s.solve()
+        assert s.values_of(ids).tobytes() == a.tobytes()
+
+
+def test_run_to_run_identical_c3_batch():
+    """A C3-style batch of maxmin_bench medium systems (disjoint union) solved twice."""
+    out = []
+    for _ in range(2):
+        ps = [L.System(False) for _ in range(256)]
+        vs = [p.gen_maxmin_bench(1, i)[1] for i, p in enumerate(ps)]
+        L.solve_batch(ps)
+        out.append(np.array([v.get_value() for vv in vs for v in vv]))
+    assert out[0].tobytes() == out[1].tobytes()
+
+
+def test_fb_sharded_on_torch_default_stream():
+    """lmmhip_ctx_set_stream(0) = the legacy null stream: shards on torch's default stream are ordered
+    with the torch-side reductions of fb_solve_sharded (handle 0 used to mean "own stream")."""
+    import torch
+
+    from tests.test_multi import fb_pair, sharded_fb_values
+
+    s, o, ovars = fb_pair()
+    f = M.export_flat(s)
+    shards = []
+
+    def make(sub):
+        sh = M.DeviceFbShard(sub, stream=torch.cuda.default_stream())
+        shards.append(sh)
+        return sh
+
+    x = sharded_fb_values(f, M.LocalExchange(), 2, make)
+    for sh in shards:
+        sh.close()
+    o.solve()
+    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+    assert np.all(np.abs(x - want) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(want)))
+
+
+def test_fb_device_shards_over_gloo():
+    """DistExchange on gloo with device-resident exchange buffers (the CPU-device branch of
+    allreduce_ used np.asarray on a CUDA tensor): a world-1 gloo group in this process."""
+    import os
+
+    import torch.distributed as dist
+
+    from tests.test_multi import fb_pair, sharded_fb_values
+
+    s, o, ovars = fb_pair(seed=6)
+    f = M.export_flat(s)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        ex = M.DistExchange()
+        shards = []
+
+        def make(sub):
+            sh = M.DeviceFbShard(sub)
+            shards.append(sh)
+            return sh
+
+        x = sharded_fb_values(f, ex, 2, make)
+        for sh in shards:
+            sh.close()
+    finally:
+        dist.destroy_process_group()
+    o.solve()
+    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+    assert np.all(np.abs(x - want) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(want)))

@@ -129,6 +129,14 @@ def test_random_fair_bottleneck_vs_oracle(seed, variant):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("kat", K.FB_TESH_KATS, ids=lambda f: f.__name__)
+def test_fair_bottleneck_tesh_kats(kat):
+    """FairBottleneck on the device vs the answers the reference's L07 tesh files print (the same KATs
+    pin the oracle in tests/test_oracle.py)."""
+    _, expect = kat(L)
+    assert not K.check_fb_kat(expect)
+
+
 def test_fair_bottleneck_nonterminating_input_is_reported():
     s = L.System(False, L.System.FAIR_BOTTLENECK)
     z = s.constraint_new(None, 0.0)  # zero-bound: its variable leaves the list with mu = 0

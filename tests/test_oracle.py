@@ -87,3 +87,11 @@ def test_oracle_feasible_and_bottlenecked_on_random():
             if not (c.get_bound() > c.get_bound() * prec):
                 continue  # skipped by lmm_solve (maxmin.cpp:524): a zero-bound constraint is ignored
             assert not (c.get_usage() - c.get_bound() > c.get_bound() * prec)
+
+
+@pytest.mark.parametrize("kat", K.FB_TESH_KATS, ids=lambda f: f.__name__)
+def test_oracle_fair_bottleneck_tesh_kats(kat):
+    """Pin the FairBottleneck restatement (fair_bottleneck.cpp:23-153) on the answers the reference's L07
+    tesh files print (examples/s4u/exec-ptask, teshsuite/simdag/comm-mxn-*, comm-p2p-latency-bound)."""
+    _, expect = kat(O)
+    assert not K.check_fb_kat(expect)
