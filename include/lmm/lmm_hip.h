@@ -66,6 +66,15 @@ int lmmhip_upload(lmmhip_ctx* ctx, int64_t n_var, int64_t n_cnst, int64_t nnz, c
                   const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
                   const double* cnst_bound, const uint8_t* cnst_flags);
 
+/* lmmhip_upload with the order of each constraint's elements given: csc_order[p] (p = 0..nnz-1,
+ * constraint-major) is the CSR index of the p-th element of constraint k's segment, k ascending; NULL =
+ * ascending CSR order.  FairBottleneck subtracts a constraint's increments one at a time in this order
+ * (fair_bottleneck.cpp:111-116), so passing each constraint's enabled_element_set_ order makes a
+ * one-context FAIR_BOTTLENECK solve bit-identical to the reference. */
+int lmmhip_upload2(lmmhip_ctx* ctx, int64_t n_var, int64_t n_cnst, int64_t nnz, const int64_t* var_ptr,
+                   const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
+                   const double* cnst_bound, const uint8_t* cnst_flags, const int64_t* csc_order);
+
 /* Update per-variable penalty/bound or per-constraint bound in place (no structural change). */
 int lmmhip_update_vars(lmmhip_ctx* ctx, const double* penalty, const double* var_bound);
 int lmmhip_update_cnsts(lmmhip_ctx* ctx, const double* cnst_bound);
@@ -161,6 +170,14 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
 #define LMMHIP_ENGINE_PERSISTENT 0
 #define LMMHIP_ENGINE_ROUNDS 1
 int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
+/* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the
+ * wall-clock time (100 MHz) of the last workgroup's arrival and of workgroup 0's exit.  With t != NULL,
+ * copies the last solve's records: t[2i] = last arrival at barrier i, t[2i+1] = exit (barrier 0 = the
+ * launch); *n = barriers recorded (fills up to cap / 2). */
+int lmmhip_persist_profile(lmmhip_ctx* ctx, int on, int64_t* t, int64_t cap, int64_t* n);
+/* Per-workgroup records of the same profiled solve, for the first *nbar barriers: t[2 (g * nblk + b)] =
+ * arrival of workgroup b at barrier g, t[... + 1] = its exit. */
+int lmmhip_persist_profile_blocks(lmmhip_ctx* ctx, int64_t* t, int64_t cap, int64_t* nbar, int64_t* nblk);
 
 /* FairBottleneck with the variables sharded over ranks (simgrid_amd/multi.py).  The
  * context holds this rank's variables and EVERY constraint (constraint indices are global).  A round

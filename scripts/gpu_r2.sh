@@ -21,4 +21,6 @@ for eng in persistent rounds; do
   rc=$?; echo "bench c4 $eng rc=$rc" >> gpurun_out/bench_c4_$eng.log
   if [ $rc -ne 0 ]; then echo "STOP after bench c4 $eng rc=$rc"; exit $rc; fi
 done
+timeout -k 10 200 python -u scripts/diag_r2.py c4 > gpurun_out/diag_c4.log 2>&1 || { echo "diag c4 rc=$?"; exit 1; }
+timeout -k 10 300 python -u scripts/diag_r2.py c2 > gpurun_out/diag_c2.log 2>&1 || { echo "diag c2 rc=$?"; exit 1; }
 exit 0

@@ -47,7 +47,8 @@ enum : int {
 // to 2^-61 of the constraint's bound / initial usage (256x finer than one fp64 ulp of it).
 struct alignas(64) CstRec {
   unsigned long long drem, duse, dcnt;  // fixed-point decrements pushed this round; dcnt = fixed elements
-  int64_t pad;
+                                        // (dcnt > 0: touched this round)
+  int64_t pad;              // round + 1 in which mm_saturate saturated the constraint (0 = never)
   double rem, use;          // remaining, usage (maxmin.cpp:520-535, 603-658)
   double ratio;             // rem / use; +inf when out of the light table
   double bound;             // constraint bound
@@ -117,7 +118,6 @@ struct Dev {
   uint64_t* chgbits;  // [nC/64 + 2] bitmap: constraints changed in the last round (written by mm_update)
   int32_t* ready;   // [nC + slack] ready constraints, one segment per mm_ready block
   int32_t* bready;  // [kMaxBlocks] ready count of each segment
-  uint8_t* touched;  // [nC] 1 = received a decrement this round (set by the pushers, cleared by mm_update)
   int32_t* balive;  // [kMaxBlocks] constraints still alive after mm_update, per block
   int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
   int32_t* clist[2];  // [nC] alive-constraint lists (periodically compacted)

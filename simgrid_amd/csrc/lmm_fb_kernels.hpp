@@ -209,6 +209,65 @@ __global__ void __launch_bounds__(kBlock) fbk_update(Dev s, double prec) {
   }
 }
 
+// :107-140 for ONE context: a shared constraint's remaining takes its elements' w * mu ONE AT A TIME in
+// the CSC order, each step a double_update (surf_interface.hpp:34-44) — the reference's own loop
+// (fair_bottleneck.cpp:111-116) operation for operation, so with the CSC in enabled_element_set_ order
+// (lmmhip_upload2) the result is bit-identical.  Not an order-free sum: the saturating constraint's
+// remaining ends a few ulps of its bound away from 0, and whether that residue is below the precision
+// (erasure, :129) depends on the rounding of this exact chain — a tree sum is more accurate and erases
+// constraints the reference keeps (C5 at 1e6 flows: 28 of them in round 0, a different fixed point for
+// 12 % of the flows).  One wave per constraint: lanes gather 64 increments into LDS, lane 0 chains them.
+// FATPIPE as fbk_update.
+__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ double dl[kBlock];
+  const int lane = threadIdx.x & (kWave - 1);
+  double* d = dl + (threadIdx.x - lane);
+  for (int64_t c = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; c < s.nC;
+       c += int64_t(gridDim.x) * (kBlock / kWave)) {  // wave-uniform
+    if (lane == 0)
+      s.erased[c] = 0;
+    if (s.ratio[c] != 0.0)
+      continue;
+    double rem = s.rem[c];
+    if (s.cflags[c] & 1) {
+      double u = s.use[c];
+      if (s.cflags[c] & 2)
+        u = fmin(u, 0.0);
+      u = fmin(u, s.xmin[c]);
+      if (lane == 0)
+        s.use[c] = u;
+      rem -= u;
+      if (rem < prec)
+        rem = 0.0;
+    } else {
+      const uint32_t ce = s.cnst_ptr[c + 1];
+      for (uint32_t base = s.cnst_ptr[c]; base < ce; base += kWave) {  // wave-uniform
+        const uint32_t j = base + lane;
+        d[lane] = j < ce ? s.csc_w[j] * s.vtmp[s.csc_v[j]] : 0.0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          const int n = int(ce - base < uint32_t(kWave) ? ce - base : uint32_t(kWave));
+          for (int k = 0; k < n; k++) {
+            rem -= d[k];
+            if (rem < prec)
+              rem = 0.0;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (lane == 0) {
+      s.rem[c] = rem;
+      if (rem <= 0.0) {
+        s.ratio[c] = dinf();
+        s.erased[c] = 1;
+      }
+    }
+  }
+}
+
 // :132-139 — the listed variables of an erased constraint leave the list
 __global__ void __launch_bounds__(kBlock) fbk_unlist(Dev s) {
   if (s.ctl[CTL_DONE])

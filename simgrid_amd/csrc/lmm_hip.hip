@@ -25,6 +25,8 @@
 
 using namespace lmmdev;
 
+constexpr unsigned kPersistProfCap = 1 << 16;  // barriers covered by lmmhip_persist_profile
+
 namespace {
 
 thread_local std::string g_err;
@@ -84,6 +86,8 @@ struct lmmhip_ctx {
   // multi-launch round chain; grid-barrier words of the persistent launch
   int engine = LMMHIP_ENGINE_PERSISTENT;
   unsigned* pbar = nullptr;
+  bool persist_prof = false;    // record barrier timestamps in the persistent launch
+  long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
   int persist_grid = 0;  // workgroups of the persistent launch (one per CU, checked at first use)
   bool ev1_done = false;  // the solve recorded ev1 itself (right behind its last kernel)
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
@@ -228,6 +232,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipFree(c->vstat);
   if (c->pbar)
     (void)hipFree(c->pbar);
+  if (c->ptime)
+    (void)hipFree(c->ptime);
   if (c->ev0)
     (void)hipEventDestroy(c->ev0);
   if (c->ev1)
@@ -288,7 +294,6 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   }
   rc |= dalloc(c, &d.chg, nC);
   rc |= dalloc(c, &d.chgbits, (nC + 127) / 128 * 2 + 2);
-  rc |= dalloc(c, &d.touched, nC);
   rc |= dalloc(c, &d.ready, nC + kMaxBlocks);
   rc |= dalloc(c, &d.bready, kMaxBlocks);
   rc |= dalloc(c, &d.balive, kMaxBlocks);
@@ -395,6 +400,13 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
 int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int64_t* var_ptr,
                   const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
                   const double* cnst_bound, const uint8_t* cnst_flags) {
+  return lmmhip_upload2(c, nV, nC, nnz, var_ptr, cnst_idx, weight, penalty, var_bound, cnst_bound, cnst_flags,
+                        nullptr);
+}
+
+int lmmhip_upload2(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int64_t* var_ptr,
+                   const int32_t* cnst_idx, const double* weight, const double* penalty, const double* var_bound,
+                   const double* cnst_bound, const uint8_t* cnst_flags, const int64_t* csc_order) {
   if (!c)
     return fail(LMMHIP_E_ARG, "null context");
   if (nV < 0 || nC < 0 || nnz < 0 || nV >= (1 << 30) || nC >= (1 << 30) || nnz > INT32_MAX)
@@ -430,7 +442,7 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
     cptr[size_t(k) + 1] += cptr[size_t(k)];
   std::vector<int32_t> cv(static_cast<size_t>(nnz));
   std::vector<double> cw(static_cast<size_t>(nnz));
-  {
+  if (!csc_order) {
     std::vector<uint32_t> cur(cptr.begin(), cptr.end() - 1);
     for (int64_t v = 0; v < nV; v++)
       for (int64_t j = var_ptr[v]; j < var_ptr[v + 1]; j++) {
@@ -438,6 +450,23 @@ int lmmhip_upload(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, const int6
         cv[pos] = int32_t(v);
         cw[pos] = weight[j];
       }
+  } else {  // the caller's order within each constraint: a permutation of its CSR elements
+    std::vector<int32_t> row(static_cast<size_t>(nnz));
+    for (int64_t v = 0; v < nV; v++)
+      for (int64_t j = var_ptr[v]; j < var_ptr[v + 1]; j++)
+        row[size_t(j)] = int32_t(v);
+    std::vector<uint8_t> seen(static_cast<size_t>(nnz), 0);
+    int64_t k = 0;
+    for (int64_t pos = 0; pos < nnz; pos++) {
+      while (k < nC && cptr[size_t(k) + 1] <= uint32_t(pos))
+        k++;
+      const int64_t j = csc_order[pos];
+      if (j < 0 || j >= nnz || seen[size_t(j)] || cnst_idx[j] != k)
+        return fail(LMMHIP_E_ARG, "csc_order is not a constraint-major permutation of the CSR elements");
+      seen[size_t(j)] = 1;
+      cv[size_t(pos)] = row[size_t(j)];
+      cw[size_t(pos)] = weight[j];
+    }
   }
   // fair bottleneck CSC chunks (lmm_fb_kernels.hpp)
   std::vector<int32_t> c_ch(static_cast<size_t>(nC) + 1, 0), ch_cnst;
@@ -1192,7 +1221,17 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   const int max_rounds = int(std::min<int64_t>(int64_t(d.nV) + 2, INT32_MAX - 1));
   const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 16);
   unsigned* barw = c->pbar;
-  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every)};
+  long long* pt = nullptr;
+  unsigned pt_cap = 0;
+  if (c->persist_prof) {  // barrier timestamps (lmmhip_persist_profile)
+    pt_cap = kPersistProfCap;
+    const size_t bytes = sizeof(long long) * (2 * size_t(pt_cap) + 2 * size_t(kPBlkCap) * size_t(grid));
+    if (!c->ptime)
+      HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->ptime), bytes));
+    HIPCHK(hipMemsetAsync(c->ptime, 0, bytes, c->stream));
+    pt = c->ptime;
+  }
+  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap};
   HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
   c->stats.kernel_launches[2] += 1;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -1234,7 +1273,10 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
     LAUNCH(4, r, fbk_accc, gC, kBlock, d);
     break;
   case 2:
-    LAUNCH(5, r, fbk_update, gC, kBlock, d, c->fb_prec);
+    if (c->fb_shard)  // shards: the summed increments come through the exchange buffer
+      LAUNCH(5, r, fbk_update, gC, kBlock, d, c->fb_prec);
+    else  // one context: element by element in the CSC order, bit-identical to the reference
+      LAUNCH(5, r, fbk_update_seq, grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec);
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
     c->fb_round++;
     break;
@@ -1287,6 +1329,46 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->stream = c->own_stream;
+  return 0;
+}
+
+int lmmhip_persist_profile(lmmhip_ctx* c, int on, int64_t* t, int64_t cap, int64_t* n) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  c->persist_prof = on != 0;
+  if (n)
+    *n = 0;
+  if (!t || !c->ptime)
+    return 0;
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<long long> h(2 * size_t(kPersistProfCap));
+  HIPCHK(hipMemcpyAsync(h.data(), c->ptime, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int64_t m = 0;
+  while (m < int64_t(kPersistProfCap) && h[2 * size_t(m) + 1] != 0)
+    m++;
+  for (int64_t i = 0; i < m && 2 * i + 1 < cap; i++) {
+    t[2 * i] = h[2 * size_t(i)];
+    t[2 * i + 1] = h[2 * size_t(i) + 1];
+  }
+  if (n)
+    *n = m;
+  return 0;
+}
+
+int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_t* nbar, int64_t* nblk) {
+  if (!c || !c->ptime || !c->persist_grid)
+    return fail(LMMHIP_E_STATE, "no profiled persistent solve");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t n = 2 * size_t(kPBlkCap) * size_t(c->persist_grid);
+  std::vector<long long> h(n);
+  HIPCHK(hipMemcpyAsync(h.data(), c->ptime + 2 * size_t(kPersistProfCap), n * sizeof(long long),
+                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < n && int64_t(i) < cap; i++)
+    t[i] = h[i];
+  *nbar = kPBlkCap;
+  *nblk = c->persist_grid;
   return 0;
 }
 

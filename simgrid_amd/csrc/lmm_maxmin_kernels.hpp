@@ -70,7 +70,6 @@ __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64
       // fixed-point scales of this solve's decrements (CstRec): a round never removes more than the
       // remaining (<= bound) or the usage (<= initial usage) from a constraint
       s.cexp[c] = alive ? int32_t((uint32_t(uint16_t(dec_scale(usage))) << 16) | uint16_t(dec_scale(bound))) : 0;
-      s.touched[c] = 0;
       s.nvote[c] = int32_t(e - b);  // no element votes yet
       s.chg[c] = uint16_t(0xFFFF);
       s.key[c] = alive ? ratio_key(r) : uint16_t(kDeadKey);
@@ -110,8 +109,7 @@ __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double 
   if (s.key[c] == kDeadKey)
     return;
   unsigned long long* r = &s.cst[c].drem;
-  s.touched[c] = 1;
-  atomicAdd(&r[2], 1ull);
+  atomicAdd(&r[2], 1ull);  // dcnt > 0 marks the constraint touched for mm_update
   if (!(s.cflags[c] & 1)) {
     const double w = s.csr_w[j];
     const int32_t ce = s.cexp[c];
@@ -621,8 +619,6 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
         const long long e1 = __shfl(a1[u], e, kWave);
         if (ec >= 0 && q < 3 && (!ef || q == 2))
           atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
-        if (ec >= 0 && q == 3)
-          s.touched[ec] = 1;  // plain byte store: mm_update reads 1 B per constraint, not the record
       }
     }
   }
@@ -635,10 +631,8 @@ template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int3
   const uint32_t ce = s.cnst_ptr[c + 1];
   for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
     saturate_chunk(s, c, r, base, ce, round, lane, pre);
-  if (k == 0 && lane == 0) {
-    s.key[c] = kDeadKey;
-    s.chg[c] = uint16_t(round);
-  }
+  if (k == 0 && lane == 0)  // c leaves the light table: mm_update (the owner of key / chg) retires it
+    st_rlx(&s.cst[c].pad, int64_t(round) + 1);
 }
 
 // K waves per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
@@ -711,14 +705,24 @@ __device__ __forceinline__ int update_wave(const Dev& s, int64_t base, int round
   const int64_t c = base + lane;
   bool changed = false, live = false, tch = false, fat = false;
   unsigned okey = kDeadKey;
+  CstRec* rec = s.cst + c;
+  unsigned long long qx = 0, qy = 0, qz = 0;
   if (c < s.nC) {
     okey = s.key[c];
-    if (okey == kDeadKey) {
-      changed = s.chg[c] == uint16_t(round);  // saturated by mm_saturate this round
-    } else {
-      live = true;
-      tch = s.touched[c];
-      fat = tch && (s.cflags[c] & 1);
+    if (okey != kDeadKey) {
+      if (rec->pad == int64_t(round) + 1) {  // saturated by mm_saturate this round (maxmin.cpp:608-615)
+        s.key[c] = kDeadKey;
+        s.chg[c] = uint16_t(round);
+        rec->ratio = dinf();
+        changed = true;
+      } else {
+        live = true;
+        qx = rec->drem;
+        qy = rec->duse;
+        qz = rec->dcnt;
+        tch = qz != 0;  // received decrements this round
+        fat = tch && (s.cflags[c] & 1);
+      }
     }
   }
   double fuse = 0.0;
@@ -742,9 +746,6 @@ __device__ __forceinline__ int update_wave(const Dev& s, int64_t base, int round
       alive = 1;
     } else {
       *touch = true;
-      s.touched[c] = 0;
-      CstRec* rec = s.cst + c;
-      const unsigned long long qx = rec->drem, qy = rec->duse, qz = rec->dcnt;
       rec->drem = rec->duse = rec->dcnt = 0;
       s.nvote[c] -= int(qz);  // fixed elements leave (voters of c were compensated)
       s.chg[c] = uint16_t(round);

@@ -28,6 +28,7 @@ constexpr int kPW = kPB / kWave;     // waves per workgroup
 constexpr int kPBitWords = 16384;    // LDS bitmap: 2^20 constraints (128 KB)
 constexpr int kPFilt = 4;            // rows per thread per filter step
 constexpr long long kSpinTicks = 400000000;  // 4 s of the 100 MHz wall clock: a barrier wait gives up
+constexpr unsigned kPBlkCap = 1024;          // barriers with per-workgroup timestamps (profiling)
 
 // Grid-barrier words (zeroed by the host before every launch), each counter on its own 64-B line.
 enum : int {
@@ -38,7 +39,8 @@ enum : int {
   BAR_XSIZE = 288,  // [8 x 16] workgroups on each XCC (counted at launch)
   BAR_FLAT = 416,   // launch rendezvous
   BAR_ALLOC = 432,  // u64 (2 words, 8-B aligned): compaction allocator (rows << 32 | elements)
-  BAR_WORDS = 448
+  BAR_PALIVE = 448,  // [2 parities x 16]: constraints alive after a round's update, 8 partial words each
+  BAR_WORDS = 480
 };
 
 __device__ __forceinline__ unsigned xcc_id() {
@@ -64,6 +66,8 @@ struct PBar {
   unsigned* w;
   int32_t* err;
   unsigned xcc, xsize, nx;  // meaningful in thread 0 only
+  long long* pt;            // profiling (else null): per barrier [last arrival, workgroup 0's exit] (wall clock)
+  unsigned pt_cap;          // barriers covered
 };
 
 // Launch rendezvous: count the workgroups per XCC (for the hierarchical barrier) and wait for all.
@@ -101,6 +105,12 @@ __device__ bool grid_sync(const PBar& b, unsigned gen) {
   __syncthreads();
   if (threadIdx.x == 0) {
     int ok = 1;
+    if (b.pt && gen < b.pt_cap) {
+      const long long now = wall_clock64();
+      atomicMax(&b.pt[2 * gen], now);
+      if (gen < kPBlkCap)  // per-workgroup arrival
+        b.pt[2 * b.pt_cap + 2 * (size_t(gen) * gridDim.x + blockIdx.x)] = now;
+    }
     const unsigned a =
         __hip_atomic_fetch_add(&b.w[BAR_XCNT + 16 * b.xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a == gen * b.xsize - 1) {  // XCC leader
@@ -118,11 +128,22 @@ __device__ bool grid_sync(const PBar& b, unsigned gen) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (b.pt && gen < b.pt_cap) {
+      const long long now = wall_clock64();
+      if (blockIdx.x == 0)
+        b.pt[2 * gen + 1] = now;
+      if (gen < kPBlkCap)  // per-workgroup exit
+        b.pt[2 * b.pt_cap + 2 * (size_t(gen) * gridDim.x + blockIdx.x) + 1] = now;
+    }
     ok_sh = ok;
   }
   __syncthreads();
   return ok_sh;
 }
+
+// Wave id interleaved over the workgroups (wave w of workgroup b -> w * grid + b): consecutive 64-item
+// groups land on different CUs (and XCDs), so a small item count still spreads over the whole chip.
+__device__ __forceinline__ int64_t pwave() { return int64_t(threadIdx.x / kWave) * gridDim.x + blockIdx.x; }
 
 template <bool kBits> struct PVoteLds {
   uint64_t bits[kBits ? kPBitWords : 2];
@@ -140,7 +161,7 @@ template <bool kBits> union PLds {
 // the target is still strictly below the row's other keys (skey), or — sensitive rows (skey 0) — when
 // its target was touched last round (chg stamp).  Queued rows are resolved kPB at a time (vote_row).
 template <bool kBits>
-__device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds<kBits>& L) {
+__device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds<kBits>& L, bool count) {
   if (kBits) {
     const int n16 = (s.nC + 127) / 128;
     const uint4* src = reinterpret_cast<const uint4*>(s.chgbits);
@@ -155,13 +176,17 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
   const uint16_t* skey = s.skey[buf];
   const uint16_t prev = uint16_t(round - 1);
   const int lane = threadIdx.x & (kWave - 1);
+  // one contiguous chunk of rows per workgroup (a multiple of 64), in steps of kPB * kPFilt rows
   constexpr int64_t kStep = int64_t(kPB) * kPFilt;
-  for (int64_t base = int64_t(blockIdx.x) * kStep; base < nrows; base += int64_t(gridDim.x) * kStep) {
+  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;
+  const int64_t lo = int64_t(blockIdx.x) * per;
+  const int64_t hi = lo + per < nrows ? lo + per : nrows;
+  for (int64_t base = lo; base < hi; base += kStep) {  // workgroup-uniform
     int tt[kPFilt];
 #pragma unroll
     for (int u = 0; u < kPFilt; u++) {
       const int64_t row = base + u * kPB + threadIdx.x;
-      tt[u] = row < nrows ? rtgt[row] : kRetired;
+      tt[u] = row < hi ? rtgt[row] : kRetired;
     }
     bool ch[kPFilt];
     unsigned sk[kPFilt], kt[kPFilt], cg[kPFilt];
@@ -181,7 +206,7 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
 #pragma unroll
     for (int u = 0; u < kPFilt; u++) {
       const int64_t row = base + u * kPB + threadIdx.x;
-      bool need = tt[u] == kUnvoted;
+      bool need = tt[u] == kUnvoted;  // (rows >= hi carry kRetired)
       if (ch[u])
         need = !(kt[u] < sk[u]);
       else if (kBits && cg[u] == prev)
@@ -211,7 +236,7 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
   const int n = L.qn;
   if (threadIdx.x < n)
     vote_row(s, buf, round, L.q[threadIdx.x], &L.st0, &L.st1);
-  if (threadIdx.x == 0 && L.nq + n)
+  if (count && threadIdx.x == 0 && L.nq + n)
     atomicAdd(&s.ctl[CTL_RESEVAL], L.nq + n);
 }
 
@@ -220,7 +245,7 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
 // variable (each alive variable votes for exactly one constraint), so the claims never race across waves.
 __device__ bool p_saturate(const Dev& s, int round, int* pre) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wave = (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave;
+  const int64_t wave = pwave();
   const int64_t nwaves = int64_t(gridDim.x) * kPW;
   bool any = false;
   for (int64_t base = wave * kWave; base < s.nC; base += nwaves * kWave) {  // wave-uniform
@@ -243,7 +268,7 @@ __device__ bool p_saturate(const Dev& s, int round, int* pre) {
 // and fixed-point sum is order-independent.
 __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned long long* alloc) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wave = (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave;
+  const int64_t wave = pwave();
   const int64_t nwaves = int64_t(gridDim.x) * kPW;
   int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
   uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
@@ -296,14 +321,17 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
 
 template <bool kBits>
 __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double prec, int max_rounds,
-                                                  int cmp_every) {
+                                                  int cmp_every, long long* pt, unsigned pt_cap) {
   __shared__ PLds<kBits> L;
-  PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0};
+  PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0, pt, pt_cap};
+  if (pt && blockIdx.x == 0 && threadIdx.x == 0)
+    pt[1] = wall_clock64();  // launch (barrier 0's exit slot)
   unsigned long long* alloc = reinterpret_cast<unsigned long long*>(barw + BAR_ALLOC);
+  int32_t* palive = reinterpret_cast<int32_t*>(barw + BAR_PALIVE);
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
   // init (maxmin.cpp:509-555) overlapped with the rendezvous
-  init_cnsts_waves(s, prec, (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave, int64_t(gridDim.x) * kPW);
+  init_cnsts_waves(s, prec, pwave(), int64_t(gridDim.x) * kPW);
   init_vars_range(s, int64_t(blockIdx.x) * kPB + threadIdx.x, int64_t(gridDim.x) * kPB);
   if (!bar_init(b))
     return;
@@ -311,15 +339,15 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
   int buf = 0;
   int64_t nrows = s.nV;
   for (int r = 0;; r++) {
-    p_vote<kBits>(s, buf, r, nrows, L.v);
+    p_vote<kBits>(s, buf, r, nrows, L.v, pt != nullptr);
     if (!grid_sync(b, ++gen))
       return;
     if (lead) {  // words first used later in this round, last read before the previous barrier
-      st_rlx(&s.ctl[CTL_PALIVE0 + ((r + 1) & 1)], 0);
+      for (int i = 0; i < 8; i++)
+        st_rlx(&palive[16 * ((r + 1) & 1) + i], 0);
       st_rlx(alloc, 0ull);
     }
-    if (p_saturate(s, r, L.pre[w]) && lane == 0)
-      atomicMax(&s.ctl[CTL_LASTR], r);
+    p_saturate(s, r, L.pre[w]);
     if (!grid_sync(b, ++gen))
       return;
     if (threadIdx.x == 0)
@@ -328,23 +356,26 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
     {
       int alive = 0;
       bool touch = false;
-      const int64_t wave = (int64_t(blockIdx.x) * kPB + threadIdx.x) / kWave;
-      for (int64_t base = wave * kWave; base < s.nC; base += int64_t(gridDim.x) * kPB)  // wave-uniform
+      for (int64_t base = pwave() * kWave; base < s.nC; base += int64_t(gridDim.x) * kPB)  // wave-uniform
         alive += update_wave(s, base, r, prec, &touch);
       alive = grp_isum<kWave>(alive);
       if (lane == 0 && alive)
         atomicAdd(&L.cnt, alive);
-      if (__any(touch) && lane == 0)
-        atomicMax(&s.ctl[CTL_LASTR], r);
     }
     __syncthreads();
+    // one add per workgroup, spread over 8 words (a single word takes ~88 atomics/us)
     if (threadIdx.x == 0 && L.cnt)
-      atomicAdd(&s.ctl[CTL_PALIVE0 + (r & 1)], L.cnt);
+      atomicAdd(&palive[16 * (r & 1) + (blockIdx.x & 7)], L.cnt);
     if (!grid_sync(b, ++gen))
       return;
-    if (ld_rlx(&s.ctl[CTL_PALIVE0 + (r & 1)]) == 0) {  // light table empty (maxmin.cpp:680)
-      if (lead)
+    int alive_all = 0;
+    for (int i = 0; i < 8; i++)
+      alive_all += ld_rlx(&palive[16 * (r & 1) + i]);
+    if (alive_all == 0) {  // light table empty (maxmin.cpp:680)
+      if (lead) {  // every round with a live constraint fixes a variable: rounds = r + 1
         s.ctl[CTL_ROUNDS] = r + 1;
+        s.ctl[CTL_LASTR] = r;
+      }
       return;
     }
     if (r + 1 >= max_rounds) {  // every round fixes a variable: a solver bug

@@ -770,6 +770,9 @@ void System::flatten_fair(Flat& f) {
       f.cflags.push_back(uint8_t((k.policy == SharingPolicy::FATPIPE ? 1 : 0) | (zero_w ? 2 : 0)));
     }
   }
+  // CSR index of every flattened element (-1 = not flattened), for the CSC order below
+  const bool ordered = f.csc_order.size() == f.cnst_idx.size();
+  std::vector<int32_t> csr_of(ordered ? elems_.size() : 0, -1);
   for (Id v = 0; v < Id(vars_.size()); v++) {
     const VarRec& r = vars_[v];
     if (!r.live || !(r.penalty > 0))
@@ -782,6 +785,8 @@ void System::flatten_fair(Flat& f) {
     for (int i = 0; i < r.n_elems; i++) {
       const ElemRec& x = elems_[r.ebase + i];
       if (x.weight > 0 && dense_c[x.cnst] >= 0) {
+        if (ordered)
+          csr_of[size_t(r.ebase + i)] = int32_t(f.cnst_idx.size());
         f.cnst_idx.push_back(dense_c[x.cnst]);
         f.weight.push_back(x.weight);
       }
@@ -791,6 +796,13 @@ void System::flatten_fair(Flat& f) {
     f.vbound.push_back(r.bound);
     f.dense_vars.push_back(v);
   }
+  // each listed constraint's flattened elements in its enabled-list order (dense constraint order)
+  if (ordered)
+    for (Id c = act_head_; c != kNone; c = cnsts_[c].act_next)
+      if (dense_c[c] >= 0)
+        for (Id e = cnsts_[c].en_head; e != kNone; e = elems_[e].next)
+          if (csr_of[size_t(e)] >= 0)
+            f.csc_order.push_back(csr_of[size_t(e)]);
 }
 
 void System::flatten_into(Flat& f) {
@@ -832,8 +844,10 @@ void System::prepare() {
   const int64_t nC = int64_t(flat_.cbound.size());
   const int64_t nnz = int64_t(flat_.cnst_idx.size());
   auto t1 = std::chrono::steady_clock::now();
-  int rc = lmmhip_upload(ctx(), nV, nC, nnz, flat_.var_ptr.data(), flat_.cnst_idx.data(), flat_.weight.data(),
-                         flat_.penalty.data(), flat_.vbound.data(), flat_.cbound.data(), flat_.cflags.data());
+  const bool ordered = int64_t(flat_.csc_order.size()) == nnz && nnz > 0;
+  int rc = lmmhip_upload2(ctx(), nV, nC, nnz, flat_.var_ptr.data(), flat_.cnst_idx.data(), flat_.weight.data(),
+                          flat_.penalty.data(), flat_.vbound.data(), flat_.cbound.data(), flat_.cflags.data(),
+                          ordered ? flat_.csc_order.data() : nullptr);
   if (rc)
     fatal(std::string("upload failed: ") + lmmhip_last_error());
   stats_.upload_ms = ms_since(t1);
@@ -1095,9 +1109,11 @@ void solve_batch(System** systems, int n) {
     var_begin[i + 1] = f.dense_vars.size();
   }
   System* s0 = systems[0];
-  int rc = lmmhip_upload(s0->ctx(), int64_t(f.dense_vars.size()), int64_t(f.cbound.size()),
-                         int64_t(f.cnst_idx.size()), f.var_ptr.data(), f.cnst_idx.data(), f.weight.data(),
-                         f.penalty.data(), f.vbound.data(), f.cbound.data(), f.cflags.data());
+  const bool ordered = f.csc_order.size() == f.cnst_idx.size() && !f.cnst_idx.empty();
+  int rc = lmmhip_upload2(s0->ctx(), int64_t(f.dense_vars.size()), int64_t(f.cbound.size()),
+                          int64_t(f.cnst_idx.size()), f.var_ptr.data(), f.cnst_idx.data(), f.weight.data(),
+                          f.penalty.data(), f.vbound.data(), f.cbound.data(), f.cflags.data(),
+                          ordered ? f.csc_order.data() : nullptr);
   if (rc)
     fatal(std::string("batch upload failed: ") + lmmhip_last_error());
   rc = lmmhip_solve(s0->ctx(), kind == SolverKind::FAIR_BOTTLENECK ? 1 : 0, maxmin_precision);

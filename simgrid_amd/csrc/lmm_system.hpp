@@ -152,6 +152,10 @@ public:
     std::vector<double> weight, penalty, vbound, cbound;
     std::vector<uint8_t> cflags;
     std::vector<Id> dense_vars;  // dense index -> variable id
+    // FairBottleneck: CSR element index of every CSC position, constraint-major, each constraint's
+    // elements in the order of its enabled_element_set_ (the order bottleneck_solve subtracts them in,
+    // fair_bottleneck.cpp:111-116); empty = the device's default order (lmmhip_upload2)
+    std::vector<int64_t> csc_order;
   };
   // Append this system's active part to `f` (constraint indices offset by f.cbound.size()).
   void flatten_into(Flat& f);

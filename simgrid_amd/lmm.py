@@ -124,6 +124,8 @@ SIGNATURES = {
     "lmmhip_ctx_set_stream": (I, [P, P]),
     "lmmhip_ctx_use_own_stream": (I, [P]),
     "lmmhip_ctx_set_engine": (I, [P, I]),
+    "lmmhip_persist_profile": (I, [P, I, PI64, I64, PI64]),
+    "lmmhip_persist_profile_blocks": (I, [P, PI64, I64, PI64, PI64]),
     "lmmhip_fb_shard_begin": (I, [P, D, P, P, P]),
     "lmmhip_fb_shard_step": (I, [P, I]),
     "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
@@ -437,6 +439,25 @@ class System:
         _check_hip(lib().lmmhip_get_touched_vars(ctx, out.ctypes.data_as(ct.POINTER(ct.c_int32)), n.value,
                                                  ct.byref(n)))
         return out
+
+    def persist_profile(self, on=True):
+        """Barrier timestamps of the persistent engine (lmmhip_persist_profile): (last arrival, exit) per
+        barrier of the last solve, in 10-ns ticks, as an (n, 2) array."""
+        ctx = self.device_ctx()
+        n = I64()
+        cap = 1 << 17
+        t = np.zeros(cap, np.int64)
+        _check_hip(lib().lmmhip_persist_profile(ctx, int(on), t.ctypes.data_as(PI64), cap, ct.byref(n)))
+        return t[:2 * n.value].reshape(-1, 2)
+
+    def persist_profile_blocks(self):
+        """Per-workgroup (arrival, exit) ticks of the profiled persistent solve: (barriers, workgroups, 2)."""
+        ctx = self.device_ctx()
+        cap = 2 * 1024 * 1024
+        t = np.zeros(cap, np.int64)
+        nb, nw = I64(), I64()
+        _check_hip(lib().lmmhip_persist_profile_blocks(ctx, t.ctypes.data_as(PI64), cap, ct.byref(nb), ct.byref(nw)))
+        return t[:2 * nb.value * nw.value].reshape(nb.value, nw.value, 2)
 
     def set_profiling(self, on):
         if lib().lmmhip_set_profiling(self.device_ctx(), int(on)) != 0:
