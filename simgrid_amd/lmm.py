@@ -102,6 +102,8 @@ SIGNATURES = {
     "lmmhip_ctx_create": (I, [I, ct.POINTER(P)]),
     "lmmhip_ctx_destroy": (I, [P]),
     "lmmhip_upload": (I, [P, I64, I64, I64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
+    "lmmhip_upload2": (I, [P, I64, I64, I64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8),
+                           PI64]),
     "lmmhip_update_vars": (I, [P, PD, PD]),
     "lmmhip_update_cnsts": (I, [P, PD]),
     "lmmhip_res_apply": (I, [P, I64, I64, I64, I64, PI64, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8), I64, ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD, PD, I64, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8)]),
