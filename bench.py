@@ -273,15 +273,20 @@ def run_config(args):
 
     t = time.time()
     shards = None
+    batch = None
     if args.workload == "c3":
         n_sys = 4096
         bounds = M.balanced_blocks(np.ones(n_sys), world)
-        s = lmm.System(False)
+        systems = []
         for i in range(bounds[rank], bounds[rank + 1]):
-            s.gen_maxmin_bench(1, i)
+            systems.append(lmm.System(False))
+            systems[-1].gen_maxmin_bench(1, i)
+        batch = M.DeviceBatch(systems)  # block-diagonal upload: one workgroup per system, system in LDS
+        del systems
         work_vars, scaling = 100 * n_sys, "strong"
         desc = dict(workload="C3: 4096 independent maxmin_bench medium systems (100 cnst x 100 vars), "
-                             "one disjoint-union solve per rank", systems=n_sys,
+                             "one block-diagonal batch per rank (lmmhip_set_batch: one workgroup per system, "
+                             "the system in LDS)", systems=n_sys,
                     parallelism=f"systems in nnz-balanced blocks x{world}")
     elif args.workload == "c4":
         flows = args.flows or 100_000
@@ -306,7 +311,9 @@ def run_config(args):
         desc = dict(workload=f"C5: {flows} L07 flows on dragonfly {C5_PLATFORM['topo_parameters']} (4096 hosts), "
                              "FairBottleneck", flows=flows,
                     parallelism=f"variables sharded x{world}, 2 all-reduces per round")
-    if shards is None:
+    if batch is not None:
+        nV, nC, nnz = batch.n_var, batch.n_cnst, batch.nnz
+    elif shards is None:
         s.prepare()
         st = s.last_stats()
         nV, nC, nnz = st["n_var"], st["n_cnst"], st["nnz"]
@@ -315,6 +322,9 @@ def run_config(args):
     log(f"[rank {rank}] {args.workload}: built in {time.time() - t:.1f}s: nV={nV} nC={nC} nnz={nnz}")
 
     def step():
+        if batch is not None:
+            batch.solve()
+            return batch.stats()["rounds"]
         if shards is None:
             s.device_solve()
             return s.last_stats()["rounds"]
@@ -344,7 +354,7 @@ def run_config(args):
     else:
         alg = 56 * tot[1] + 24 * tot[0] + 32 * tot[2]
     ach = alg / (ms_per_step * 1e-3) / 1e9
-    if args.profile_json and rank == 0 and shards is None:  # per-launch HIP events of one extra solve
+    if args.profile_json and rank == 0 and shards is None and batch is None:  # per-launch HIP events of one extra solve
         s.set_profiling(True)
         s.device_solve()
         s.set_profiling(False)
@@ -373,6 +383,8 @@ def run_config(args):
     if shards is not None:
         for sh in shards:
             sh.close()
+    if batch is not None:
+        batch.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -120,6 +120,14 @@ int lmmhip_flat_download(lmmhip_ctx* ctx, int64_t* counts3, uint32_t* var_ptr, i
                          uint32_t* cnst_ptr, int32_t* csc_v, double* csc_w, double* penalty, double* var_bound,
                          double* cnst_bound, uint8_t* cnst_flags);
 
+/* Declare the uploaded system a disjoint union of nsys independent systems (a parameter sweep, SURVEY.md
+ * §8(a) C3): system i owns the dense variables [var_off[i], var_off[i+1]) and constraints
+ * [cnst_off[i], cnst_off[i+1]) (offsets cover the system; checked on the device: no element may link two
+ * systems).  A MAXMIN lmmhip_solve then runs one workgroup per system with the system in LDS
+ * (lmm_batch_kernels.hpp) when the largest one fits (< 65535 variables / constraints / elements,
+ * <= 64 KB of LDS), else the global engines.  nsys = 0 clears; every upload clears. */
+int lmmhip_set_batch(lmmhip_ctx* ctx, int64_t nsys, const int64_t* var_off, const int64_t* cnst_off);
+
 /* Solve on the device; values stay resident in HBM until lmmhip_get_values(). */
 int lmmhip_solve(lmmhip_ctx* ctx, int kind, double precision);
 
@@ -162,13 +170,15 @@ int lmmhip_ctx_set_stream(lmmhip_ctx* ctx, void* hip_stream);
 int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
 
 /* Max-min engine (the round loop of maxmin.cpp:560-680):
- *   LMMHIP_ENGINE_PERSISTENT (default) — ONE cooperative launch per solve: the rounds' phases separated
- *     by grid barriers, termination decided on the device, no host round-trip;
+ *   LMMHIP_ENGINE_PERSISTENT — ONE cooperative launch per solve: the rounds' phases separated by grid
+ *     barriers, termination decided on the device, no host round-trip;
  *   LMMHIP_ENGINE_ROUNDS — one launch per phase per round, the host polling termination every few
- *     rounds (also the engine of the profiling mode, which times every phase launch).
- * Both give bit-identical results.  The environment variable LMMHIP_ENGINE=rounds|persistent overrides. */
+ *     rounds (also the engine of the profiling mode, which times every phase launch);
+ *   LMMHIP_ENGINE_AUTO (default) — persistent up to 2^18 variables, rounds above.
+ * All give bit-identical results.  The environment variable LMMHIP_ENGINE=rounds|persistent overrides. */
 #define LMMHIP_ENGINE_PERSISTENT 0
 #define LMMHIP_ENGINE_ROUNDS 1
+#define LMMHIP_ENGINE_AUTO 2
 int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
 /* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the
  * wall-clock time (100 MHz) of the last workgroup's arrival and of workgroup 0's exit.  With t != NULL,

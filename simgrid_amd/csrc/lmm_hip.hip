@@ -20,12 +20,14 @@
 #include "lmm_step_kernels.hpp"
 #include "lmm_maxmin_kernels.hpp"
 #include "lmm_persist_kernels.hpp"
+#include "lmm_batch_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
 #include "lmm_scan.hpp"
 
 using namespace lmmdev;
 
 constexpr unsigned kPersistProfCap = 1 << 16;  // barriers covered by lmmhip_persist_profile
+constexpr int64_t kAutoPersistVars = 1 << 18;   // LMMHIP_ENGINE_AUTO: persistent up to this many variables
 
 namespace {
 
@@ -84,12 +86,19 @@ struct lmmhip_ctx {
   int32_t* vstat = nullptr;  // profiling counters of mm_vote ([round][block] x 2)
   // maxmin engine (lmmhip_ctx_set_engine): one persistent launch per solve (default) or the
   // multi-launch round chain; grid-barrier words of the persistent launch
-  int engine = LMMHIP_ENGINE_PERSISTENT;
+  int engine = LMMHIP_ENGINE_AUTO;
   unsigned* pbar = nullptr;
   bool persist_prof = false;    // record barrier timestamps in the persistent launch
   long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
   int persist_grid = 0;  // workgroups of the persistent launch (one per CU, checked at first use)
   bool ev1_done = false;  // the solve recorded ev1 itself (right behind its last kernel)
+  // block-diagonal batch (lmmhip_set_batch): system offsets on the device, largest system
+  int64_t bt_n = 0;
+  int64_t* bt_voff = nullptr;
+  int64_t* bt_coff = nullptr;
+  int32_t* bt_rounds = nullptr;  // [grid] rounds of each workgroup's systems
+  int bt_max_nv = 0, bt_max_nc = 0, bt_max_nnz = 0;
+  int64_t bt_cap = 0;
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
   int64_t fb_round = 0;
   double fb_prec = 0;
@@ -232,6 +241,9 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipFree(c->vstat);
   if (c->pbar)
     (void)hipFree(c->pbar);
+  for (void* p : {(void*)c->bt_voff, (void*)c->bt_coff, (void*)c->bt_rounds})
+    if (p)
+      (void)hipFree(p);
   if (c->ptime)
     (void)hipFree(c->ptime);
   if (c->ev0)
@@ -390,6 +402,7 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
   }
   c->uploaded = true;
   c->solved = false;
+  c->bt_n = 0;  // a new system: no batch declared
   c->stats = lmmhip_stats{};
   c->stats.n_var = nV;
   c->stats.n_cnst = nC;
@@ -981,6 +994,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec);
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec);
 static int solve_fair(lmmhip_ctx* c, double prec);
 static int engine_of(const lmmhip_ctx* c);
+static bool batch_fits(const lmmhip_ctx* c);
+static int solve_maxmin_batch(lmmhip_ctx* c, double prec);
 static int resolve_profile(lmmhip_ctx* c);
 
 int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
@@ -1012,6 +1027,7 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   c->solved = false;
   c->ev1_done = false;
   int rc = kind == LMMHIP_KIND_FAIR_BOTTLENECK ? solve_fair(c, precision)
+           : batch_fits(c)                             ? solve_maxmin_batch(c, precision)
            : engine_of(c) == LMMHIP_ENGINE_PERSISTENT ? solve_maxmin_persist(c, precision)
                                                      : solve_maxmin(c, precision);
   if (rc)
@@ -1196,7 +1212,13 @@ static int engine_of(const lmmhip_ctx* c) {
   const char* e = std::getenv("LMMHIP_ENGINE");
   if (e && *e)
     return std::strcmp(e, "rounds") == 0 ? LMMHIP_ENGINE_ROUNDS : LMMHIP_ENGINE_PERSISTENT;
-  return c->engine;
+  if (c->engine != LMMHIP_ENGINE_AUTO)
+    return c->engine;
+  // AUTO (measured): one launch per solve where the host round-trips and launches of the
+  // round chain dominate (small systems: a tie at C4, 1e5 variables, and ahead below); the round chain
+  // above, where the kernel boundaries (~1.5 us) are cheaper than grid barriers (~4 us) and per-launch
+  // grids keep 32 waves per CU in flight instead of 16
+  return int64_t(c->d.nV) <= kAutoPersistVars ? LMMHIP_ENGINE_PERSISTENT : LMMHIP_ENGINE_ROUNDS;
 }
 
 // One cooperative launch per solve (lmm_persist_kernels.hpp): one 1024-thread workgroup per CU, all
@@ -1231,7 +1253,8 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
     HIPCHK(hipMemsetAsync(c->ptime, 0, bytes, c->stream));
     pt = c->ptime;
   }
-  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap};
+  int sysf = env_int("LMMHIP_PERSIST_SYSFENCE", 0);
+  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf};
   HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
   c->stats.kernel_launches[2] += 1;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -1243,6 +1266,45 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   if (c->h_ctl[CTL_ERR] == 2)
     return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
   return 0;
+}
+
+// ---- block-diagonal batches: one workgroup per system, the system in LDS (lmm_batch_kernels.hpp) ----
+constexpr size_t kBatchLdsMax = 64 * 1024;  // per workgroup; larger systems take the global engines
+
+static bool batch_fits(const lmmhip_ctx* c) {
+  if (c->bt_n <= 0 || c->profiling)
+    return false;
+  if (const char* e = std::getenv("LMMHIP_BATCH"); e && *e == '0')
+    return false;
+  return c->bt_max_nv < 65535 && c->bt_max_nc < 65535 && c->bt_max_nnz < 65535 &&
+         batch_lds_bytes(c->bt_max_nv, c->bt_max_nc, c->bt_max_nnz) <= kBatchLdsMax;
+}
+
+static int solve_maxmin_batch(lmmhip_ctx* c, double prec) {
+  const size_t lds = batch_lds_bytes(c->bt_max_nv, c->bt_max_nc, c->bt_max_nnz);
+  int per_cu = 0;
+  HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&mm_batch_lds),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, int(kBatchLdsMax)));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&mm_batch_lds), kBB,
+                                                      lds));
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(c->bt_n, int64_t(c->n_cu) * std::max(per_cu, 1)));
+  if (grid > c->bt_cap) {
+    if (c->bt_rounds)
+      HIPCHK(hipFree(c->bt_rounds));
+    c->bt_rounds = nullptr;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->bt_rounds), sizeof(int32_t) * size_t(grid)));
+    c->bt_cap = grid;
+  }
+  Dev d = c->d;
+  hipLaunchKernelGGL(mm_batch_lds, dim3(unsigned(grid)), dim3(kBB), lds, c->stream, d, c->bt_voff, c->bt_coff,
+                     c->bt_n, prec, c->bt_max_nv, c->bt_max_nc, c->bt_max_nnz, c->bt_rounds);
+  HIPCHK(hipGetLastError());
+  c->stats.kernel_launches[2] += 1;
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->ev1_done = true;
+  hipLaunchKernelGGL(mm_batch_rounds, dim3(1), dim3(kBlock), 0, c->stream, c->bt_rounds, int(grid), d.ctl);
+  HIPCHK(hipGetLastError());
+  return poll_ctl(c);
 }
 
 static int fb_begin(lmmhip_ctx* c, double prec) {
@@ -1332,6 +1394,54 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* c) {
   return 0;
 }
 
+int lmmhip_set_batch(lmmhip_ctx* c, int64_t nsys, const int64_t* var_off, const int64_t* cnst_off) {
+  if (!c || !c->uploaded)
+    return fail(LMMHIP_E_STATE, "no system uploaded");
+  c->bt_n = 0;
+  if (nsys == 0)
+    return 0;
+  if (nsys < 0 || !var_off || !cnst_off)
+    return fail(LMMHIP_E_ARG, "bad batch arguments");
+  const Dev& d = c->d;
+  if (var_off[0] != 0 || var_off[nsys] != d.nV || cnst_off[0] != 0 || cnst_off[nsys] != d.nC)
+    return fail(LMMHIP_E_ARG, "batch offsets must cover the uploaded system");
+  for (int64_t i = 0; i < nsys; i++)
+    if (var_off[i + 1] < var_off[i] || cnst_off[i + 1] < cnst_off[i])
+      return fail(LMMHIP_E_ARG, "batch offsets not monotone");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<uint32_t> vp(size_t(d.nV) + 1);
+  HIPCHK(hipMemcpyAsync(vp.data(), d.var_ptr, vp.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int64_t mv = 0, mc = 0, me = 0;
+  for (int64_t i = 0; i < nsys; i++) {
+    mv = std::max(mv, var_off[i + 1] - var_off[i]);
+    mc = std::max(mc, cnst_off[i + 1] - cnst_off[i]);
+    me = std::max(me, int64_t(vp[size_t(var_off[i + 1])]) - int64_t(vp[size_t(var_off[i])]));
+  }
+  for (void* p : {(void*)c->bt_voff, (void*)c->bt_coff})
+    if (p)
+      HIPCHK(hipFree(p));
+  c->bt_voff = c->bt_coff = nullptr;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->bt_voff), sizeof(int64_t) * size_t(nsys + 1)));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->bt_coff), sizeof(int64_t) * size_t(nsys + 1)));
+  HIPCHK(hipMemcpyAsync(c->bt_voff, var_off, sizeof(int64_t) * size_t(nsys + 1), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->bt_coff, cnst_off, sizeof(int64_t) * size_t(nsys + 1), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(d.ctl + CTL_ERR, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(mm_batch_check, dim3(unsigned(std::min<int64_t>(nsys, 4096))), dim3(kBlock), 0, c->stream, d,
+                     c->bt_voff, c->bt_coff, nsys, d.ctl + CTL_ERR);
+  HIPCHK(hipGetLastError());
+  int32_t bad = 0;
+  HIPCHK(hipMemcpyAsync(&bad, d.ctl + CTL_ERR, sizeof(bad), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (bad)
+    return fail(LMMHIP_E_ARG, "batch: an element links two declared systems (not block-diagonal)");
+  c->bt_n = nsys;
+  c->bt_max_nv = int(mv);
+  c->bt_max_nc = int(mc);
+  c->bt_max_nnz = int(me);
+  return 0;
+}
+
 int lmmhip_persist_profile(lmmhip_ctx* c, int on, int64_t* t, int64_t cap, int64_t* n) {
   if (!c)
     return fail(LMMHIP_E_ARG, "null context");
@@ -1375,7 +1485,7 @@ int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_
 int lmmhip_ctx_set_engine(lmmhip_ctx* c, int engine) {
   if (!c)
     return fail(LMMHIP_E_ARG, "null context");
-  if (engine != LMMHIP_ENGINE_PERSISTENT && engine != LMMHIP_ENGINE_ROUNDS)
+  if (engine != LMMHIP_ENGINE_PERSISTENT && engine != LMMHIP_ENGINE_ROUNDS && engine != LMMHIP_ENGINE_AUTO)
     return fail(LMMHIP_E_ARG, "unknown maxmin engine");
   c->engine = engine;
   return 0;

@@ -784,6 +784,123 @@ __device__ __forceinline__ int update_wave(const Dev& s, int64_t base, int round
   return alive;
 }
 
+// update_wave over K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups
+// (key, then record, flags, scale, votes) is issued before any of them is used, so a wave keeps K times
+// the memory requests in flight — the persistent engine has 16 waves per CU, not 32.  Same arithmetic
+// as update_wave (bit-identical results).
+template <int K>
+__device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
+                                             bool* touch) {
+  const int lane = threadIdx.x & (kWave - 1);
+  unsigned okey[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int64_t c = base0 + k * stride + lane;
+    okey[k] = c < s.nC ? unsigned(s.key[c]) : kDeadKey;
+  }
+  int64_t pad[K];
+  unsigned long long qx[K], qy[K], qz[K];
+  double rem[K], use[K], bnd[K];
+  int32_t ce[K], nv[K];
+  uint8_t fl[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int64_t c = base0 + k * stride + lane;
+    pad[k] = 0;
+    qx[k] = qy[k] = qz[k] = 0;
+    rem[k] = use[k] = bnd[k] = 0.0;
+    ce[k] = nv[k] = 0;
+    fl[k] = 0;
+    if (okey[k] != kDeadKey) {
+      const CstRec* rec = s.cst + c;
+      pad[k] = rec->pad;
+      qx[k] = rec->drem;
+      qy[k] = rec->duse;
+      qz[k] = rec->dcnt;
+      rem[k] = rec->rem;
+      use[k] = rec->use;
+      bnd[k] = rec->bound;
+      ce[k] = s.cexp[c];
+      nv[k] = s.nvote[c];
+      fl[k] = s.cflags[c];
+    }
+  }
+  int alive = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int64_t gbase = base0 + k * stride;
+    if (gbase >= s.nC)  // wave-uniform
+      break;
+    const int64_t c = gbase + lane;
+    const bool live0 = okey[k] != kDeadKey;
+    const bool sat = live0 && pad[k] == int64_t(round) + 1;
+    const bool live = live0 && !sat;
+    const bool tch = live && qz[k] != 0;
+    const bool fat = tch && (fl[k] & 1);
+    double fuse = 0.0;
+    unsigned long long fm = __ballot(fat);
+    while (fm) {  // wave-uniform: FATPIPE usage over the still-unfixed elements (maxmin.cpp:625-658)
+      const int l = __ffsll((long long)fm) - 1;
+      fm &= fm - 1;
+      const int64_t cl = gbase + l;
+      const uint32_t b = s.cnst_ptr[cl], e = s.cnst_ptr[cl + 1];
+      double m = 0.0;
+      for (uint32_t j = b + lane; j < e; j += kWave)
+        if (!(s.x[s.csc_v[j]] > 0))
+          m = fmax(m, s.csc_u[j]);
+      m = wave_max(m);
+      if (lane == l)
+        fuse = m;
+    }
+    bool changed = false;
+    CstRec* rec = s.cst + c;
+    if (sat) {
+      s.key[c] = kDeadKey;
+      s.chg[c] = uint16_t(round);
+      rec->ratio = dinf();
+      changed = true;
+    } else if (live) {
+      if (!tch) {
+        alive++;
+      } else {
+        *touch = true;
+        rec->drem = rec->duse = rec->dcnt = 0;
+        s.nvote[c] = nv[k] - int(qz[k]);
+        s.chg[c] = uint16_t(round);
+        double r0 = rem[k], u0;
+        if (!fat) {
+          u0 = use[k] - dec_val(qy[k], cexp_use(ce[k]));
+          r0 -= dec_val(qx[k], cexp_rem(ce[k]));
+          if (r0 < bnd[k] * prec)
+            r0 = 0.0;
+          if (u0 < prec)
+            u0 = 0.0;
+        } else {
+          u0 = fuse;
+        }
+        rec->rem = r0;
+        rec->use = u0;
+        if (!(u0 > prec) || !(r0 > bnd[k] * prec)) {
+          rec->ratio = dinf();
+          s.key[c] = kDeadKey;
+          changed = true;
+        } else {
+          const double r = r0 / u0;
+          rec->ratio = r;
+          const unsigned nk = ratio_key(r);
+          s.key[c] = uint16_t(nk);
+          changed = nk != okey[k];
+          alive++;
+        }
+      }
+    }
+    const unsigned long long word = __ballot(changed);
+    if (lane == 0)
+      s.chgbits[gbase >> 6] = word;
+  }
+  return alive;
+}
+
 // balive[block] = constraints of the block's range still in the light table (read by mm_done; plain
 // stores, no global atomic).
 __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {

@@ -68,6 +68,7 @@ struct PBar {
   unsigned xcc, xsize, nx;  // meaningful in thread 0 only
   long long* pt;            // profiling (else null): per barrier [last arrival, workgroup 0's exit] (wall clock)
   unsigned pt_cap;          // barriers covered
+  int sysf;                 // 1: system-scope release / acquire (also writes back / invalidates the L2)
 };
 
 // Launch rendezvous: count the workgroups per XCC (for the hierarchical barrier) and wait for all.
@@ -114,7 +115,10 @@ __device__ bool grid_sync(const PBar& b, unsigned gen) {
     const unsigned a =
         __hip_atomic_fetch_add(&b.w[BAR_XCNT + 16 * b.xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a == gen * b.xsize - 1) {  // XCC leader
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (b.sysf)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      else
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned t = __hip_atomic_fetch_add(&b.w[BAR_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == gen * b.nx - 1)
@@ -126,7 +130,10 @@ __device__ bool grid_sync(const PBar& b, unsigned gen) {
     } else {
       ok = spin_geq(&b.w[BAR_XGEN + 16 * b.xcc], gen, b.err);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (b.sysf)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (b.pt && gen < b.pt_cap) {
       const long long now = wall_clock64();
@@ -262,22 +269,52 @@ __device__ bool p_saturate(const Dev& s, int round, int* pre) {
   return any;
 }
 
-// C: order-free compaction of the alive rows of buffer `in` into `out`: per wave ONE 64-bit atomic
-// allocates its rows AND their elements (rows << 32 | elements), so consecutive allocations stay
-// consistent in both (row k's end = row k+1's start).  Row order does not matter: every vote, claim
-// and fixed-point sum is order-independent.
-__device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned long long* alloc) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wave = pwave();
-  const int64_t nwaves = int64_t(gridDim.x) * kPW;
+// C: compaction of the alive rows of buffer `in` into `out`, one contiguous chunk of rows per workgroup:
+// pass 1 counts the chunk's alive rows and elements, ONE 64-bit atomic per workgroup allocates both
+// (rows << 32 | elements, so consecutive allocations stay consistent: row k's end = row k+1's start),
+// pass 2 writes them in chunk order (workgroup scans).  Chunks land in allocation order: row order is
+// free (every vote, claim and fixed-point sum is order-independent).
+__device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned long long* alloc, int* sh) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
   uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
   int32_t* ocol = const_cast<int32_t*>(s.ccol[out]);
-  for (int64_t base = wave * kWave; base < nrows; base += nwaves * kWave) {  // wave-uniform
-    const int64_t row = base + lane;
+  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kPB - 1) / kPB * kPB;
+  const int64_t lo = int64_t(blockIdx.x) * per;
+  const int64_t hi = lo + per < nrows ? lo + per : nrows;
+  int nr = 0, ne = 0;  // pass 1
+  for (int64_t row = lo + threadIdx.x; row < hi; row += kPB)
+    if (s.vstate[s.cvar[in][row]] == 0) {
+      nr++;
+      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
+    }
+  nr = grp_isum<kWave>(nr);
+  ne = grp_isum<kWave>(ne);
+  if (lane == 0) {
+    sh[2 * w] = nr;
+    sh[2 * w + 1] = ne;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tr = 0, te = 0;
+    for (int i = 0; i < kPW; i++) {
+      tr += unsigned(sh[2 * i]);
+      te += unsigned(sh[2 * i + 1]);
+    }
+    const unsigned long long old = tr ? atomicAdd(alloc, (tr << 32) | te) : 0ull;
+    sh[2 * kPW] = int(old >> 32);
+    sh[2 * kPW + 1] = int(uint32_t(old));
+    sh[2 * kPW + 2] = tr != 0;
+  }
+  __syncthreads();
+  uint32_t rbase = uint32_t(sh[2 * kPW]), ebase = uint32_t(sh[2 * kPW + 1]);
+  const bool allocated = sh[2 * kPW + 2] != 0;
+  __syncthreads();
+  for (int64_t b0 = lo; b0 < hi; b0 += kPB) {  // pass 2, workgroup-uniform
+    const int64_t row = b0 + threadIdx.x;
     int32_t v = -1;
     uint32_t b = 0, e = 0;
-    if (row < nrows) {
+    if (row < hi) {
       v = s.cvar[in][row];
       if (s.vstate[v] == 0) {
         b = s.crow[in][row];
@@ -286,44 +323,52 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
         v = -1;
       }
     }
-    const int len = int(e - b);
-    int incl = len;
+    int xr = v >= 0, xe = int(e - b);
+    int ir = xr, ie = xe;  // inclusive wave scans
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
-      const int t = __shfl_up(incl, o, kWave);
-      if (lane >= o)
-        incl += t;
+      const int tr = __shfl_up(ir, o, kWave), te = __shfl_up(ie, o, kWave);
+      if (lane >= o) {
+        ir += tr;
+        ie += te;
+      }
     }
-    const unsigned total = unsigned(__shfl(incl, kWave - 1, kWave));
-    const unsigned long long m = __ballot(v >= 0);
-    if (!m)
-      continue;
-    const unsigned k = unsigned(__popcll(m));
-    unsigned long long old = 0;
-    if (lane == 0)
-      old = atomicAdd(alloc, (static_cast<unsigned long long>(k) << 32) | total);
-    old = __shfl(old, 0, kWave);
-    const uint32_t r0 = uint32_t(old >> 32), e0 = uint32_t(old);
+    if (lane == kWave - 1) {
+      sh[2 * w] = ir;
+      sh[2 * w + 1] = ie;
+    }
+    __syncthreads();
+    int orr = 0, oe = 0, tr = 0, te = 0;
+    for (int i = 0; i < kPW; i++) {
+      orr += i < w ? sh[2 * i] : 0;
+      oe += i < w ? sh[2 * i + 1] : 0;
+      tr += sh[2 * i];
+      te += sh[2 * i + 1];
+    }
     if (v >= 0) {
-      const uint32_t o = r0 + uint32_t(__popcll(m & ((1ull << lane) - 1)));
-      const uint32_t dst = e0 + uint32_t(incl - len);
+      const uint32_t o = rbase + uint32_t(orr + ir - xr);
+      const uint32_t dst = ebase + uint32_t(oe + ie - xe);
       ovar[o] = v;
       s.rtgt[out][o] = s.rtgt[in][row];
       s.skey[out][o] = s.skey[in][row];
       orow[o] = dst;
-      for (uint32_t j = 0; j < uint32_t(len); j++)
+      for (int j = 0; j < xe; j++)
         ocol[dst + j] = s.ccol[in][b + j];
     }
-    if (lane == 63 - __clzll(m))  // the wave's last row also writes the end of its elements
-      orow[r0 + k] = e0 + total;
+    rbase += uint32_t(tr);
+    ebase += uint32_t(te);
+    __syncthreads();
   }
+  // the end of the workgroup's last row: the next allocation's start (or the total, for the last one)
+  if (threadIdx.x == 0 && allocated)
+    orow[rbase] = ebase;
 }
 
 template <bool kBits>
 __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double prec, int max_rounds,
-                                                  int cmp_every, long long* pt, unsigned pt_cap) {
+                                                  int cmp_every, long long* pt, unsigned pt_cap, int sysf) {
   __shared__ PLds<kBits> L;
-  PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0, pt, pt_cap};
+  PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0, pt, pt_cap, sysf};
   if (pt && blockIdx.x == 0 && threadIdx.x == 0)
     pt[1] = wall_clock64();  // launch (barrier 0's exit slot)
   unsigned long long* alloc = reinterpret_cast<unsigned long long*>(barw + BAR_ALLOC);
@@ -356,8 +401,10 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
     {
       int alive = 0;
       bool touch = false;
-      for (int64_t base = pwave() * kWave; base < s.nC; base += int64_t(gridDim.x) * kPB)  // wave-uniform
-        alive += update_wave(s, base, r, prec, &touch);
+      constexpr int kU = 3;  // groups of 64 constraints per wave step, loads in flight together
+      const int64_t stride = int64_t(gridDim.x) * kPB;
+      for (int64_t base = pwave() * kWave; base < s.nC; base += kU * stride)  // wave-uniform
+        alive += update_groups<kU>(s, base, stride, r, prec, &touch);
       alive = grp_isum<kWave>(alive);
       if (lane == 0 && alive)
         atomicAdd(&L.cnt, alive);
@@ -385,7 +432,7 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
     }
     if (cmp_every > 0 && r % cmp_every == cmp_every - 1 && nrows > kPB) {
       const int out = buf == 1 ? 2 : 1;
-      p_compact(s, buf, out, nrows, alloc);
+      p_compact(s, buf, out, nrows, alloc, &L.pre[0][0]);
       if (!grid_sync(b, ++gen))
         return;
       nrows = int64_t(ld_rlx(alloc) >> 32);

@@ -1100,13 +1100,15 @@ void solve_batch(System** systems, int n) {
   const SolverKind kind = systems[0]->kind();
   System::Flat f;
   std::vector<size_t> var_begin(size_t(n) + 1, 0);
-  std::vector<std::vector<Id>> dense(n);
+  std::vector<int64_t> voff(size_t(n) + 1, 0), coff(size_t(n) + 1, 0);  // block-diagonal layout
   for (int i = 0; i < n; i++) {
     check(systems[i]->kind() == kind, "solve_batch: mixed solver kinds");
     size_t before = f.dense_vars.size();
     systems[i]->flatten_into(f);
     var_begin[i] = before;
     var_begin[i + 1] = f.dense_vars.size();
+    voff[size_t(i) + 1] = int64_t(f.dense_vars.size());
+    coff[size_t(i) + 1] = int64_t(f.cbound.size());
   }
   System* s0 = systems[0];
   const bool ordered = f.csc_order.size() == f.cnst_idx.size() && !f.cnst_idx.empty();
@@ -1116,6 +1118,8 @@ void solve_batch(System** systems, int n) {
                           ordered ? f.csc_order.data() : nullptr);
   if (rc)
     fatal(std::string("batch upload failed: ") + lmmhip_last_error());
+  if (kind == SolverKind::MAXMIN && (rc = lmmhip_set_batch(s0->ctx(), n, voff.data(), coff.data())))
+    fatal(std::string("batch declaration failed: ") + lmmhip_last_error());
   rc = lmmhip_solve(s0->ctx(), kind == SolverKind::FAIR_BOTTLENECK ? 1 : 0, maxmin_precision);
   if (rc)
     fatal(std::string("batch solve failed: ") + lmmhip_last_error());

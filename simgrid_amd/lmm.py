@@ -37,6 +37,12 @@ def platform_params(topology=FAT_TREE, topo_parameters="", bw=1.25e8, lat=5e-5, 
     return PlatformParams(topology, topo_parameters.encode(), bw, lat, policy, loopback_bw, loopback_lat, limiter_bw,
                           speed, model, int(crosstraffic), n_flows, seed, size_min, size_max, tcp_gamma)
 
+class LmmhipStats(ct.Structure):
+    """lmmhip_stats (include/lmm/lmm_hip.h)."""
+    _fields_ = [("rounds", I64), ("n_var", I64), ("n_cnst", I64), ("nnz", I64), ("device_ms", D),
+                ("kernel_ms", D * 8), ("kernel_launches", I64 * 8)]
+
+
 SIGNATURES = {
     # include/lmm/lmm_system.h
     "lmm_set_precision": (None, [D]),
@@ -114,6 +120,7 @@ SIGNATURES = {
     "lmmhip_res_refreshes": (I, [P, PI64]),
     "lmmhip_flat_download": (I, [P, PI64, P, P, P, P, P, P, P, P, P, P]),
     "lmmhip_solve": (I, [P, I, D]),
+    "lmmhip_set_batch": (I, [P, I64, PI64, PI64]),
     "lmmhip_get_values": (I, [P, PD]),
     "lmmhip_values_device_ptr": (I, [P, ct.POINTER(P)]),
     "lmmhip_get_saturated": (I, [P, ct.POINTER(ct.c_uint8)]),
@@ -412,11 +419,11 @@ class System:
             raise LmmError(lib().lmm_last_error().decode())
         return c
 
-    ENGINE_PERSISTENT, ENGINE_ROUNDS = 0, 1
+    ENGINE_PERSISTENT, ENGINE_ROUNDS, ENGINE_AUTO = 0, 1, 2
 
     def set_engine(self, engine):
         """Max-min engine of this system's device context (lmmhip_ctx_set_engine): ENGINE_PERSISTENT (one
-        launch per solve, default) or ENGINE_ROUNDS (one launch per phase per round)."""
+        launch per solve), ENGINE_ROUNDS (one launch per phase per round) or ENGINE_AUTO (default)."""
         _check_hip(lib().lmmhip_ctx_set_engine(self.device_ctx(), int(engine)))
 
     def device_values(self):

@@ -164,6 +164,71 @@ def device_solve_flat(f, kind, precision=None, device=None):
         L.lmmhip_ctx_destroy(ctx)
 
 
+class DeviceBatch:
+    """Independent max-min systems (a parameter sweep) as ONE block-diagonal device
+    system: their flattened systems concatenated, uploaded once (lmmhip_upload) and declared a batch
+    (lmmhip_set_batch), so every solve() runs one workgroup per system with the system in LDS
+    (lmm_batch_kernels.hpp).  Inputs stay resident in HBM across solves."""
+
+    def __init__(self, systems, precision=None, device=None):
+        import torch
+
+        L = lmm.lib()
+        self.L = L
+        self.prec = lmm.get_precision() if precision is None else precision
+        flats = [export_flat(s) for s in systems]
+        nvs = np.array([len(f.penalty) for f in flats], np.int64)
+        ncs = np.array([len(f.cbound) for f in flats], np.int64)
+        self.var_off = np.concatenate([[0], np.cumsum(nvs)]).astype(np.int64)
+        self.cnst_off = np.concatenate([[0], np.cumsum(ncs)]).astype(np.int64)
+        nnzs = np.array([len(f.cnst_idx) for f in flats], np.int64)
+        eoff = np.concatenate([[0], np.cumsum(nnzs)])
+        var_ptr = np.concatenate([f.var_ptr[:-1] + eoff[i] for i, f in enumerate(flats)] + [[eoff[-1]]]).astype(np.int64)
+        cnst_idx = np.concatenate([f.cnst_idx + self.cnst_off[i] for i, f in enumerate(flats)]).astype(np.int32)
+        cat = lambda name, dt: np.ascontiguousarray(np.concatenate([getattr(f, name) for f in flats]), dtype=dt)
+        self.arrays = (var_ptr, cnst_idx, cat("weight", np.float64), cat("penalty", np.float64),
+                       cat("vbound", np.float64), cat("cbound", np.float64), cat("cflags", np.uint8))
+        self.var_ids = [f.var_ids for f in flats]
+        self.n_var, self.n_cnst, self.nnz = int(self.var_off[-1]), int(self.cnst_off[-1]), int(len(cnst_idx))
+        self.ctx = ct.c_void_p()
+        dev = torch.cuda.current_device() if device is None else device
+        if L.lmmhip_ctx_create(dev, ct.byref(self.ctx)) != 0:
+            raise lmm.LmmError(L.lmmhip_last_error().decode())
+
+        def p(a, t):
+            return a.ctypes.data_as(ct.POINTER(t))
+
+        vp, ci, w, pen, vb, cb, cf = self.arrays
+        self._check(L.lmmhip_upload(self.ctx, self.n_var, self.n_cnst, self.nnz, p(vp, ct.c_int64),
+                                    p(ci, ct.c_int32), p(w, ct.c_double), p(pen, ct.c_double), p(vb, ct.c_double),
+                                    p(cb, ct.c_double), p(cf, ct.c_uint8)))
+        self._check(L.lmmhip_set_batch(self.ctx, len(flats), p(self.var_off, ct.c_int64),
+                                       p(self.cnst_off, ct.c_int64)))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise lmm.LmmError(self.L.lmmhip_last_error().decode())
+
+    def solve(self):
+        self._check(self.L.lmmhip_solve(self.ctx, 0, self.prec))
+
+    def stats(self):
+        st = lmm.LmmhipStats()
+        self._check(self.L.lmmhip_get_stats(self.ctx, ct.byref(st)))
+        return dict(rounds=st.rounds, device_ms=st.device_ms, n_var=st.n_var, n_cnst=st.n_cnst, nnz=st.nnz)
+
+    def values(self):
+        """Dense values of every system (concatenated, the systems' dense orders)."""
+        x = np.empty(self.n_var, np.float64)
+        self._check(self.L.lmmhip_get_values(self.ctx, x.ctypes.data_as(ct.POINTER(ct.c_double))))
+        return x
+
+    def close(self):
+        if self.ctx:
+            self.L.lmmhip_ctx_destroy(self.ctx)
+            self.ctx = None
+
+
 # ---- collectives ------------------------------------------------------------------------------
 
 class LocalExchange:
