@@ -7,12 +7,12 @@
 // workgroup stages one system's structure in LDS (16-bit local indices) and runs the same local-minimum
 // progressive filling as the global engines (lmm_maxmin_kernels.hpp; maxmin.cpp:509-680) with every round
 // inside the workgroup — no grid-wide synchronisation, no host round-trip:
-//   init     usage = sum / max of w/p over the constraint's elements, one wave per constraint, the same
-//            accumulation order as mm_init_cnsts (maxmin.cpp:520-555)
-//   round:   V  thread per variable: exact minimum ratio over its live constraints (ties: smallest id); a
-//               variable whose bound*penalty is below it is fixed at its bound (maxmin.cpp:563-595)
-//            R  thread per constraint: ready iff every live element votes for it (a local minimum)
-//            S  thread per variable voting for a ready constraint: x = ratio / penalty (maxmin.cpp:583);
+//   init     usage = sum / max of w/p over the constraint's elements, thread per constraint, sequential in
+//            CSC order like the reference's loop (maxmin.cpp:520-555)
+//   round:   V  kG lanes per variable: exact minimum ratio over its live constraints (ties: smallest id);
+//               a variable whose bound*penalty is below it is fixed at its bound (maxmin.cpp:563-595)
+//            R  kG lanes per constraint: ready iff every live element votes for it (a local minimum)
+//            S  kG lanes per variable voting for a ready constraint: x = ratio / penalty (maxmin.cpp:583);
 //               its decrements go to its other live constraints as fixed-point integers (LDS atomics)
 //            U  thread per constraint: the update of update_wave (clamps, FATPIPE recompute, saturation)
 // Decrements are fixed-point integers (CstRec): results do not depend on the order of the LDS atomics.
@@ -22,10 +22,11 @@
 namespace lmmdev {
 
 constexpr int kBB = 256;  // threads per workgroup
+constexpr int kG = 4;     // lanes per variable (vote, saturation) and per constraint (ready test)
 
 // LDS bytes of a workgroup for systems of at most nv variables, nc constraints and nnz elements
 __host__ __device__ inline size_t batch_lds_bytes(int nv, int nc, int nnz) {
-  size_t b = sizeof(double) * (4 * size_t(nc) + 3 * size_t(nv) + size_t(nnz)) +  // cnst / var state, w/p
+  size_t b = sizeof(double) * (4 * size_t(nc) + 3 * size_t(nv)) +                 // cnst / var state
              sizeof(unsigned long long) * 3 * size_t(nc) +                         // decrement records
              sizeof(int32_t) * size_t(nc) +                                        // scale exponents
              sizeof(uint16_t) * (size_t(nv) + 1 + size_t(nc) + 1 + 2 * size_t(nnz) + size_t(nv)) +
@@ -33,7 +34,7 @@ __host__ __device__ inline size_t batch_lds_bytes(int nv, int nc, int nnz) {
   return (b + 15) / 16 * 16;
 }
 
-__global__ void __launch_bounds__(kBB) mm_batch_lds(Dev s, const int64_t* __restrict__ var_off,
+__global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __restrict__ var_off,
                                                    const int64_t* __restrict__ cnst_off, int64_t nsys, double prec,
                                                    int max_nv, int max_nc, int max_nnz, int32_t* block_rounds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -44,8 +45,7 @@ __global__ void __launch_bounds__(kBB) mm_batch_lds(Dev s, const int64_t* __rest
   double* v_x = c_bnd + max_nc;
   double* v_pen = v_x + max_nv;
   double* v_vb = v_pen + max_nv;
-  double* l_u = v_vb + max_nv;  // [max_nnz] w/p of the CSC elements
-  unsigned long long* c_q = reinterpret_cast<unsigned long long*>(l_u + max_nnz);  // [3 * max_nc]
+  unsigned long long* c_q = reinterpret_cast<unsigned long long*>(v_vb + max_nv);  // [3 * max_nc]
   int32_t* c_exp = reinterpret_cast<int32_t*>(c_q + 3 * max_nc);
   uint16_t* l_vp = reinterpret_cast<uint16_t*>(c_exp + max_nc);  // [max_nv + 1] CSR offsets
   uint16_t* l_cp = l_vp + (max_nv + 1);                           // [max_nc + 1] CSC offsets
@@ -71,7 +71,6 @@ __global__ void __launch_bounds__(kBB) mm_batch_lds(Dev s, const int64_t* __rest
     for (int j = threadIdx.x; j < ne; j += kBB) {
       l_cc[j] = uint16_t(s.csr_c[eb + j] - cb);
       l_cv[j] = uint16_t(s.csc_v[kb + j] - vb);
-      l_u[j] = s.csc_u[kb + j];
     }
     for (int v = threadIdx.x; v < nv; v += kBB) {
       v_x[v] = 0.0;
@@ -80,93 +79,104 @@ __global__ void __launch_bounds__(kBB) mm_batch_lds(Dev s, const int64_t* __rest
       v_vb[v] = s.vbound[vb + v];
     }
     __syncthreads();
-    // ---- init: maxmin.cpp:520-555 (accumulation as init_cnsts_waves) ----
-    for (int c = wv; c < nc; c += kW) {
+    // ---- init: maxmin.cpp:520-555, thread per constraint: usage = sum (FATPIPE: max) of w/p over its
+    // elements in CSC order, one addition after the other like the reference's loop ----
+    for (int c = threadIdx.x; c < nc; c += kBB) {
       const int b = l_cp[c], e = l_cp[c + 1];
       const bool fat = s.cflags[cb + c] & 1;
       double acc = 0.0;
-      for (int j0 = b + lane; j0 < e; j0 += 4 * kWave) {
-        double u[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          u[k] = j0 + k * kWave < e ? l_u[j0 + k * kWave] : 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          acc = fat ? fmax(acc, u[k]) : acc + u[k];
+      for (int k = b; k < e; k++) {
+        const double u = s.csc_u[kb + k];
+        acc = fat ? fmax(acc, u) : acc + u;
       }
-      acc = fat ? wave_max(acc) : wave_sum(acc);
-      if (lane == 0) {
-        const double bound = s.cbound[cb + c];
-        const bool part = bound > bound * prec;
-        const double usage = part ? acc : 0.0;
-        const bool alive = part && usage > 0;
-        c_rem[c] = bound;
-        c_use[c] = usage;
-        c_bnd[c] = bound;
-        c_rat[c] = alive ? bound / usage : dinf();
-        c_exp[c] = alive ? int32_t((uint32_t(uint16_t(dec_scale(usage))) << 16) | uint16_t(dec_scale(bound))) : 0;
-        c_q[3 * c] = c_q[3 * c + 1] = c_q[3 * c + 2] = 0;
-        c_st[c] = alive ? 0 : 1;
-        c_fl[c] = fat;
-      }
+      const double bound = s.cbound[cb + c];
+      const bool part = bound > bound * prec;
+      const double usage = part ? acc : 0.0;
+      const bool alive = part && usage > 0;
+      c_rem[c] = bound;
+      c_use[c] = usage;
+      c_bnd[c] = bound;
+      c_rat[c] = alive ? bound / usage : dinf();
+      c_exp[c] = alive ? int32_t((uint32_t(uint16_t(dec_scale(usage))) << 16) | uint16_t(dec_scale(bound))) : 0;
+      c_q[3 * c] = c_q[3 * c + 1] = c_q[3 * c + 2] = 0;
+      c_st[c] = alive ? 0 : 1;
+      c_fl[c] = fat;
     }
     __syncthreads();
     int round = 0;
     for (;; round++) {
-      // ---- V: votes and bound fixes ----
-      for (int v = threadIdx.x; v < nv; v += kBB) {
-        if (v_st[v] != 0)
-          continue;
+      // ---- V: votes and bound fixes, G lanes per variable ----
+      for (int v = threadIdx.x / kG; v < nv; v += kBB / kG) {  // uniform within each G-lane group
+        const int g = threadIdx.x & (kG - 1);
+        const bool in = v_st[v] == 0;
         double minr = dinf();
         int t = 0xFFFF;
-        for (int j = l_vp[v]; j < l_vp[v + 1]; j++) {
+        const int jb = in ? l_vp[v] : 0, je = in ? l_vp[v + 1] : 0;
+        for (int j = jb + g; j < je; j += kG) {
           const int c = l_cc[j];
-          if (c_st[c] != 1) {
-            const double r = c_rat[c];
-            if (r < minr || (r == minr && c < t)) {
-              minr = r;
-              t = c;
-            }
+          const double r = c_rat[c];  // +inf once c left the light table
+          if (r < minr || (r == minr && c < t)) {
+            minr = r;
+            t = c;
           }
         }
+#pragma unroll
+        for (int o = 1; o < kG; o <<= 1) {  // (min ratio, smallest id) over the group
+          const double r2 = __shfl_xor(minr, o, kWave);
+          const int t2 = __shfl_xor(t, o, kWave);
+          if (r2 < minr || (r2 == minr && t2 < t)) {
+            minr = r2;
+            t = t2;
+          }
+        }
+        if (!in)
+          continue;
         const double vbd = v_vb[v], p = v_pen[v];
-        if (t == 0xFFFF) {  // every constraint of v left the light table: v stays at 0
-          v_st[v] = 1;
+        if (!(minr < dinf())) {  // every constraint of v left the light table: v stays at 0
+          if (g == 0)
+            v_st[v] = 1;
         } else if (vbd > 0 && vbd * p < minr) {  // maxmin.cpp:587-589
-          v_x[v] = vbd;
-          v_st[v] = 2;
-          for (int j = l_vp[v]; j < l_vp[v + 1]; j++) {
+          if (g == 0) {
+            v_x[v] = vbd;
+            v_st[v] = 2;
+          }
+          for (int j = jb + g; j < je; j += kG) {
             const int c = l_cc[j];
+            const double w = s.csr_w[eb + j];
             if (c_st[c] == 1)
               continue;
             atomicAdd(&c_q[3 * c + 2], 1ull);
             if (!c_fl[c]) {
-              const double w = s.csr_w[eb + j];
               atomicAdd(&c_q[3 * c], dec_q(w * vbd, cexp_rem(c_exp[c])));
               atomicAdd(&c_q[3 * c + 1], dec_q(w / p, cexp_use(c_exp[c])));
             }
           }
-        } else {
+        } else if (g == 0) {
           v_vote[v] = uint16_t(t);
         }
       }
       __syncthreads();
-      // ---- R: local minima ----
-      for (int c = threadIdx.x; c < nc; c += kBB) {
-        if (c_st[c] != 0)
-          continue;
+      // ---- R: local minima, G lanes per constraint ----
+      for (int c = threadIdx.x / kG; c < nc; c += kBB / kG) {
+        const int g = threadIdx.x & (kG - 1);
+        const bool in = c_st[c] == 0;
         bool rdy = true;
-        for (int k = l_cp[c]; k < l_cp[c + 1] && rdy; k++) {
-          const int v = l_cv[k];
-          const int st = v_st[v];
-          rdy = !(st == 2 || (st == 0 && v_vote[v] != c));
-        }
-        if (rdy)
+        if (in)
+          for (int k = l_cp[c] + g; k < l_cp[c + 1]; k += kG) {
+            const int v = l_cv[k];
+            const int st = v_st[v];
+            rdy &= !(st == 2 || (st == 0 && v_vote[v] != c));
+          }
+#pragma unroll
+        for (int o = 1; o < kG; o <<= 1)
+          rdy &= __shfl_xor(int(rdy), o, kWave) != 0;
+        if (in && rdy && g == 0)
           c_st[c] = 2;
       }
       __syncthreads();
-      // ---- S: saturation of the ready constraints' variables ----
-      for (int v = threadIdx.x; v < nv; v += kBB) {
+      // ---- S: saturation of the ready constraints' variables, G lanes per variable ----
+      for (int v = threadIdx.x / kG; v < nv; v += kBB / kG) {
+        const int g = threadIdx.x & (kG - 1);
         if (v_st[v] != 0)
           continue;
         const int t = v_vote[v];
@@ -174,15 +184,17 @@ __global__ void __launch_bounds__(kBB) mm_batch_lds(Dev s, const int64_t* __rest
           continue;
         const double p = v_pen[v];
         const double x = c_rat[t] / p;
-        v_x[v] = x;
-        v_st[v] = 3;
-        for (int j = l_vp[v]; j < l_vp[v + 1]; j++) {
+        if (g == 0) {
+          v_x[v] = x;
+          v_st[v] = 3;
+        }
+        for (int j = l_vp[v] + g; j < l_vp[v + 1]; j += kG) {
           const int c = l_cc[j];
+          const double w = s.csr_w[eb + j];
           if (c == t || c_st[c] == 1)
             continue;
           atomicAdd(&c_q[3 * c + 2], 1ull);
           if (!c_fl[c]) {
-            const double w = s.csr_w[eb + j];
             atomicAdd(&c_q[3 * c], dec_q(w * x, cexp_rem(c_exp[c])));
             atomicAdd(&c_q[3 * c + 1], dec_q(w / p, cexp_use(c_exp[c])));
           }
@@ -221,7 +233,7 @@ __global__ void __launch_bounds__(kBB) mm_batch_lds(Dev s, const int64_t* __rest
           use = 0.0;
           for (int k = l_cp[c]; k < l_cp[c + 1]; k++)
             if (!(v_x[l_cv[k]] > 0))
-              use = fmax(use, l_u[k]);
+              use = fmax(use, s.csc_u[kb + k]);
         }
         c_rem[c] = rem;
         c_use[c] = use;
