@@ -25,11 +25,27 @@ void lmm_set_precision(double precision);
 double lmm_get_precision(void);
 void lmm_set_default_concurrency_limit(int limit);
 
+/* --cfg-style configuration, "key:value" (sg_config.cpp:45 parses --cfg=key:value the same way):
+ *   maxmin/precision:<double>         sg_maxmin_precision (sg_config.cpp:261)
+ *   maxmin/concurrency-limit:<int>    sg_concurrency_limit (sg_config.cpp:264)
+ *   maxmin/solver:hip|hip-auto|hip-persistent|hip-rounds
+ *                                     the solver-selection flag the reference lacks: the
+ *                                     device engine of the systems created afterwards (lmmhip_ctx_set_engine);
+ *                                     this library has no CPU solver, so there is no "cpu" value
+ *   maxmin/resident:yes|no            new max-min systems start in resident mode (default yes)
+ * Returns 0, or -1 for an unknown key / bad value (message in lmm_last_error()).  lmm_config_get copies
+ * the current value into buf (cap bytes) and returns its length. */
+int lmm_config_set(const char* key_value);
+int lmm_config_get(const char* key, char* buf, int cap);
+
 /* make_new_maxmin_system (maxmin.cpp:25) / make_new_fair_bottleneck_system (fair_bottleneck.cpp:18) */
 lmm_sys* lmm_system_new(int selective_update, int kind /* 0 maxmin, 1 fair bottleneck */);
 void lmm_system_free(lmm_sys* s);
 
 int64_t lmm_constraint_new(lmm_sys* s, double bound);                                  /* maxmin.hpp:395 */
+/* The same with the opaque id the reference takes (Constraint::id_ = the Resource*, maxmin.hpp:395) */
+int64_t lmm_constraint_new_id(lmm_sys* s, void* id, double bound);
+void* lmm_constraint_get_id(lmm_sys* s, int64_t c);                                    /* :244 get_id */
 int lmm_constraint_unshare(lmm_sys* s, int64_t c);                                     /* :185 */
 int lmm_constraint_is_shared(lmm_sys* s, int64_t c);                                   /* :188 */
 int lmm_constraint_set_concurrency_limit(lmm_sys* s, int64_t c, int limit);            /* :195 */
@@ -45,6 +61,9 @@ int lmm_constraint_elements(lmm_sys* s, int64_t c, int* var_rank, double* weight
                             int cap);
 
 int64_t lmm_variable_new(lmm_sys* s, double penalty, double bound, int64_t n_cnst);   /* :404 */
+/* The same with the opaque id the reference takes (Variable::id_ = the Action*, maxmin.hpp:404) */
+int64_t lmm_variable_new_id(lmm_sys* s, void* id, double penalty, double bound, int64_t n_cnst);
+void* lmm_variable_get_id(lmm_sys* s, int64_t v);                                      /* :330 get_id */
 int lmm_variable_free(lmm_sys* s, int64_t v);                                         /* :411 */
 int lmm_variable_free_all(lmm_sys* s);                                                /* :414 */
 int lmm_variable_set_concurrency_share(lmm_sys* s, int64_t v, int share);             /* :305 */
@@ -57,6 +76,8 @@ int lmm_get_values(lmm_sys* s, const int64_t* vars, int64_t n, double* out);
 int lmm_system_variables(lmm_sys* s, int64_t* out, int cap);          /* variable_set order      */
 int lmm_system_active_constraints(lmm_sys* s, int64_t* out, int cap); /* active_constraint_set   */
 int lmm_modified_actions(lmm_sys* s, int64_t* out, int cap);          /* Action::ModifiedSet     */
+/* the same set as the variables' ids (the Action* the reference pushes, maxmin.cpp:536-538) */
+int lmm_modified_action_ids(lmm_sys* s, void** out, int cap);
 int lmm_clear_modified_actions(lmm_sys* s);
 
 int lmm_expand(lmm_sys* s, int64_t c, int64_t v, double w);                            /* :422 */

@@ -55,8 +55,6 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
   uint8_t* c_st = reinterpret_cast<uint8_t*>(v_vote + max_nv);    // 0 live, 1 out, 2 ready this round
   uint8_t* c_fl = c_st + max_nc;                                  // FATPIPE
   uint8_t* v_st = c_fl + max_nc;  // 0 live, 1 done, 2 fixed at its bound this round, 3 saturated this round
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  constexpr int kW = kBB / kWave;
   int rounds_max = 0;
   for (int64_t sy = blockIdx.x; sy < nsys; sy += gridDim.x) {
     const int64_t vb = var_off[sy], cb = cnst_off[sy];

@@ -66,6 +66,99 @@ lmm_sys* lmm_system_new(int selective, int kind) {
 }
 void lmm_system_free(lmm_sys* s) { delete s; }
 
+// --cfg-style configuration (sg_config.cpp:232-466 registers the reference's flags; "maxmin/solver"
+// and "maxmin/resident" are this build's own): "key:value", one per call.
+int lmm_config_set(const char* kv) {
+  try {
+    const std::string s(kv ? kv : "");
+    const size_t colon = s.find(':');
+    if (colon == std::string::npos)
+      throw std::invalid_argument("lmm_config_set: expected key:value, got '" + s + "'");
+    const std::string key = s.substr(0, colon), val = s.substr(colon + 1);
+    if (key == "maxmin/precision") {
+      simgrid_amd::lmm::maxmin_precision = std::stod(val);
+    } else if (key == "maxmin/concurrency-limit") {
+      simgrid_amd::lmm::concurrency_limit = std::stoi(val);
+    } else if (key == "maxmin/solver") {
+      // hip = hip-auto: the device engine chosen by size; hip-persistent / hip-rounds force one
+      if (val == "hip" || val == "hip-auto")
+        simgrid_amd::lmm::solver_engine = LMMHIP_ENGINE_AUTO;
+      else if (val == "hip-persistent")
+        simgrid_amd::lmm::solver_engine = LMMHIP_ENGINE_PERSISTENT;
+      else if (val == "hip-rounds")
+        simgrid_amd::lmm::solver_engine = LMMHIP_ENGINE_ROUNDS;
+      else
+        throw std::invalid_argument("maxmin/solver: hip, hip-auto, hip-persistent or hip-rounds (this build has no "
+                                    "CPU solver), got '" + val + "'");
+    } else if (key == "maxmin/resident") {
+      if (val == "yes" || val == "1" || val == "on")
+        simgrid_amd::lmm::resident_default = true;
+      else if (val == "no" || val == "0" || val == "off")
+        simgrid_amd::lmm::resident_default = false;
+      else
+        throw std::invalid_argument("maxmin/resident: yes or no, got '" + val + "'");
+    } else {
+      throw std::invalid_argument("lmm_config_set: unknown key '" + key + "'");
+    }
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int lmm_config_get(const char* key, char* buf, int cap) {
+  const std::string k(key ? key : "");
+  std::string v;
+  if (k == "maxmin/precision")
+    v = std::to_string(simgrid_amd::lmm::maxmin_precision);
+  else if (k == "maxmin/concurrency-limit")
+    v = std::to_string(simgrid_amd::lmm::concurrency_limit);
+  else if (k == "maxmin/solver")
+    v = simgrid_amd::lmm::solver_engine == LMMHIP_ENGINE_PERSISTENT ? "hip-persistent"
+        : simgrid_amd::lmm::solver_engine == LMMHIP_ENGINE_ROUNDS   ? "hip-rounds"
+                                                                    : "hip-auto";
+  else if (k == "maxmin/resident")
+    v = simgrid_amd::lmm::resident_default ? "yes" : "no";
+  else {
+    g_err = "lmm_config_get: unknown key '" + k + "'";
+    return -1;
+  }
+  if (buf && cap > 0) {
+    std::strncpy(buf, v.c_str(), size_t(cap) - 1);
+    buf[cap - 1] = 0;
+  }
+  return int(v.size());
+}
+
+int64_t lmm_constraint_new_id(lmm_sys* s, void* id, double bound) {
+  try {
+    return s->sys.constraint_new(id, bound);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int64_t lmm_variable_new_id(lmm_sys* s, void* id, double penalty, double bound, int64_t n_cnst) {
+  try {
+    return s->sys.variable_new(id, penalty, bound, size_t(n_cnst));
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+void* lmm_constraint_get_id(lmm_sys* s, int64_t c) { return s->sys.cnst(Id(c)).id; }
+void* lmm_variable_get_id(lmm_sys* s, int64_t v) { return s->sys.var(Id(v)).id; }
+
+int lmm_modified_action_ids(lmm_sys* s, void** out, int cap) {
+  auto& v = s->sys.modified_actions();
+  for (int i = 0; i < int(v.size()) && i < cap; i++)
+    out[i] = s->sys.var(Id(v[i])).id;
+  return int(v.size());
+}
+
 int64_t lmm_constraint_new(lmm_sys* s, double bound) {
   try {
     return s->sys.constraint_new(nullptr, bound);

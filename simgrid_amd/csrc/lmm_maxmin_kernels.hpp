@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int f
 // re-vote in LDS; each full queue of kBlock rows is then resolved one lane per row, with up to kReg
 // independent gathers in flight, so the rare slow rows no longer stall whole waves of fast ones.
 constexpr int kReg = 8;
-constexpr int kFilt = 4;  // rows per lane per filter step (their loads in flight together)
+constexpr int kFilt = 8;  // rows per lane per filter step (their loads in flight together)
 constexpr int kFlush = 4;  // filter rows between two queue flushes (queue capacity (kFlush + 1) x B)
 
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
@@ -454,7 +454,7 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
     unsigned kt[kFilt], sk[kFilt], cg[kFilt];
 #pragma unroll
     for (int u = 0; u < kFilt; u++)
-      sk[u] = (kBits ? tt[u] >= 0 : ch[u]) ? skey[base + u * B + threadIdx.x] : 1u;
+      sk[u] = base + u * B + threadIdx.x < hi ? skey[base + u * B + threadIdx.x] : 1u;  // streamed with rtgt
 #pragma unroll
     for (int u = 0; u < kFilt; u++) {  // target key (changed targets) / stamp (sensitive rows), together
       kt[u] = ch[u] ? key[tt[u]] : 0u;
@@ -914,9 +914,10 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   __syncthreads();
   int alive = 0;
   bool any_touch = false;
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
-       base += int64_t(gridDim.x) * kBlock)  // wave-uniform
-    alive += update_wave(s, base, round, prec, &any_touch);
+       base += 2 * stride)  // wave-uniform; two groups of 64 constraints per step, loads in flight together
+    alive += update_groups<2>(s, base, stride, round, prec, &any_touch);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();

@@ -25,6 +25,8 @@ namespace lmm {
 
 double maxmin_precision = 1e-5;
 int concurrency_limit = -1;
+int solver_engine = LMMHIP_ENGINE_AUTO;
+bool resident_default = true;
 
 [[noreturn]] void fatal(const std::string& msg) { throw std::runtime_error("lmm: " + msg); }
 
@@ -41,7 +43,12 @@ int CnstRec::slack() const {
   return conc_limit < 0 ? std::numeric_limits<int>::max() : conc_limit - conc_current;
 }
 
-System::System(bool selective_update, SolverKind kind) : selective_(selective_update), kind_(kind) {}
+// Max-min systems start in resident mode by default (HBM mirror + delta log + device flatten, §9 of
+// DESIGN.md): the host never walks the whole system per solve.  FairBottleneck systems keep the host
+// flatten, which hands the device each constraint's elements in the reference's list order
+// (flatten_fair): the bit-identical element-by-element remaining update needs it.
+System::System(bool selective_update, SolverKind kind)
+    : selective_(selective_update), kind_(kind), resident_(resident_default && kind == SolverKind::MAXMIN) {}
 
 System::~System() {
   if (ctx_)
@@ -53,6 +60,8 @@ lmmhip_ctx* System::ctx() {
     int rc = lmmhip_ctx_create(-1, &ctx_);
     if (rc)
       fatal(std::string("cannot create HIP context: ") + lmmhip_last_error());
+    if ((rc = lmmhip_ctx_set_engine(ctx_, solver_engine)))
+      fatal(std::string("cannot select the max-min engine: ") + lmmhip_last_error());
   }
   return ctx_;
 }

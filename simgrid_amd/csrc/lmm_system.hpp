@@ -24,6 +24,10 @@ namespace lmm {
 
 extern double maxmin_precision;  // sg_maxmin_precision, maxmin.cpp:12
 extern int concurrency_limit;    // sg_concurrency_limit, maxmin.cpp:14
+// solver selection (lmm_config_set "maxmin/solver", "maxmin/resident"): the engine of every new device
+// context (LMMHIP_ENGINE_*) and whether new max-min systems start in resident mode
+extern int solver_engine;
+extern bool resident_default;
 
 enum class SharingPolicy : int { FATPIPE = 0, SHARED = 1 };  // s4u::Link::SharingPolicy subset
 enum class SolverKind : int { MAXMIN = 0, FAIR_BOTTLENECK = 1 };

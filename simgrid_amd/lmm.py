@@ -48,6 +48,13 @@ SIGNATURES = {
     "lmm_set_precision": (None, [D]),
     "lmm_get_precision": (D, []),
     "lmm_set_default_concurrency_limit": (None, [I]),
+    "lmm_config_set": (I, [ct.c_char_p]),
+    "lmm_config_get": (I, [ct.c_char_p, ct.c_char_p, I]),
+    "lmm_constraint_new_id": (I64, [P, P, D]),
+    "lmm_variable_new_id": (I64, [P, P, D, D, I64]),
+    "lmm_constraint_get_id": (P, [P, I64]),
+    "lmm_variable_get_id": (P, [P, I64]),
+    "lmm_modified_action_ids": (I, [P, ct.POINTER(P), I]),
     "lmm_system_new": (P, [I, I]),
     "lmm_system_free": (None, [P]),
     "lmm_constraint_new": (I64, [P, D]),
@@ -201,6 +208,19 @@ def get_precision():
     return lib().lmm_get_precision()
 
 
+def config_set(key_value):
+    """--cfg-style "key:value" (lmm_config_set): maxmin/precision, maxmin/concurrency-limit,
+    maxmin/solver (hip, hip-auto, hip-persistent, hip-rounds), maxmin/resident (yes, no)."""
+    _check(lib().lmm_config_set(key_value.encode()))
+
+
+def config_get(key):
+    buf = ct.create_string_buffer(64)
+    if lib().lmm_config_get(key.encode(), buf, 64) < 0:
+        raise LmmError(lib().lmm_last_error().decode())
+    return buf.value.decode()
+
+
 def device_count():
     return lib().lmm_device_count()
 
@@ -250,6 +270,9 @@ class Constraint:
     def get_bound(self):
         return lib().lmm_constraint_get_bound(self.sys.h, self.h)
 
+    def get_id(self):
+        return lib().lmm_constraint_get_id(self.sys.h, self.h)
+
     @property
     def rank(self):
         return lib().lmm_constraint_rank(self.sys.h, self.h)
@@ -276,6 +299,9 @@ class Variable:
 
     def get_penalty(self):
         return lib().lmm_variable_get_penalty(self.sys.h, self.h)
+
+    def get_id(self):
+        return lib().lmm_variable_get_id(self.sys.h, self.h)
 
     def set_concurrency_share(self, s):
         _check(lib().lmm_variable_set_concurrency_share(self.sys.h, self.h, s))
@@ -304,13 +330,15 @@ class System:
             self.h = None
 
     def constraint_new(self, id_, bound):
-        h = lib().lmm_constraint_new(self.h, bound)
+        h = lib().lmm_constraint_new_id(self.h, id_, bound) if isinstance(id_, int) else \
+            lib().lmm_constraint_new(self.h, bound)
         if h < 0:
             raise LmmError(lib().lmm_last_error().decode())
         return Constraint(self, h)
 
     def variable_new(self, id_, penalty, bound=-1.0, number_of_constraints=1):
-        h = lib().lmm_variable_new(self.h, penalty, bound, number_of_constraints)
+        h = lib().lmm_variable_new_id(self.h, id_, penalty, bound, number_of_constraints) if isinstance(id_, int) \
+            else lib().lmm_variable_new(self.h, penalty, bound, number_of_constraints)
         if h < 0:
             raise LmmError(lib().lmm_last_error().decode())
         return Variable(self, h)
@@ -519,6 +547,13 @@ class System:
         arr = (I64 * n)()
         lib().lmm_system_active_constraints(self.h, arr, n)
         return [Constraint(self, arr[i]) for i in range(n)]
+
+    def modified_action_ids(self):
+        """The opaque ids (Action*) of the modified set, in modified_actions() order."""
+        n = lib().lmm_modified_action_ids(self.h, None, 0)
+        arr = (P * n)()
+        lib().lmm_modified_action_ids(self.h, arr, n)
+        return [arr[i] for i in range(n)]
 
     def modified_actions(self):
         n = lib().lmm_modified_actions(self.h, None, 0)

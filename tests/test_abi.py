@@ -44,3 +44,23 @@ def test_solve_without_gpu_fails_loudly():
     s.expand(c, v, 1.0)
     with pytest.raises(L.LmmError, match="no HIP device"):
         s.solve()
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+C_DRIVE = os.path.join(ROOT, "tests", "c", "abi_drive")
+
+
+def build_c_drive():
+    """Compile tests/c/abi_drive.c (plain C, gcc) against include/lmm/*.h and link liblmm_amd.so."""
+    import subprocess
+
+    lib_dir = os.path.dirname(L.LIB_PATH)
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "abi_drive.c"), "-o", C_DRIVE, "-L", lib_dir, "-llmm_amd",
+                           "-Wl,-rpath," + lib_dir, "-lm"])
+    return C_DRIVE
+
+
+def test_c_client_compiles_against_the_headers():
+    """The boundary is a C ABI: a C99 program includes both headers and links the library."""
+    assert os.path.exists(build_c_drive())

@@ -270,3 +270,15 @@ def test_synthetic_certificate_matches_oracle_certificate(variant):
     ps.solve()
     excess, n_inf, n_unb = ps.check_certificate()
     assert n_inf == 0 and n_unb == 0, (excess, n_inf, n_unb)
+
+
+def test_c_client_drives_a_solve():
+    """tests/c/abi_drive.c: a plain C client of include/lmm/lmm_system.h + lmm_hip.h solves the
+    maxmin_test.cpp:17-42 system and the exec-ptask L07 system on the device."""
+    import subprocess
+
+    from tests.test_abi import build_c_drive
+
+    r = subprocess.run([build_c_drive()], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "abi_drive: ok" in r.stdout

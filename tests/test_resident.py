@@ -113,6 +113,9 @@ def step_ops(rng, cs, vs, next_var, n_new=8, n_free=6, n_pen=6, n_bound=6, max_e
 
 def test_resident_flag_and_full_pending():
     s = L.System(False)
+    assert s.resident()  # max-min systems start resident (maxmin/resident:yes)
+    assert not L.System(False, L.System.FAIR_BOTTLENECK).resident()  # FairBottleneck keeps the host flatten
+    s.set_resident(False)
     assert not s.resident()
     s.set_resident(True)
     assert s.resident()
@@ -167,3 +170,37 @@ def test_staging_moves_are_logged():
     s.variable_free(vs[0])  # frees a slot: a staged variable gets enabled
     sh.apply(s.drain_deltas())
     assert_same_device_view(sh, full_dump(s))
+
+
+def test_config_flags():
+    """--cfg-style flags (lmm_config_set): the solver selector the reference lacks, resident default."""
+    assert L.config_get("maxmin/solver") == "hip-auto"
+    L.config_set("maxmin/solver:hip-rounds")
+    assert L.config_get("maxmin/solver") == "hip-rounds"
+    L.config_set("maxmin/solver:hip")
+    assert L.config_get("maxmin/solver") == "hip-auto"
+    with pytest.raises(L.LmmError, match="no CPU solver"):
+        L.config_set("maxmin/solver:cpu")
+    with pytest.raises(L.LmmError, match="unknown key"):
+        L.config_set("maxmin/nope:1")
+    L.config_set("maxmin/resident:no")
+    try:
+        assert not L.System(False).resident()
+    finally:
+        L.config_set("maxmin/resident:yes")
+    assert L.System(False).resident()
+    L.config_set("maxmin/precision:1e-6")
+    assert L.get_precision() == 1e-6
+    L.config_set("maxmin/precision:1e-5")
+
+
+def test_opaque_ids():
+    """Constraint / Variable ids (maxmin.hpp:395, :404): borrowed Resource* / Action* handed back by
+    get_id() and by the modified set (maxmin.cpp:536-538)."""
+    s = L.System(True)
+    c = s.constraint_new(0x1000, 3.0)
+    v = s.variable_new(0x2000, 1.0, -1.0, 1)
+    w = s.variable_new(None, 1.0, -1.0, 1)
+    s.expand(c, v, 1.0)
+    s.expand(c, w, 1.0)
+    assert c.get_id() == 0x1000 and v.get_id() == 0x2000 and w.get_id() is None
