@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_ready", 4: "mm_saturate",
-              5: "mm_update", 6: "compaction"}
+              5: "mm_update", 6: "compaction", 7: "vote_diag"}
 # rocprofv3 kernel names (profiles/*_traffic.json keys) behind each launch slot
 SLOT_KERNELS = {"mm_vote": ("mm_vote_lane", "mm_vote"), "mm_saturate": ("mm_saturate",),
                 "mm_update": ("mm_update",), "mm_ready": ("mm_ready",), "compaction": ("cmp_write",),
@@ -35,6 +35,31 @@ TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def host_info():
+    """CPU model and core counts of the box the CPU baseline ran on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity}
+
+
+def mean_sd(xs):
+    import numpy as np
+
+    a = np.asarray(xs, dtype=np.float64)
+    return float(a.mean()), float(a.std(ddof=1)) if len(a) > 1 else 0.0
 
 
 def kernel_bytes(slot, nV, nC, av, ae, fv, fe, rv, re_):
@@ -74,7 +99,16 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2 = the BASELINE metric's config (default); c3/c4/c5 = the other SURVEY.md §8(d) configs")
     ap.add_argument("--flows", type=int, default=None, help="c4/c5: number of flows (default 1e5 / 1e7)")
+    ap.add_argument("--variant", default="plain", choices=["plain", "stress"],
+                    help="c2: stress = 5%% FATPIPE constraints, 10%% bounded variables, penalties {1,2,4}")
+    ap.add_argument("--dropin-steps", type=int, default=3,
+                    help="c2: System::solve() steps through the public API after the timed region (0 = skip)")
+    ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline repetitions (mean and sd reported)")
+    ap.add_argument("--cpu-worker", nargs=3, metavar=("WORKLOAD", "LO", "HI"), default=None,
+                    help=argparse.SUPPRESS)  # child process of the N-process CPU baseline
     args = ap.parse_args()
+    if args.cpu_worker:
+        return cpu_worker(*args.cpu_worker)
     if args.workload != "c2":
         return run_config(args)
 
@@ -102,7 +136,8 @@ def main():
     # ---- construction (not timed) ----
     t = time.time()
     s = lmm.System(False)
-    s.gen_synthetic(args.cnst, args.vars, args.k, seed=rank + 1, want_vars=False)
+    gen_kw = STRESS_KW if args.variant == "stress" else {}
+    vs = s.gen_synthetic(args.cnst, args.vars, args.k, seed=rank + 1, want_vars=args.dropin_steps > 0, **gen_kw)
     t_gen = time.time() - t
     t = time.time()
     s.prepare()  # flatten + upload: inputs resident in HBM from here on
@@ -175,19 +210,51 @@ def main():
                            device_ms=st["device_ms"], launch_slot=slot.tolist(), launch_round=rnd.tolist(),
                            launch_ms=ms.tolist()), f)
 
+    # ---- drop-in step: System::solve() through the public API after simulation-side mutations ----
+    # Each step first changes 1e4 variable penalties and 1e3 constraint bounds through the API (untimed: the
+    # simulation's own work), then times solve() = delta-log ship + device flatten or refresh + device solve
+    # + value scatter into the host System (resident mode, the default).
+    dropin = None
+    if args.dropin_steps > 0:
+        rng = np.random.default_rng(9 + rank)
+        rows = []
+        for _ in range(args.dropin_steps):
+            for i in rng.choice(args.vars, 10_000, replace=False):
+                s.update_variable_penalty(lmm.Variable(s, int(vs[i])), float(rng.choice([0.5, 1.0, 2.0])))
+            for c in rng.choice(args.cnst, 1_000, replace=False):
+                s.update_constraint_bound(lmm.Constraint(s, int(c)), float(rng.uniform(0.5, 10.0)))
+            t1 = time.perf_counter()
+            s.solve()
+            wall = (time.perf_counter() - t1) * 1e3
+            st2 = s.last_stats()
+            rows.append((wall, st2["flatten_ms"], st2["upload_ms"], st2["device_ms"], st2["fetch_ms"]))
+        med = np.median(np.array(rows), axis=0)
+        dropin = {"solve_step_ms": round(float(med[0]), 2), "host_ms": round(float(med[1]), 2),
+                  "ship_and_device_flatten_ms": round(float(med[2]), 2), "device_solve_ms": round(float(med[3]), 2),
+                  "value_scatter_ms": round(float(med[4]), 2), "steps": args.dropin_steps,
+                  "vars_per_s": round(args.vars / (float(med[0]) * 1e-3), 1),
+                  "mutations_per_step": "1e4 penalty + 1e3 constraint-bound updates (untimed)",
+                  "path": "System::solve(), resident mode (default): median over the steps"}
+
     # ---- CPU baseline: the oracle (single-threaded restatement), bounded sample, rank 0, N=1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import pyoracle as O
 
         div = args.cpu_sample_div
-        o = O.System(False)
-        o.gen_synthetic(args.cnst // div, args.vars // div, args.k, seed=1, want_vars=False)
-        tcpu = o.timed_solve()
-        cpu = {"value": round((args.vars // div) / tcpu, 1), "unit": "vars/s", "cores": 1, "kind": "port",
+        times, rounds = [], 0
+        for _ in range(max(1, args.cpu_reps)):  # a fresh system per repetition (solve() runs once per change)
+            o = O.System(False)
+            o.gen_synthetic(args.cnst // div, args.vars // div, args.k, seed=1, want_vars=False, **gen_kw)
+            times.append(o.timed_solve())
+            rounds = o.last_rounds
+            del o
+        m, sd = mean_sd(times)
+        cpu = {"value": round((args.vars // div) / m, 1), "unit": "vars/s", "cores": 1, "kind": "port",
                "sample": f"same generator at 1/{div} scale ({args.cnst // div} cnst x {args.vars // div} vars x {args.k}),"
-                         f" one solve() timed with steady_clock: {tcpu:.2f} s, {o.last_rounds} sequential rounds"}
-        del o
+                         f" solve() timed with steady_clock, {len(times)} reps: {m:.3f} +- {sd:.3f} s,"
+                         f" {rounds} sequential rounds",
+               "reps": len(times), "solve_s_mean": round(m, 4), "solve_s_sd": round(sd, 4), **host_info()}
 
     if rank == 0:
         out = {
@@ -195,9 +262,12 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (maxmin_bench-style generator, splitmix64 seed = rank+1)",
-            "config": {"workload": "C2: 1e6 constraints x 1e7 variables x 8 elements/var, one lmm_solve per step",
-                       "nb_cnst": args.cnst, "nb_var": args.vars, "elems_per_var": args.k,
+            "config": {"workload": "C2: 1e6 constraints x 1e7 variables x 8 elements/var, one lmm_solve per step"
+                                   + (" (stress variant: 5% FATPIPE, 10% bounded, penalties {1,2,4})"
+                                      if args.variant == "stress" else ""),
+                       "nb_cnst": args.cnst, "nb_var": args.vars, "elems_per_var": args.k, "variant": args.variant,
                        "active_vars": nV, "active_cnsts": nC, "nnz": nnz, "device_rounds": rounds,
+                       "device_solve_ms": round(ms_per_step, 3), "dropin_step": dropin,
                        "parallelism": f"replicas x{world} (independent systems per rank)"},
             "roofline": roofline, "cpu_baseline": cpu,
         }
@@ -210,35 +280,92 @@ C4_PLATFORM = dict(topology=0, topo_parameters="3;16,16,16;1,16,16;1,1,1", loopb
 C5_PLATFORM = dict(topology=1, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8)  # DRAGONFLY
 
 
-def config_cpu_baseline(workload, flows):
-    """The oracle (single-threaded restatement of maxmin.cpp / fair_bottleneck.cpp) on a bounded sample of
-    the same workload, rank 0, N=1: C3 solves its 4096 medium systems one lmm_solve each (the reference
-    solves independent systems one by one), C4 the same 1e5-flow fat-tree system, C5 the same dragonfly
-    generator at 1e6 flows (1/10 of the GPU workload)."""
+STRESS_KW = dict(penalty_mix=1, bounded_permille=100, fatpipe_permille=50)  # C2 stress variant (generator knobs)
+C3_SYSTEMS = 4096
+
+
+def c3_cpu_slice(lo, hi):
+    """Σ solve() seconds and sequential rounds of medium systems lo..hi-1 on the oracle (one core)."""
     from oracle import pyoracle as O
 
-    if workload == "c3":
-        tcpu, rounds = 0.0, 0
-        for i in range(4096):
-            o = O.System(False)
-            o.gen_maxmin_bench(1, i)
-            tcpu += o.timed_solve()
-            rounds += o.last_rounds
-        return {"value": round(100 * 4096 / tcpu, 1), "unit": "vars/s", "cores": 1, "kind": "port",
-                "sample": f"the same 4096 medium systems, one solve() each timed with steady_clock: {tcpu:.3f} s in"
-                          f" total, {rounds} sequential rounds"}
-    if workload == "c4":
-        n = flows or 100_000
+    tcpu, rounds = 0.0, 0
+    for i in range(lo, hi):
         o = O.System(False)
-        o.gen_platform_flows(O.platform_params(model=O.LV08, n_flows=n, seed=1, **C4_PLATFORM))
-    else:
-        n = min(flows or 10_000_000, 1_000_000)
-        o = O.System(False, O.System.FAIR_BOTTLENECK)
-        o.gen_platform_flows(O.platform_params(model=O.L07, n_flows=n, seed=1, **C5_PLATFORM))
-    tcpu = o.timed_solve()
-    return {"value": round(n / tcpu, 1), "unit": "vars/s", "cores": 1, "kind": "port",
-            "sample": f"same generator, {n} flows, one solve() timed with steady_clock: {tcpu:.2f} s,"
-                      f" {o.last_rounds} sequential rounds"}
+        o.gen_maxmin_bench(1, i)
+        tcpu += o.timed_solve()
+        rounds += o.last_rounds
+    return tcpu, rounds
+
+
+def cpu_worker(workload, lo, hi):
+    """Child process of the N-process CPU baseline: prints its slice's Σ solve() seconds."""
+    assert workload == "c3"
+    tcpu, rounds = c3_cpu_slice(int(lo), int(hi))
+    print(json.dumps({"solve_s": tcpu, "rounds": rounds}), flush=True)
+
+
+def c3_cpu_processes(nproc):
+    """the 4096 systems split over `nproc` processes (one per host core), each solving its
+    contiguous slice; throughput = Σ variables / the slowest process's Σ solve() time.  Processes are
+    children started with subprocess (nothing forks or execs the GPU-initialised parent)."""
+    import subprocess
+
+    cuts = [C3_SYSTEMS * k // nproc for k in range(nproc + 1)]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", "c3", str(cuts[k]),
+                               str(cuts[k + 1])], stdout=subprocess.PIPE, text=True) for k in range(nproc)]
+    t0 = time.perf_counter()
+    res = []
+    for p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"CPU baseline worker failed (rc {p.returncode})")
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    wall = time.perf_counter() - t0
+    slowest = max(r["solve_s"] for r in res)
+    return {"value": round(100 * C3_SYSTEMS / slowest, 1), "unit": "vars/s", "cores": nproc,
+            "slowest_process_solve_s": round(slowest, 4), "wall_s_incl_generation": round(wall, 2)}
+
+
+def config_cpu_baseline(workload, flows, reps=3):
+    """The oracle (single-threaded restatement of maxmin.cpp / fair_bottleneck.cpp) on a bounded sample of
+    the same workload, rank 0, N=1, `reps` repetitions (mean and sd): C3 solves its 4096 medium systems
+    one lmm_solve each (the reference solves independent systems one by one), plus the N-process leg of
+    BASELINE.md §2; C4 the same 1e5-flow fat-tree system; C5 the same dragonfly generator at 1e6 flows (1/10
+    of the GPU workload)."""
+    from oracle import pyoracle as O
+
+    reps = max(1, reps)
+    if workload == "c3":
+        times = []
+        for _ in range(reps):
+            tcpu, rounds = c3_cpu_slice(0, C3_SYSTEMS)
+            times.append(tcpu)
+        m, sd = mean_sd(times)
+        hi = host_info()
+        nproc = max(1, min(16, hi["affinity_cpus"] or 1))  # the box's CPU share is 16 cores per GPU
+        return {"value": round(100 * C3_SYSTEMS / m, 1), "unit": "vars/s", "cores": 1, "kind": "port",
+                "sample": f"the same 4096 medium systems, one solve() each timed with steady_clock, {reps} reps:"
+                          f" {m:.4f} +- {sd:.4f} s in total, {rounds} sequential rounds",
+                "reps": reps, "solve_s_mean": round(m, 5), "solve_s_sd": round(sd, 5),
+                "n_process": c3_cpu_processes(nproc), **hi}
+    times = []
+    for _ in range(reps):  # a fresh system per repetition (solve() runs once per change)
+        if workload == "c4":
+            n = flows or 100_000
+            o = O.System(False)
+            o.gen_platform_flows(O.platform_params(model=O.LV08, n_flows=n, seed=1, **C4_PLATFORM))
+        else:
+            n = min(flows or 10_000_000, 1_000_000)
+            o = O.System(False, O.System.FAIR_BOTTLENECK)
+            o.gen_platform_flows(O.platform_params(model=O.L07, n_flows=n, seed=1, **C5_PLATFORM))
+        times.append(o.timed_solve())
+        rounds = o.last_rounds
+        del o
+    m, sd = mean_sd(times)
+    return {"value": round(n / m, 1), "unit": "vars/s", "cores": 1, "kind": "port",
+            "sample": f"same generator, {n} flows, solve() timed with steady_clock, {reps} reps: {m:.3f} +- {sd:.3f} s,"
+                      f" {rounds} sequential rounds",
+            "reps": reps, "solve_s_mean": round(m, 4), "solve_s_sd": round(sd, 4), **host_info()}
 
 
 def run_config(args):
@@ -368,7 +495,7 @@ def run_config(args):
                            launch_round=rnd.tolist(), launch_ms=ms.tolist()), f)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = config_cpu_baseline(args.workload, args.flows)
+        cpu = config_cpu_baseline(args.workload, args.flows, args.cpu_reps)
     if rank == 0:
         desc.update(active_vars=int(tot[0]), nnz=int(tot[1]), device_rounds=int(rounds))
         print(json.dumps({

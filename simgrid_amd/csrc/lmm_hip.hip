@@ -87,6 +87,7 @@ struct lmmhip_ctx {
   // maxmin engine (lmmhip_ctx_set_engine): one persistent launch per solve (default) or the
   // multi-launch round chain; grid-barrier words of the persistent launch
   int engine = LMMHIP_ENGINE_AUTO;
+  bool vote_diag = std::getenv("LMMHIP_VOTE_DIAG") != nullptr;  // profiling: diagnostic vote launches
   unsigned* pbar = nullptr;
   bool persist_prof = false;    // record barrier timestamps in the persistent launch
   long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
@@ -1104,6 +1105,10 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   case 4:
   case 8:  // short rows: one lane per row (more gathers in flight per wave)
     if (int64_t(d.nC) <= int64_t(kBitWords) * 64) {
+      if (c->profiling && c->vote_diag) {  // measurement: bitmap load alone, filter alone (slot 7)
+        LAUNCH(7, r + 1000000, (mm_vote_lane<kVBlock, true, 2>), c->n_cu, kVBlock, d, buf, int(r));
+        LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, buf, int(r));
+      }
       LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, buf, int(r));
     } else {
       LAUNCH(2, r, (mm_vote_lane<kBlock, false>), grid, kBlock, d, buf, int(r));

@@ -406,7 +406,9 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 // targets.  One 1024-thread block per CU (the bitmap takes up to kBitWords * 8 B of LDS).
 constexpr int kVBlock = 1024;
 constexpr int kBitWords = 17408;  // LDS bitmap capacity: 1,114,112 constraints
-template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int buf, int round) {
+// kDiag (measurement only, LMMHIP_VOTE_DIAG): 1 = the filter pass alone (rows queued, none resolved, no
+// global writes), 2 = the bitmap load alone.
+template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int buf, int round) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ int st_rows, st_elems;
@@ -423,6 +425,11 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
       dst[i] = src[i];
   }
   __syncthreads();
+  if (kDiag == 2) {
+    if (threadIdx.x == 0 && bits[1] == 0x5a5a5a5a5a5a5a5aull)  // keeps the load
+      s.ctl[CTL_WORDS - 1] = 1;
+    return;
+  }
   const int64_t nrows = s.ctl[CTL_NROWS + buf];
   const int32_t* __restrict__ rtgt = s.rtgt[buf];
   const uint16_t* __restrict__ skey = s.skey[buf];
@@ -481,7 +488,8 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
         __syncthreads();
         int n = qn;
         while (n >= B) {  // resolve full queues: the last B entries each time
-          vote_row(s, buf, round, lo + q[n - B + threadIdx.x], &st_rows, &st_elems);
+          if (kDiag == 0)
+            vote_row(s, buf, round, lo + q[n - B + threadIdx.x], &st_rows, &st_elems);
           n -= B;
         }
         __syncthreads();
@@ -492,6 +500,11 @@ template <int B, bool kBits> __global__ void __launch_bounds__(B) mm_vote_lane(D
     }
   }
   const int n = qn;
+  if (kDiag) {
+    if (threadIdx.x == 0 && n == -7)  // keeps the filter
+      s.ctl[CTL_WORDS - 1] = 1;
+    return;
+  }
   if (threadIdx.x < n)
     vote_row(s, buf, round, lo + q[threadIdx.x], &st_rows, &st_elems);
   if (s.vstat) {
