@@ -70,13 +70,13 @@ def kernel_bytes(slot, nV, nC, av, ae, fv, fe, rv, re_):
         #            per re-evaluated row cvar 4 + vstate 4 + crow 8 + vbound 8 + pen 8 + rtgt/skey 6;
         #            per re-evaluated element ccol 4 + key 2
         return av * 8 + rv * 38 + re_ * 6
-    if slot == 3:  # mm_ready: key 2 + votes 4 + acnt 4 per constraint
+    if slot == 3:  # mm_ready: list entry 4 + key 2 + nvote 4 per alive constraint
         return nC * 10
     if slot == 4:  # mm_saturate: per fixed var csc idx 4 + vstate 4 + pen 8 + x 8 + row ptr 8;
-        #            per fixed element csr idx 4 + w 8 + key 2 + cflags 1 + atomics dcnt 4, drem 8, duse 8
-        return fv * 32 + fe * 35
-    if slot == 5:  # mm_update: key 2 + dcnt 4 per constraint; per touched constraint ~56 B of state
-        return nC * 6 + min(fe, nC) * 56
+        #            per fixed element csr idx 4 + w 8 + key 2 + cflags 1 + touch 1 + atomics dcnt 4, drem 8, duse 8
+        return fv * 32 + fe * 36
+    if slot == 5:  # mm_update: key 2 + touch flag 1 per constraint; per touched constraint ~56 B of state
+        return nC * 3 + min(fe, nC) * 56
     if slot == 0:  # mm_init_cnsts: CSC idx 4 + w 8 + pen gather 8 per element; bound 8 + state writes 48 per constraint
         return 20 * ae + 56 * nC
     if slot == 1:
@@ -204,8 +204,11 @@ def main():
                 "solve_alg_bytes": int(solve_alg),
                 "solve_frac": round(solve_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
     if args.profile_json and rank == 0:
+        extra = {}
+        if os.environ.get("LMMHIP_VOTE_DIAG"):
+            extra["vote_diag"] = s.vote_diag_profile().tolist()
         with open(args.profile_json, "w") as f:
-            json.dump(dict(per_kernel=per_kernel, rounds=rounds, alive_vars=av.tolist(), alive_elems=ae.tolist(),
+            json.dump(dict(per_kernel=per_kernel, rounds=rounds, alive_vars=av.tolist(), alive_elems=ae.tolist(), **extra,
                            reeval_vars=rv.tolist(), reeval_elems=re_.tolist(),
                            device_ms=st["device_ms"], launch_slot=slot.tolist(), launch_round=rnd.tolist(),
                            launch_ms=ms.tolist()), f)

@@ -48,7 +48,7 @@ enum : int {
 struct alignas(64) CstRec {
   unsigned long long drem, duse, dcnt;  // fixed-point decrements pushed this round; dcnt = fixed elements
                                         // (dcnt > 0: touched this round)
-  int64_t pad;              // round + 1 in which mm_saturate saturated the constraint (0 = never)
+  int64_t pad;              // unused (keeps the record one 64-B line)
   double rem, use;          // remaining, usage (maxmin.cpp:520-535, 603-658)
   double ratio;             // rem / use; +inf when out of the light table
   double bound;             // constraint bound
@@ -97,6 +97,10 @@ struct Dev {
   const double* vbound;      // [nV]
   const double* cbound;      // [nC]
   const uint8_t* cflags;     // [nC] bit0 FATPIPE, bit1 zero-weight enabled element
+  // [nC] 1 = some variable has two elements on the constraint (expand() without expand_add; set at upload by
+  // mm_dup_check): its saturation claims variables with atomicCAS.  Elsewhere a plain store claims — ready
+  // constraints share no alive variable, so only a duplicate inside one constraint could claim twice.
+  uint8_t* cdup;
   // per-variable state
   double* x;        // [nV] values (output)
   int32_t* fixr;    // [nV] fair bottleneck: last round the variable was listed (measurement only)
@@ -114,10 +118,11 @@ struct Dev {
   // for every alive constraint each round); ready iff 0.  Vote moves add/subtract the moving
   // variable's multiplicity, fixed elements leave through the record's count in mm_update.
   int32_t* nvote;
+  uint8_t* ctouch;  // [nC] maxmin, this round: 1 = received decrements, 2 = saturated (mm_update resets it)
   uint16_t* chg;    // [nC] last round (mod 2^16) in which ratio / liveness changed
-  uint64_t* chgbits;  // [nC/64 + 2] bitmap: constraints changed in the last round (written by mm_update)
   int32_t* ready;   // [nC + slack] ready constraints, one segment per mm_ready block
   int32_t* bready;  // [kMaxBlocks] ready count of each segment
+  uint64_t* chgbits;  // [nC/64 + 2] bitmap: constraints changed in the last round (written by mm_update)
   int32_t* balive;  // [kMaxBlocks] constraints still alive after mm_update, per block
   int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
   int32_t* clist[2];  // [nC] alive-constraint lists (periodically compacted)

@@ -70,7 +70,6 @@ struct lmmhip_ctx {
   bool uploaded = false;
   bool profiling = false;
   int group = 8;  // lanes per row in mm_vote (power of two >= mean row length, <= 64)
-  int sat_waves = 1;  // waves per ready constraint in mm_saturate (mean 64-element CSC chunks, 1/2/4)
   int n_cu = 256;  // compute units (grid of the one-block-per-CU kernels)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // per-launch event pairs (profiling mode): recorded without synchronising, resolved after the
@@ -87,6 +86,7 @@ struct lmmhip_ctx {
   // maxmin engine (lmmhip_ctx_set_engine): one persistent launch per solve (default) or the
   // multi-launch round chain; grid-barrier words of the persistent launch
   int engine = LMMHIP_ENGINE_AUTO;
+  int sat_waves = 1;  // waves per ready constraint in mm_saturate (mean 64-element CSC chunks, 1/2/4)
   bool vote_diag = std::getenv("LMMHIP_VOTE_DIAG") != nullptr;  // profiling: diagnostic vote launches
   unsigned* pbar = nullptr;
   bool persist_prof = false;    // record barrier timestamps in the persistent launch
@@ -119,7 +119,7 @@ struct lmmhip_ctx {
   int64_t res_nE = 0, res_nV = 0, res_nC = 0;  // host table sizes of the last delta batch
   bool res_flat = false;                        // the uploaded system came from lmmhip_res_flatten
   FlatBufs fb_last{};
-  int tune_upd = 0, tune_rdy = 0, tune_sat = 0;
+  int tune_upd = 0, tune_sat = 0;
   double* pin_vals = nullptr;  // pinned host staging of lmmhip_res_values_pinned
   uint8_t* pin_rst = nullptr;
   int64_t pin_cap = 0;  // launch-width caps of the round kernels (0 = none)
@@ -309,6 +309,8 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   rc |= dalloc(c, &d.chgbits, (nC + 127) / 128 * 2 + 2);
   rc |= dalloc(c, &d.ready, nC + kMaxBlocks);
   rc |= dalloc(c, &d.bready, kMaxBlocks);
+  rc |= dalloc(c, &d.ctouch, nC);
+  rc |= dalloc(c, &d.cdup, nC);
   rc |= dalloc(c, &d.balive, kMaxBlocks);
   rc |= dalloc(c, &d.clist[0], nC);
   rc |= dalloc(c, &d.clist[1], nC);
@@ -396,8 +398,12 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
   const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
   c->sat_waves = cmean <= 64 ? 1 : cmean <= 160 ? 2 : 4;
+  if (nC > 0)  // constraints with a duplicate (variable, constraint) pair (structure only)
+    HIPCHK(hipMemsetAsync(d.cdup, 0, size_t(nC), c->stream));
   if (nnz > 0) {  // per-element usage w / penalty, kept in step with pen (lmmhip_update_vars)
     hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, c->stream, d);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(mm_dup_check, dim3(grid_for(nV, kBlock)), dim3(kBlock), 0, c->stream, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
   }
@@ -1145,7 +1151,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // Launch-width caps (tuning knobs, environment; 0 = uncapped): fewer blocks cut the fixed per-round
   // cost of the grid-stride round kernels once the alive set is small.
   const int cap_upd = env_int("LMMHIP_UPD_BLOCKS", c->tune_upd);
-  const int cap_rdy = env_int("LMMHIP_READY_BLOCKS", c->tune_rdy);
   const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat);
   auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
@@ -1159,7 +1164,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
   int buf = 0, cb = 0, chunk = 2;
   for (;;) {
-    const int gL = capped(grid_for(ncl, kBlock), cap_rdy);
+    const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
       if (int rc = launch_vote(c, r, nrows, buf))
         return rc;
@@ -1233,8 +1238,12 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   Dev d = c->d;
   d.vstat = nullptr;
   const bool bits = int64_t(d.nC) <= int64_t(kPBitWords) * 64;
-  const void* kern = bits ? reinterpret_cast<const void*>(&mm_persist<true>)
-                          : reinterpret_cast<const void*>(&mm_persist<false>);
+  // registers per row in the re-vote: 8, or 12 for longer mean rows (C4's LV08 routes: 11.7 elements)
+  const bool r16 = c->group > 8;
+  const void* kern = bits ? (r16 ? reinterpret_cast<const void*>(&mm_persist<true, 12>)
+                                 : reinterpret_cast<const void*>(&mm_persist<true, 8>))
+                          : (r16 ? reinterpret_cast<const void*>(&mm_persist<false, 12>)
+                                 : reinterpret_cast<const void*>(&mm_persist<false, 8>));
   if (!c->pbar)
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->pbar), BAR_WORDS * sizeof(unsigned)));
   int per_cu = 0;
@@ -1880,13 +1889,26 @@ int lmmhip_vote_profile(lmmhip_ctx* c, int64_t* rows, int64_t* elems, int cap) {
   HIPCHK(hipMemcpy(h.data(), c->vstat, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost));
   for (int r = 0; r < R && r < cap; r++) {
     int64_t a = 0, b = 0;
-    for (int k = 0; k < kMaxBlocks; k++) {
+    for (int k = 0; k < kDiagSlot; k++) {
       a += h[2 * (size_t(r) * kMaxBlocks + k)];
       b += h[2 * (size_t(r) * kMaxBlocks + k) + 1];
     }
     rows[r] = a;
     elems[r] = b;
   }
+  return R;
+}
+
+int lmmhip_vote_diag_profile(lmmhip_ctx* c, int64_t* out4, int cap) {
+  if (!c || !c->vstat)
+    return fail(LMMHIP_E_STATE, "no profiled maxmin solve");
+  const int R = int(std::min<int64_t>(c->stats.rounds, kStatRounds));
+  std::vector<int32_t> h(size_t(2) * kStatRounds * kMaxBlocks);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(h.data(), c->vstat, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost));
+  for (int r = 0; r < R && r < cap; r++)
+    for (int k = 0; k < 4; k++)
+      out4[4 * r + k] = h[2 * (size_t(r) * kMaxBlocks + kDiagSlot) + k];
   return R;
 }
 

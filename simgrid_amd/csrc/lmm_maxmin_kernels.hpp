@@ -13,8 +13,9 @@
 //                the vote; a variable whose level bound*penalty is below its minimum is fixed at its
 //                bound right here (maxmin.cpp:563-595); a variable with no alive constraint drops.
 //   mm_ready     one thread per constraint: no alive element votes elsewhere (nvote == 0) -> ready list.
-//   mm_saturate  one wave per ready constraint: claim its alive variables (atomicCAS), fix them at
-//                ratio/penalty (maxmin.cpp:583), push w*x, w/p and count decrements (maxmin.cpp:601-606).
+//   mm_saturate  K waves per ready constraint: claim its alive variables, fix them at ratio/penalty
+//                (maxmin.cpp:583), push w*x, w/p and count decrements (maxmin.cpp:601-606) and flag the
+//                receiving constraints (ctouch).  (The persistent engine fuses the two: sat_block.)
 //   mm_update    one thread per constraint: apply decrements, clamp (surf_interface.hpp:34-44 —
 //                clamping a sum of non-negative decrements == clamping after each one), drop
 //                saturated constraints (maxmin.cpp:608-623), refresh ratio, key and change stamp;
@@ -29,6 +30,23 @@ namespace lmmdev {
 __global__ void __launch_bounds__(kBlock) mm_elem_usage(Dev s) {
   for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz; j += int64_t(gridDim.x) * kBlock)
     s.csc_u[j] = s.csc_w[j] / s.pen[s.csc_v[j]];
+}
+
+// cdup (zeroed before): constraints holding two elements of one variable; every constraint of a row longer
+// than 64 elements is flagged without the pairwise test.
+__global__ void __launch_bounds__(kBlock) mm_dup_check(Dev s) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
+    const uint32_t b = s.var_ptr[v], e = s.var_ptr[v + 1];
+    if (e - b > 64) {
+      for (uint32_t i = b; i < e; i++)
+        s.cdup[s.csr_c[i]] = 1;
+      continue;
+    }
+    for (uint32_t i = b; i < e; i++)
+      for (uint32_t j = i + 1; j < e; j++)
+        if (s.csr_c[i] == s.csr_c[j])
+          s.cdup[s.csr_c[i]] = 1;
+  }
 }
 
 // Init, one wave per constraint: maxmin.cpp:520-555.  remaining = bound; skipped when
@@ -62,6 +80,7 @@ __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64
       CstRec rec;
       rec.drem = rec.duse = rec.dcnt = 0;
       rec.pad = 0;
+      s.ctouch[c] = 0;
       rec.rem = bound;
       rec.use = usage;
       rec.ratio = alive ? r : dinf();
@@ -109,7 +128,8 @@ __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double 
   if (s.key[c] == kDeadKey)
     return;
   unsigned long long* r = &s.cst[c].drem;
-  atomicAdd(&r[2], 1ull);  // dcnt > 0 marks the constraint touched for mm_update
+  s.ctouch[c] = 1;  // receives decrements this round (mm_update reads its record)
+  atomicAdd(&r[2], 1ull);  // fixed elements leaving c (mm_update subtracts them from nvote)
   if (!(s.cflags[c] & 1)) {
     const double w = s.csr_w[j];
     const int32_t ce = s.cexp[c];
@@ -283,10 +303,11 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int f
 // row targets (one lane per row, kFilt rows in flight per lane) and queues the rows that need a
 // re-vote in LDS; each full queue of kBlock rows is then resolved one lane per row, with up to kReg
 // independent gathers in flight, so the rare slow rows no longer stall whole waves of fast ones.
-constexpr int kReg = 8;
 constexpr int kFilt = 8;  // rows per lane per filter step (their loads in flight together)
-constexpr int kFlush = 4;  // filter rows between two queue flushes (queue capacity (kFlush + 1) x B)
 
+// Re-vote of one row, one lane: the first R elements in registers (their loads in flight together), longer
+// rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
+template <int R>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
@@ -297,36 +318,38 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   const uint16_t* __restrict__ key = s.key;
   const int t = rtgt[row];
   const int v = cvar[row];
-  if (s.vstate[v] != 0) {  // fixed by mm_saturate since: retire the row
+  const uint32_t b = crow[row], e = crow[row + 1];
+  const int32_t vst = s.vstate[v];
+  const double vb = s.vbound[v];
+  const double p = s.pen[v];
+  if (vst != 0) {  // fixed by a saturation since: retire the row
     rtgt[row] = kRetired;
     return;
   }
-  const uint32_t b = crow[row], e = crow[row + 1];
   if (s.vstat) {
     atomicAdd(st_rows, 1);
     atomicAdd(st_elems, int(e - b));
   }
-  int32_t cc[kReg];
-  unsigned kk[kReg];
+  int32_t cc[R];
+  unsigned kk[R];
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     cc[i] = b + i < e ? ccol[b + i] : -1;
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     kk[i] = cc[i] >= 0 ? key[cc[i]] : kDeadKey;
   unsigned mk = kDeadKey;
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     mk = min(mk, kk[i]);
-  for (uint32_t j = b + kReg; j < e; j++)
+  for (uint32_t j = b + R; j < e; j++)
     mk = min(mk, (unsigned)key[ccol[j]]);
   int nmin = 0;
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     nmin += kk[i] == mk;
-  for (uint32_t j = b + kReg; j < e; j++)
+  for (uint32_t j = b + R; j < e; j++)
     nmin += key[ccol[j]] == mk;
-  const double vb = s.vbound[v];
   if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
     s.vstate[v] = round + 1;  // fixed / dropped in this round
     rtgt[row] = kRetired;
@@ -335,10 +358,10 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   double minr = dinf();
   if (nmin > 1 || vb > 0) {
 #pragma unroll
-    for (int i = 0; i < kReg; i++)
+    for (int i = 0; i < R; i++)
       if (kk[i] == mk)
         minr = fmin(minr, s.cst[cc[i]].ratio);
-    for (uint32_t j = b + kReg; j < e; j++) {
+    for (uint32_t j = b + R; j < e; j++) {
       const int32_t c = ccol[j];
       if (key[c] == mk)
         minr = fmin(minr, s.cst[c].ratio);
@@ -346,11 +369,10 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   }
   int mult_old = 0;
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     mult_old += cc[i] == t;
-  for (uint32_t j = b + kReg; j < e; j++)
+  for (uint32_t j = b + R; j < e; j++)
     mult_old += ccol[j] == t;
-  const double p = s.pen[v];
   if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
     s.vstate[v] = round + 1;  // fixed / dropped in this round
     s.x[v] = vb;
@@ -363,20 +385,20 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   }
   int newt = INT_MAX;
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     if (kk[i] == mk && (nmin == 1 || s.cst[cc[i]].ratio == minr))
       newt = min(newt, cc[i]);
-  for (uint32_t j = b + kReg; j < e; j++) {
+  for (uint32_t j = b + R; j < e; j++) {
     const int32_t c = ccol[j];
     if (key[c] == mk && (nmin == 1 || s.cst[c].ratio == minr))
       newt = min(newt, c);
   }
   unsigned sk = kDeadKey;  // min key over the other constraints of the row
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     if (cc[i] != newt)
       sk = min(sk, kk[i]);
-  for (uint32_t j = b + kReg; j < e; j++) {
+  for (uint32_t j = b + R; j < e; j++) {
     const int32_t c = ccol[j];
     if (c != newt)
       sk = min(sk, (unsigned)key[c]);
@@ -390,9 +412,9 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     return;
   int mult_new = 0;
 #pragma unroll
-  for (int i = 0; i < kReg; i++)
+  for (int i = 0; i < R; i++)
     mult_new += cc[i] == newt;
-  for (uint32_t j = b + kReg; j < e; j++)
+  for (uint32_t j = b + R; j < e; j++)
     mult_new += ccol[j] == newt;
   if (t >= 0 && key[t] != kDeadKey)
     atomicAdd(&s.nvote[t], mult_old);
@@ -400,23 +422,114 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   rtgt[row] = newt;
 }
 
-// kBits: the "target changed last round" test reads a bitmap of the changed constraints held in LDS
-// (built by mm_update, one bit per constraint, loaded once per block) instead of gathering the 16-bit
-// change stamp of every alive row's target from HBM/L2 — the filter then streams only the row
-// targets.  One 1024-thread block per CU (the bitmap takes up to kBitWords * 8 B of LDS).
+// Filter + re-vote of the rows [lo, hi) of buffer `buf` by the calling workgroup, every wave on its own
+// contiguous share of 64-row groups with no workgroup barrier: a wave streams F rows per lane at a time
+// (targets and floors, loads in flight together), tests the target against the changed-constraint bitmap
+// (kBits: in LDS, built by mm_update — a set bit means the target's KEY changed or it died last round;
+// otherwise the 16-bit change stamps), gathers the target's key for those rows, and queues the rows whose
+// vote may move in its own LDS queue `qw` (2 x 64 entries); every full 64 are resolved one lane per row
+// (vote_row) right away, so one wave's dependent gathers overlap the other waves' streaming.
+// A row re-votes when it never voted, when its target's key changed or it died and the key is no longer
+// strictly below the row's floor (skey: its other keys only grow), or — sensitive rows (skey 0) — when its
+// target was touched at all (chg stamp).  Returns the rows this wave queued (lane-uniform).
+// kDiag (measurement only, LMMHIP_VOTE_DIAG): 1 = the filter alone (rows queued, none resolved), with
+// per-round counters of target-changed / sensitive / queued rows in vstat's kDiagSlot.
+constexpr int kQW = 2 * kWave;  // per-wave queue capacity
+constexpr int kDiagSlot = kMaxBlocks - 4;  // vstat block slots kDiagSlot.. hold the vote diagnostics (kDiag)
+
+template <bool kBits, int R, int F, int kDiag>
+__device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
+                                          const uint64_t* bits, int* qw, int* st_rows, int* st_elems) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave, nw = blockDim.x / kWave;
+  const int64_t ngr = (hi - lo + kWave - 1) / kWave;
+  const int64_t gpw = (ngr + nw - 1) / nw;
+  const int64_t wlo = lo + int64_t(w) * gpw * kWave;
+  const int64_t whi = wlo + gpw * kWave < hi ? wlo + gpw * kWave : hi;
+  const int32_t* __restrict__ rtgt = s.rtgt[buf];
+  const uint16_t* __restrict__ skey = s.skey[buf];
+  const uint16_t* __restrict__ key = s.key;
+  const uint16_t prev = uint16_t(round - 1);
+  const unsigned long long below = (1ull << lane) - 1;
+  int qn = 0, nq = 0;
+  for (int64_t base = wlo; base < whi; base += int64_t(F) * kWave) {  // wave-uniform
+    int tt[F];
+    unsigned sk[F];
+#pragma unroll
+    for (int u = 0; u < F; u++) {
+      const int64_t row = base + u * kWave + lane;
+      tt[u] = row < whi ? rtgt[row] : kRetired;
+      sk[u] = row < whi ? unsigned(skey[row]) : 1u;
+    }
+    bool ch[F];
+#pragma unroll
+    for (int u = 0; u < F; u++) {
+      if (kBits)
+        ch[u] = tt[u] >= 0 && ((bits[tt[u] >> 6] >> (tt[u] & 63)) & 1);
+      else
+        ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
+    }
+    unsigned kt[F], cg[F];
+#pragma unroll
+    for (int u = 0; u < F; u++) {  // target key (changed targets) / stamp (sensitive rows), together
+      kt[u] = ch[u] ? key[tt[u]] : 0u;
+      cg[u] = (kBits && !ch[u] && tt[u] >= 0 && sk[u] == 0) ? unsigned(s.chg[tt[u]]) : 0x10000u;
+    }
+    unsigned needm = 0;
+#pragma unroll
+    for (int u = 0; u < F; u++) {
+      bool need = tt[u] == kUnvoted;  // (rows >= whi carry kRetired)
+      if (ch[u])
+        need = !(kt[u] < sk[u]);
+      else if (kBits && cg[u] == prev)
+        need = true;
+      needm |= unsigned(need) << u;
+      if (kDiag == 1 && s.vstat && round < kStatRounds) {
+        const unsigned long long mc = __ballot(ch[u]), ms = __ballot(tt[u] >= 0 && sk[u] == 0);
+        const unsigned long long mq = __ballot(need);
+        if (lane == 0) {
+          int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
+          atomicAdd(&d[0], __popcll(mc));
+          atomicAdd(&d[1], __popcll(ms));
+          atomicAdd(&d[2], __popcll(mq));
+        }
+      }
+    }
+#pragma unroll 1
+    for (int u = 0; u < F; u++) {
+      const bool need = (needm >> u) & 1;
+      const unsigned long long m = __ballot(need);
+      if (need)
+        qw[qn + __popcll(m & below)] = int(base + u * kWave + lane);
+      qn += __popcll(m);
+      if (qn >= kWave) {  // wave-uniform: resolve the newest 64
+        __builtin_amdgcn_wave_barrier();
+        qn -= kWave;
+        nq += kWave;
+        const int row = qw[qn + lane];
+        __builtin_amdgcn_wave_barrier();
+        if (kDiag == 0)
+          vote_row<R>(s, buf, round, row, st_rows, st_elems);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (kDiag == 0 && lane < qn)
+    vote_row<R>(s, buf, round, qw[lane], st_rows, st_elems);
+  return nq + qn;
+}
+
+// Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
+// to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
 constexpr int kBitWords = 17408;  // LDS bitmap capacity: 1,114,112 constraints
-// kDiag (measurement only, LMMHIP_VOTE_DIAG): 1 = the filter pass alone (rows queued, none resolved, no
-// global writes), 2 = the bitmap load alone.
 template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int buf, int round) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ int st_rows, st_elems;
-  __shared__ int q[B * (kFlush + 1)];  // queued rows (relative to the block's chunk base)
-  __shared__ int qn;
+  __shared__ int q[(B / kWave) * kQW];  // per-wave queues of rows to re-vote
   __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
   if (threadIdx.x == 0)
-    st_rows = st_elems = qn = 0;
+    st_rows = st_elems = 0;
   if (kBits) {
     const int n16 = (s.nC + 127) / 128;  // 16-B pieces of the bitmap
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(s.chgbits);
@@ -425,89 +538,25 @@ template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B)
       dst[i] = src[i];
   }
   __syncthreads();
-  if (kDiag == 2) {
+  if (kDiag == 2) {  // measurement only: the bitmap load alone, and the changed-constraint count
+    if (kBits && blockIdx.x == 0 && s.vstat && round < kStatRounds) {
+      int pc = 0;
+      for (int i = threadIdx.x; i < (s.nC + 63) / 64; i += B)
+        pc += __popcll(bits[i]);
+      atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 3, pc);
+    }
     if (threadIdx.x == 0 && bits[1] == 0x5a5a5a5a5a5a5a5aull)  // keeps the load
       s.ctl[CTL_WORDS - 1] = 1;
     return;
   }
   const int64_t nrows = s.ctl[CTL_NROWS + buf];
-  const int32_t* __restrict__ rtgt = s.rtgt[buf];
-  const uint16_t* __restrict__ skey = s.skey[buf];
-  const uint16_t* __restrict__ key = s.key;
-  const uint16_t prev = uint16_t(round - 1);
-  // contiguous chunk per block so queued rows fit in 32-bit offsets from the chunk base
-  constexpr int kStep = B * kFilt;
-  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + B - 1) / B * B;  // rows per block
+  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;  // rows per workgroup
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
-  for (int64_t base = lo; base < hi; base += kStep) {  // block-uniform
-    int tt[kFilt];
-#pragma unroll
-    for (int u = 0; u < kFilt; u++) {
-      const int64_t row = base + u * B + threadIdx.x;
-      tt[u] = row < hi ? rtgt[row] : kRetired;
-    }
-    bool ch[kFilt];
-#pragma unroll
-    for (int u = 0; u < kFilt; u++) {
-      if (kBits)
-        ch[u] = tt[u] >= 0 && ((bits[tt[u] >> 6] >> (tt[u] & 63)) & 1);
-      else
-        ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
-    }
-    // With the bitmap, a set bit means the target's KEY changed (or it died) last round; a sensitive
-    // row (skey 0: bounded variable or key-level tie) also re-votes when its target was merely touched
-    // (chg stamp).  Without it, chg marks every touched target.
-    unsigned kt[kFilt], sk[kFilt], cg[kFilt];
-#pragma unroll
-    for (int u = 0; u < kFilt; u++)
-      sk[u] = base + u * B + threadIdx.x < hi ? skey[base + u * B + threadIdx.x] : 1u;  // streamed with rtgt
-#pragma unroll
-    for (int u = 0; u < kFilt; u++) {  // target key (changed targets) / stamp (sensitive rows), together
-      kt[u] = ch[u] ? key[tt[u]] : 0u;
-      cg[u] = (kBits && !ch[u] && tt[u] >= 0 && sk[u] == 0) ? unsigned(s.chg[tt[u]]) : 0x10000u;
-    }
-#pragma unroll
-    for (int u = 0; u < kFilt; u++) {
-      const int64_t row = base + u * B + threadIdx.x;
-      bool need = tt[u] == kUnvoted;
-      if (ch[u])  // target changed last round: does the vote still stand?
-        need = !(kt[u] < sk[u]);
-      else if (kBits && cg[u] == prev)
-        need = true;
-      const unsigned long long m = __ballot(need);  // one LDS atomic per wave
-      const int lane = threadIdx.x & (kWave - 1);
-      const int leader = m ? __ffsll((long long)m) - 1 : 0;
-      int at = 0;
-      if (m && lane == leader)
-        at = atomicAdd(&qn, __popcll(m));
-      at = __shfl(at, leader, kWave);
-      if (need)
-        q[at + __popcll(m & ((1ull << lane) - 1))] = int(row - lo);
-      if ((u % kFlush) == kFlush - 1) {  // at most kFlush * B rows queued since the last flush
-        __syncthreads();
-        int n = qn;
-        while (n >= B) {  // resolve full queues: the last B entries each time
-          if (kDiag == 0)
-            vote_row(s, buf, round, lo + q[n - B + threadIdx.x], &st_rows, &st_elems);
-          n -= B;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0)
-          qn = n;
-        __syncthreads();
-      }
-    }
-  }
-  const int n = qn;
-  if (kDiag) {
-    if (threadIdx.x == 0 && n == -7)  // keeps the filter
-      s.ctl[CTL_WORDS - 1] = 1;
-    return;
-  }
-  if (threadIdx.x < n)
-    vote_row(s, buf, round, lo + q[threadIdx.x], &st_rows, &st_elems);
-  if (s.vstat) {
+  if (lo < hi)
+    vote_waves<kBits, 8, kFilt, kDiag>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW, &st_rows,
+                                       &st_elems);
+  if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
       s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x)] = st_rows;
@@ -542,6 +591,10 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
     s.bready[blockIdx.x] = cnt;
 }
 
+
+// Round phase 3 — saturation of the ready constraints (maxmin.cpp:578-606): sat_block for the persistent
+// engine (ready test fused in), mm_saturate over mm_ready's list for the multi-launch engine.
+
 // Round phase 3 — saturate the ready constraints: maxmin.cpp:578-606.
 // K waves per ready constraint c (K = the host's estimate of c's 64-element CSC chunks), wave k taking
 // chunks k, k + K, ...  Per chunk: lanes claim the alive variables (atomicCAS: a duplicate element
@@ -555,13 +608,17 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
 constexpr int kSatU = 4;
 
 __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
-                                               int round, int lane, int* pre) {
+                                               int round, int lane, int* pre, bool dup) {
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
   int32_t lv = -1;
   if (j < ce) {
     lv = s.csc_v[j];
-    if (s.vstate[lv] != 0 || atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
+    if (s.vstate[lv] != 0)
+      lv = -1;
+    else if (!dup)
+      s.vstate[lv] = round + 1;
+    else if (atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
       lv = -1;
   }
   double lp = 1.0, lx = 0.0;
@@ -611,6 +668,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       if (cc[u] >= 0 && (cc[u] == c || s.key[cc[u]] == kDeadKey))
         cc[u] = -1;
       if (cc[u] >= 0) {
+        s.ctouch[cc[u]] = 1;  // receives decrements this round (mm_update reads its record)
         fat[u] = s.cflags[cc[u]] & 1;
         const double w = s.csr_w[kk[u]];
         const int32_t ce = s.cexp[cc[u]];
@@ -638,14 +696,118 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
   __builtin_amdgcn_wave_barrier();
 }
 
+// Ready test + saturation, block-cooperative.  In pass p, wave w of workgroup b tests the 64 constraints of
+// group (p * NBW + w) * grid + b (consecutive groups on different workgroups, so the ready constraints spread
+// over the chip; lanes stay coalesced); entries are list positions (cl) or identity ids (cl == nullptr).  The
+// ready ones of all the workgroup's passes are collected in LDS with the prefix of their 64-element CSC
+// chunks (up to CAP at a time), then the workgroup's waves take the chunks round-robin: a high-degree
+// constraint (a fat-tree core link) spreads over the waves instead of serialising one, and the saturation
+// chains of many constraints run side by side.  Ready constraints share no alive variable (each alive
+// variable votes for exactly one), so claims never race between them.  c leaves the light table:
+// ctouch[c] = 2 tells mm_update (the owner of key / chg) to retire it; c's ratio is left in place.
+template <int NB, int CAP> struct SatLds {
+  int32_t rc[CAP];      // collected ready constraints
+  int32_t rr[CAP + 1];  // exclusive prefix of their chunk counts
+  int wa[NB / kWave], wb[NB / kWave];
+  int na, nb;           // collected constraints / chunks
+  int pre[NB / kWave][kWave];  // saturate_chunk's per-wave row-length prefix
+};
+
+template <int NB, int CAP>
+__device__ __forceinline__ void sat_flush(const Dev& s, int round, SatLds<NB, CAP>& L) {
+  constexpr int NBW = NB / kWave;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int ta = L.na, tb = L.nb;
+  for (int g = w; g < tb; g += NBW) {  // wave-uniform
+    int k = 0;  // last collected entry whose first chunk is <= g
+#pragma unroll
+    for (int step = CAP / 2; step > 0; step >>= 1)
+      if (k + step < ta && L.rr[k + step] <= g)
+        k += step;
+    const int32_t cc = L.rc[k];
+    const int ch = g - L.rr[k];
+    const double r = ld_rlx(&s.cst[cc].ratio);  // wave-uniform address: keep it off the scalar cache
+    saturate_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
+                   s.cdup[cc] != 0);
+    if (ch == 0 && lane == 0)
+      s.ctouch[cc] = 2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    L.na = L.nb = 0;
+  __syncthreads();
+}
+
+// Returns whether the workgroup found a ready constraint.
+template <int NB, int CAP>
+__device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t* __restrict__ cl, int64_t n,
+                                          SatLds<NB, CAP>& L) {
+  static_assert(CAP >= NB, "one pass must fit");
+  constexpr int NBW = NB / kWave;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (threadIdx.x == 0)
+    L.na = L.nb = 0;
+  __syncthreads();
+  bool any = false;
+  for (int64_t p = 0; p * NB * gridDim.x < n; p++) {  // workgroup-uniform
+    const int64_t i = ((p * NBW + w) * gridDim.x + blockIdx.x) * kWave + lane;
+    int32_t c = -1;
+    if (i < n)
+      c = cl ? cl[i] : int32_t(i);
+    const bool rdy = c >= 0 && s.key[c] != kDeadKey && s.nvote[c] == 0;
+    const int nch = rdy ? int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave) : 0;
+    int ia = rdy, ib = nch;  // block exclusive scans of (ready, chunks)
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int xa = __shfl_up(ia, o, kWave), xb = __shfl_up(ib, o, kWave);
+      if (lane >= o) {
+        ia += xa;
+        ib += xb;
+      }
+    }
+    if (lane == kWave - 1) {
+      L.wa[w] = ia;
+      L.wb[w] = ib;
+    }
+    __syncthreads();
+    int oa = L.na, ob = L.nb, ta = 0, tb = 0;
+#pragma unroll
+    for (int k = 0; k < NBW; k++) {
+      oa += k < w ? L.wa[k] : 0;
+      ob += k < w ? L.wb[k] : 0;
+      ta += L.wa[k];
+      tb += L.wb[k];
+    }
+    if (rdy) {
+      L.rc[oa + ia - 1] = c;
+      L.rr[oa + ia - 1] = ob + ib - nch;
+    }
+    any |= ta > 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      L.na += ta;
+      L.nb += tb;
+    }
+    __syncthreads();
+    if (L.na > CAP - NB)  // workgroup-uniform: the next pass might not fit
+      sat_flush<NB, CAP>(s, round, L);
+  }
+  if (L.na)
+    sat_flush<NB, CAP>(s, round, L);
+  return any;
+}
+
+// Multi-launch engine: saturation of mm_ready's list, K waves per ready constraint (chunks k, k + K, ...)
+// spread evenly over the whole grid — the ready list is global here, so the work balances across workgroups.
 template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int k, int round, int lane,
                                                               int* pre) {
   const double r = ld_rlx(&s.cst[c].ratio);  // wave-uniform address: keep it off the scalar cache
   const uint32_t ce = s.cnst_ptr[c + 1];
+  const bool dup = s.cdup[c] != 0;
   for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
-    saturate_chunk(s, c, r, base, ce, round, lane, pre);
+    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup);
   if (k == 0 && lane == 0)  // c leaves the light table: mm_update (the owner of key / chg) retires it
-    st_rlx(&s.cst[c].pad, int64_t(round) + 1);
+    s.ctouch[c] = 2;
 }
 
 // K waves per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
@@ -706,6 +868,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
   }
 }
 
+
 // Round phase 4 — constraint update: maxmin.cpp:603-658, one wave = 64 consecutive constraints (identity
 // order), so the changed-constraint bitmap the next vote reads is one ballot per wave.  A bit is set when
 // the constraint's 16-bit KEY changed or it left the light table (the only events that can move a
@@ -713,105 +876,20 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 // FATPIPE usage is recomputed wave-cooperatively: max w/p over the elements whose variable is still at
 // 0 (maxmin.cpp:625-658), 64 elements per step.  Returns (per lane) alive constraints; *touch = some
 // constraint of the wave was touched.
-__device__ __forceinline__ int update_wave(const Dev& s, int64_t base, int round, double prec, bool* touch) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t c = base + lane;
-  bool changed = false, live = false, tch = false, fat = false;
-  unsigned okey = kDeadKey;
-  CstRec* rec = s.cst + c;
-  unsigned long long qx = 0, qy = 0, qz = 0;
-  if (c < s.nC) {
-    okey = s.key[c];
-    if (okey != kDeadKey) {
-      if (rec->pad == int64_t(round) + 1) {  // saturated by mm_saturate this round (maxmin.cpp:608-615)
-        s.key[c] = kDeadKey;
-        s.chg[c] = uint16_t(round);
-        rec->ratio = dinf();
-        changed = true;
-      } else {
-        live = true;
-        qx = rec->drem;
-        qy = rec->duse;
-        qz = rec->dcnt;
-        tch = qz != 0;  // received decrements this round
-        fat = tch && (s.cflags[c] & 1);
-      }
-    }
-  }
-  double fuse = 0.0;
-  unsigned long long fm = __ballot(fat);
-  while (fm) {  // wave-uniform
-    const int l = __ffsll((long long)fm) - 1;
-    fm &= fm - 1;
-    const int64_t cl = base + l;
-    const uint32_t b = s.cnst_ptr[cl], e = s.cnst_ptr[cl + 1];
-    double m = 0.0;
-    for (uint32_t j = b + lane; j < e; j += kWave)
-      if (!(s.x[s.csc_v[j]] > 0))
-        m = fmax(m, s.csc_u[j]);
-    m = wave_max(m);
-    if (lane == l)
-      fuse = m;
-  }
-  int alive = 0;
-  if (live) {
-    if (!tch) {  // untouched: ratio unchanged
-      alive = 1;
-    } else {
-      *touch = true;
-      rec->drem = rec->duse = rec->dcnt = 0;
-      s.nvote[c] -= int(qz);  // fixed elements leave (voters of c were compensated)
-      s.chg[c] = uint16_t(round);
-      const double bound = rec->bound;
-      double rem = rec->rem, use;
-      if (!fat) {
-        const int32_t ce = s.cexp[c];
-        use = rec->use - dec_val(qy, cexp_use(ce));
-        rem -= dec_val(qx, cexp_rem(ce));
-        if (rem < bound * prec)
-          rem = 0.0;
-        if (use < prec)
-          use = 0.0;
-      } else {
-        use = fuse;
-      }
-      rec->rem = rem;
-      rec->use = use;
-      if (!(use > prec) || !(rem > bound * prec)) {
-        rec->ratio = dinf();
-        s.key[c] = kDeadKey;
-        changed = true;
-      } else {
-        const double r = rem / use;
-        rec->ratio = r;
-        const unsigned nk = ratio_key(r);
-        s.key[c] = uint16_t(nk);
-        changed = nk != okey;
-        alive = 1;
-      }
-    }
-  }
-  const unsigned long long word = __ballot(changed);
-  if (lane == 0)
-    s.chgbits[base >> 6] = word;
-  return alive;
-}
-
-// update_wave over K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups
-// (key, then record, flags, scale, votes) is issued before any of them is used, so a wave keeps K times
-// the memory requests in flight — the persistent engine has 16 waves per CU, not 32.  Same arithmetic
-// as update_wave (bit-identical results).
+// K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups (key and touch
+// flag, then — touched constraints only — record, flags, scale, votes) is issued before any of them is
+// used, so a wave keeps K times the memory requests in flight.
 template <int K>
 __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
                                              bool* touch) {
   const int lane = threadIdx.x & (kWave - 1);
-  unsigned okey[K];
+  unsigned okey[K], tf[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int64_t c = base0 + k * stride + lane;
     okey[k] = c < s.nC ? unsigned(s.key[c]) : kDeadKey;
+    tf[k] = c < s.nC ? unsigned(s.ctouch[c]) : 0u;  // 1 = received decrements, 2 = saturated this round
   }
-  int64_t pad[K];
   unsigned long long qx[K], qy[K], qz[K];
   double rem[K], use[K], bnd[K];
   int32_t ce[K], nv[K];
@@ -819,14 +897,12 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int64_t c = base0 + k * stride + lane;
-    pad[k] = 0;
     qx[k] = qy[k] = qz[k] = 0;
     rem[k] = use[k] = bnd[k] = 0.0;
     ce[k] = nv[k] = 0;
     fl[k] = 0;
-    if (okey[k] != kDeadKey) {
+    if (okey[k] != kDeadKey && tf[k] == 1) {  // an untouched constraint keeps its record as it is
       const CstRec* rec = s.cst + c;
-      pad[k] = rec->pad;
       qx[k] = rec->drem;
       qy[k] = rec->duse;
       qz[k] = rec->dcnt;
@@ -846,9 +922,9 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       break;
     const int64_t c = gbase + lane;
     const bool live0 = okey[k] != kDeadKey;
-    const bool sat = live0 && pad[k] == int64_t(round) + 1;
+    const bool sat = live0 && tf[k] == 2;
     const bool live = live0 && !sat;
-    const bool tch = live && qz[k] != 0;
+    const bool tch = live && tf[k] == 1;
     const bool fat = tch && (fl[k] & 1);
     double fuse = 0.0;
     unsigned long long fm = __ballot(fat);
@@ -870,6 +946,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     if (sat) {
       s.key[c] = kDeadKey;
       s.chg[c] = uint16_t(round);
+      s.ctouch[c] = 0;
       rec->ratio = dinf();
       changed = true;
     } else if (live) {
@@ -877,6 +954,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
         alive++;
       } else {
         *touch = true;
+        s.ctouch[c] = 0;
         rec->drem = rec->duse = rec->dcnt = 0;
         s.nvote[c] = nv[k] - int(qz[k]);
         s.chg[c] = uint16_t(round);

@@ -9,8 +9,8 @@
 //   init            mm_init_cnsts / mm_init_vars bodies (maxmin.cpp:509-555)
 //   round r:  V     filter + re-vote of the rows whose target's key changed (vote_row)
 //             |     grid barrier
-//             S     ready test (nvote == 0) fused with saturation: the wave that finds a ready
-//             |     constraint saturates it (saturate_one), maxmin.cpp:578-606
+//             S     ready test (nvote == 0) fused with saturation (sat_block: the ready constraints'
+//             |     CSC chunks shared by the workgroup's waves), maxmin.cpp:578-606
 //             |     grid barrier
 //             U     constraint update (update_wave), maxmin.cpp:603-658; alive count
 //             |     grid barrier; alive == 0 -> done (every block reads the same count)
@@ -154,20 +154,20 @@ __device__ __forceinline__ int64_t pwave() { return int64_t(threadIdx.x / kWave)
 
 template <bool kBits> struct PVoteLds {
   uint64_t bits[kBits ? kPBitWords : 2];
-  int q[kPB * (kPFilt + 1)];  // queued rows (global row ids)
-  int qn, nq, st0, st1;
+  int q[kPW * kQW];  // per-wave queues of rows to re-vote (vote_waves)
+  int st0, st1;
 };
+using PSatLds = SatLds<kPB, 4 * kPB>;
 template <bool kBits> union PLds {
   PVoteLds<kBits> v;
-  int pre[kPW][kWave];  // saturate_chunk's per-wave row-length prefix
+  PSatLds sat;  // ready test + saturation
+  int pre[kPW][kWave];  // compaction scratch
   int cnt;              // update: alive constraints of the workgroup
 };
 
-// V: the rows of buffer `buf` in tiles of kPB * kPFilt (tile t -> workgroup t mod grid).  A row re-votes
-// when it never voted, when its target's key changed or the target died last round (bitmap bit), unless
-// the target is still strictly below the row's other keys (skey), or — sensitive rows (skey 0) — when
-// its target was touched last round (chg stamp).  Queued rows are resolved kPB at a time (vote_row).
-template <bool kBits>
+// V: the rows of buffer `buf`, one contiguous chunk (a multiple of 64) per workgroup, filtered and re-voted
+// by vote_waves (every wave on its own share, no workgroup barrier after the bitmap load).
+template <bool kBits, int R>
 __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds<kBits>& L, bool count) {
   if (kBits) {
     const int n16 = (s.nC + 127) / 128;
@@ -176,98 +176,21 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
     for (int i = threadIdx.x; i < n16; i += kPB)
       dst[i] = src[i];
   }
-  if (threadIdx.x == 0)
-    L.qn = L.nq = 0;
   __syncthreads();
-  const int32_t* rtgt = s.rtgt[buf];
-  const uint16_t* skey = s.skey[buf];
-  const uint16_t prev = uint16_t(round - 1);
-  const int lane = threadIdx.x & (kWave - 1);
-  // one contiguous chunk of rows per workgroup (a multiple of 64), in steps of kPB * kPFilt rows
-  constexpr int64_t kStep = int64_t(kPB) * kPFilt;
   const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
-  for (int64_t base = lo; base < hi; base += kStep) {  // workgroup-uniform
-    int tt[kPFilt];
-#pragma unroll
-    for (int u = 0; u < kPFilt; u++) {
-      const int64_t row = base + u * kPB + threadIdx.x;
-      tt[u] = row < hi ? rtgt[row] : kRetired;
-    }
-    bool ch[kPFilt];
-    unsigned sk[kPFilt], kt[kPFilt], cg[kPFilt];
-#pragma unroll
-    for (int u = 0; u < kPFilt; u++) {
-      if (kBits)
-        ch[u] = tt[u] >= 0 && ((L.bits[tt[u] >> 6] >> (tt[u] & 63)) & 1);
-      else
-        ch[u] = tt[u] >= 0 && s.chg[tt[u]] == prev;
-      sk[u] = (kBits ? tt[u] >= 0 : ch[u]) ? skey[base + u * kPB + threadIdx.x] : 1u;
-    }
-#pragma unroll
-    for (int u = 0; u < kPFilt; u++) {
-      kt[u] = ch[u] ? s.key[tt[u]] : 0u;
-      cg[u] = (kBits && !ch[u] && tt[u] >= 0 && sk[u] == 0) ? unsigned(s.chg[tt[u]]) : 0x10000u;
-    }
-#pragma unroll
-    for (int u = 0; u < kPFilt; u++) {
-      const int64_t row = base + u * kPB + threadIdx.x;
-      bool need = tt[u] == kUnvoted;  // (rows >= hi carry kRetired)
-      if (ch[u])
-        need = !(kt[u] < sk[u]);
-      else if (kBits && cg[u] == prev)
-        need = true;
-      const unsigned long long m = __ballot(need);  // one LDS atomic per wave
-      const int leader = m ? __ffsll((long long)m) - 1 : 0;
-      int at = 0;
-      if (m && lane == leader)
-        at = atomicAdd(&L.qn, __popcll(m));
-      at = __shfl(at, leader, kWave);
-      if (need)
-        L.q[at + __popcll(m & ((1ull << lane) - 1))] = int(row);
-    }
-    __syncthreads();
-    int n = L.qn;
-    while (n >= kPB) {  // resolve full queues: the last kPB entries each time
-      vote_row(s, buf, round, L.q[n - kPB + threadIdx.x], &L.st0, &L.st1);
-      n -= kPB;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      L.nq += L.qn - n;
-      L.qn = n;
-    }
-    __syncthreads();
-  }
-  const int n = L.qn;
-  if (threadIdx.x < n)
-    vote_row(s, buf, round, L.q[threadIdx.x], &L.st0, &L.st1);
-  if (count && threadIdx.x == 0 && L.nq + n)
-    atomicAdd(&s.ctl[CTL_RESEVAL], L.nq + n);
+  int nq = 0;
+  if (lo < hi)
+    nq = vote_waves<kBits, R, kPFilt, 0>(s, buf, round, lo, hi, L.bits, L.q + (threadIdx.x / kWave) * kQW, &L.st0,
+                                         &L.st1);
+  if (count && (threadIdx.x & (kWave - 1)) == 0 && nq)
+    atomicAdd(&s.ctl[CTL_RESEVAL], nq);
 }
 
-// S: identity-order scan of the constraints, 64 per wave step; a ready constraint (every alive element
-// votes for it, nvote == 0) is saturated by the wave that found it.  Ready constraints share no alive
-// variable (each alive variable votes for exactly one constraint), so the claims never race across waves.
-__device__ bool p_saturate(const Dev& s, int round, int* pre) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wave = pwave();
-  const int64_t nwaves = int64_t(gridDim.x) * kPW;
-  bool any = false;
-  for (int64_t base = wave * kWave; base < s.nC; base += nwaves * kWave) {  // wave-uniform
-    const int64_t c = base + lane;
-    const bool rdy = c < s.nC && s.key[c] != kDeadKey && s.nvote[c] == 0;
-    unsigned long long m = __ballot(rdy);
-    any |= m != 0;
-    while (m) {
-      const int l = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      saturate_one<1>(s, int32_t(base + l), 0, round, lane, pre);
-    }
-  }
-  return any;
-}
+// S: ready test fused with saturation over every constraint (identity ids), sat_block (the ready
+// constraints' CSC chunks shared by the workgroup's 16 waves).
+__device__ void p_saturate(const Dev& s, int round, PSatLds& L) { sat_block<kPB, 4 * kPB>(s, round, nullptr, s.nC, L); }
 
 // C: compaction of the alive rows of buffer `in` into `out`, one contiguous chunk of rows per workgroup:
 // pass 1 counts the chunk's alive rows and elements, ONE 64-bit atomic per workgroup allocates both
@@ -364,7 +287,7 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
     orow[rbase] = ebase;
 }
 
-template <bool kBits>
+template <bool kBits, int R>
 __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double prec, int max_rounds,
                                                   int cmp_every, long long* pt, unsigned pt_cap, int sysf) {
   __shared__ PLds<kBits> L;
@@ -373,7 +296,7 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
     pt[1] = wall_clock64();  // launch (barrier 0's exit slot)
   unsigned long long* alloc = reinterpret_cast<unsigned long long*>(barw + BAR_ALLOC);
   int32_t* palive = reinterpret_cast<int32_t*>(barw + BAR_PALIVE);
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
   // init (maxmin.cpp:509-555) overlapped with the rendezvous
   init_cnsts_waves(s, prec, pwave(), int64_t(gridDim.x) * kPW);
@@ -384,7 +307,7 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
   int buf = 0;
   int64_t nrows = s.nV;
   for (int r = 0;; r++) {
-    p_vote<kBits>(s, buf, r, nrows, L.v, pt != nullptr);
+    p_vote<kBits, R>(s, buf, r, nrows, L.v, pt != nullptr);
     if (!grid_sync(b, ++gen))
       return;
     if (lead) {  // words first used later in this round, last read before the previous barrier
@@ -392,7 +315,7 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
         st_rlx(&palive[16 * ((r + 1) & 1) + i], 0);
       st_rlx(alloc, 0ull);
     }
-    p_saturate(s, r, L.pre[w]);
+    p_saturate(s, r, L.sat);
     if (!grid_sync(b, ++gen))
       return;
     if (threadIdx.x == 0)

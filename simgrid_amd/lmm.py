@@ -137,6 +137,7 @@ SIGNATURES = {
     "lmmhip_launch_profile": (I, [P, PI, PI, ct.POINTER(ct.c_float), I]),
     "lmmhip_round_profile": (I, [P, PI64, PI64, I]),
     "lmmhip_vote_profile": (I, [P, PI64, PI64, I]),
+    "lmmhip_vote_diag_profile": (I, [P, PI64, I]),
     "lmmhip_ctx_set_stream": (I, [P, P]),
     "lmmhip_ctx_use_own_stream": (I, [P]),
     "lmmhip_ctx_set_engine": (I, [P, I]),
@@ -531,6 +532,16 @@ class System:
         if r < 0:
             raise LmmError(lib().lmmhip_last_error().decode())
         return rv[:r], re_[:r]
+
+    def vote_diag_profile(self):
+        """LMMHIP_VOTE_DIAG runs: per round (target-changed rows, sensitive rows, queued rows, changed constraints)."""
+        c = self.device_ctx()
+        cap = 1 << 16
+        out = np.zeros(4 * cap, np.int64)
+        r = lib().lmmhip_vote_diag_profile(c, out.ctypes.data_as(PI64), cap)
+        if r < 0:
+            raise LmmError(lib().lmmhip_last_error().decode())
+        return out[:4 * r].reshape(r, 4)
 
     @property
     def modified(self):
