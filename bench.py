@@ -245,18 +245,18 @@ def main():
         from oracle import pyoracle as O
 
         div = args.cpu_sample_div
-        times, rounds = [], 0
+        times, cpu_rounds = [], 0
         for _ in range(max(1, args.cpu_reps)):  # a fresh system per repetition (solve() runs once per change)
             o = O.System(False)
             o.gen_synthetic(args.cnst // div, args.vars // div, args.k, seed=1, want_vars=False, **gen_kw)
             times.append(o.timed_solve())
-            rounds = o.last_rounds
+            cpu_rounds = o.last_rounds
             del o
         m, sd = mean_sd(times)
         cpu = {"value": round((args.vars // div) / m, 1), "unit": "vars/s", "cores": 1, "kind": "port",
                "sample": f"same generator at 1/{div} scale ({args.cnst // div} cnst x {args.vars // div} vars x {args.k}),"
                          f" solve() timed with steady_clock, {len(times)} reps: {m:.3f} +- {sd:.3f} s,"
-                         f" {rounds} sequential rounds",
+                         f" {cpu_rounds} sequential rounds",
                "reps": len(times), "solve_s_mean": round(m, 4), "solve_s_sd": round(sd, 4), **host_info()}
 
     if rank == 0:
@@ -275,6 +275,7 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    del s  # free the device context while the HIP runtime is up (not in interpreter teardown)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -515,6 +516,7 @@ def run_config(args):
             sh.close()
     if batch is not None:
         batch.close()
+    s = None  # free the device context while the HIP runtime is up (not in interpreter teardown)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -16,4 +16,4 @@ echo "bench rc=$rc" >> gpurun_out/bench_default.log
 if [ $rc -ne 0 ]; then echo "STOP bench rc=$rc"; tail -20 gpurun_out/bench_default.log; exit $rc; fi
 cat gpurun_out/bench_default.json
 bash scripts/gpu_configs.sh || exit $?
-bash scripts/profile.sh
+# rocprofv3 evidence: scripts/profile.sh (its own gpurun call)

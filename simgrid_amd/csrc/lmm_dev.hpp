@@ -157,9 +157,12 @@ __device__ __forceinline__ double dinf() { return __builtin_huge_val(); }
 // 16-bit monotone key: round the ratio down to f32, keep the upper 16 bits (sign, exponent, 7 bits
 // of mantissa).  Monotone non-decreasing, so key(a) < key(b) => a < b; equal keys need the exact
 // fp64 comparison.
+#ifndef LMM_KEY_MANT
+#define LMM_KEY_MANT 7  // mantissa bits of the key (build knob, measurement)
+#endif
 __device__ __forceinline__ uint16_t ratio_key(double r) {
   float f = __double2float_rd(r);
-  return uint16_t(__float_as_uint(f) >> 16);
+  return uint16_t(__float_as_uint(f) >> (23 - LMM_KEY_MANT));
 }
 
 template <int W> __device__ __forceinline__ double grp_min(double v) {

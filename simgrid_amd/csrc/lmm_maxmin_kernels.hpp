@@ -451,6 +451,7 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   const uint16_t prev = uint16_t(round - 1);
   const unsigned long long below = (1ull << lane) - 1;
   int qn = 0, nq = 0;
+  int dg[3] = {0, 0, 0};  // kDiag 1: target-changed / sensitive / queued rows of this lane
   for (int64_t base = wlo; base < whi; base += int64_t(F) * kWave) {  // wave-uniform
     int tt[F];
     unsigned sk[F];
@@ -483,15 +484,10 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
       else if (kBits && cg[u] == prev)
         need = true;
       needm |= unsigned(need) << u;
-      if (kDiag == 1 && s.vstat && round < kStatRounds) {
-        const unsigned long long mc = __ballot(ch[u]), ms = __ballot(tt[u] >= 0 && sk[u] == 0);
-        const unsigned long long mq = __ballot(need);
-        if (lane == 0) {
-          int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
-          atomicAdd(&d[0], __popcll(mc));
-          atomicAdd(&d[1], __popcll(ms));
-          atomicAdd(&d[2], __popcll(mq));
-        }
+      if (kDiag == 1) {
+        dg[0] += ch[u];
+        dg[1] += tt[u] >= 0 && sk[u] == 0;
+        dg[2] += need;
       }
     }
 #pragma unroll 1
@@ -515,13 +511,31 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   __builtin_amdgcn_wave_barrier();
   if (kDiag == 0 && lane < qn)
     vote_row<R>(s, buf, round, qw[lane], st_rows, st_elems);
+  if (kDiag == 1 && s.vstat && round < kStatRounds) {
+    int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
+    for (int k = 0; k < 3; k++) {
+      const int t = grp_isum<kWave>(dg[k]);
+      if (lane == 0 && t)
+        atomicAdd(&d[k], t);
+    }
+  }
   return nq + qn;
+}
+
+constexpr int kBitWords = 17408;  // LDS bitmap capacity of the multi-launch vote: 1,114,112 constraints
+
+// The changed-constraint bitmap into LDS (16 B per thread per step).
+template <int B> __device__ __forceinline__ void load_bits(const Dev& s, uint64_t* bits) {
+  const int n16 = (s.nC + 127) / 128;
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(s.chgbits);
+  uint4* dst = reinterpret_cast<uint4*>(bits);
+  for (int i = threadIdx.x; i < n16; i += B)
+    dst[i] = src[i];
 }
 
 // Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
 // to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
-constexpr int kBitWords = 17408;  // LDS bitmap capacity: 1,114,112 constraints
 template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int buf, int round) {
   if (s.ctl[CTL_DONE])
     return;
@@ -530,13 +544,8 @@ template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B)
   __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
   if (threadIdx.x == 0)
     st_rows = st_elems = 0;
-  if (kBits) {
-    const int n16 = (s.nC + 127) / 128;  // 16-B pieces of the bitmap
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(s.chgbits);
-    uint4* dst = reinterpret_cast<uint4*>(bits);
-    for (int i = threadIdx.x; i < n16; i += B)
-      dst[i] = src[i];
-  }
+  if (kBits)
+    load_bits<B>(s, bits);
   __syncthreads();
   if (kDiag == 2) {  // measurement only: the bitmap load alone, and the changed-constraint count
     if (kBits && blockIdx.x == 0 && s.vstat && round < kStatRounds) {

@@ -169,13 +169,8 @@ template <bool kBits> union PLds {
 // by vote_waves (every wave on its own share, no workgroup barrier after the bitmap load).
 template <bool kBits, int R>
 __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds<kBits>& L, bool count) {
-  if (kBits) {
-    const int n16 = (s.nC + 127) / 128;
-    const uint4* src = reinterpret_cast<const uint4*>(s.chgbits);
-    uint4* dst = reinterpret_cast<uint4*>(L.bits);
-    for (int i = threadIdx.x; i < n16; i += kPB)
-      dst[i] = src[i];
-  }
+  if (kBits)
+    load_bits<kPB>(s, L.bits);
   __syncthreads();
   const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;
   const int64_t lo = int64_t(blockIdx.x) * per;
