@@ -10,11 +10,12 @@
 //   init     usage = sum / max of w/p over the constraint's elements, thread per constraint, sequential in
 //            CSC order like the reference's loop (maxmin.cpp:520-555)
 //   round:   V  kG lanes per variable: exact minimum ratio over its live constraints (ties: smallest id);
-//               a variable whose bound*penalty is below it is fixed at its bound (maxmin.cpp:563-595)
-//            R  kG lanes per constraint: ready iff every live element votes for it (a local minimum)
+//               a variable whose bound*penalty is below it is fixed at its bound (maxmin.cpp:563-595);
+//               each live variable marks the constraints it blocks (votes elsewhere / bound fix), so a live
+//               constraint left unmarked is a local minimum (ready: every live element votes for it)
 //            S  kG lanes per variable voting for a ready constraint: x = ratio / penalty (maxmin.cpp:583);
 //               its decrements go to its other live constraints as fixed-point integers (LDS atomics)
-//            U  thread per constraint: the update of update_wave (clamps, FATPIPE recompute, saturation)
+//            U  thread per constraint: the update of update_groups (clamps, FATPIPE recompute, saturation)
 // Decrements are fixed-point integers (CstRec): results do not depend on the order of the LDS atomics.
 #pragma once
 #include "lmm_dev.hpp"
@@ -23,6 +24,7 @@ namespace lmmdev {
 
 constexpr int kBB = 256;  // threads per workgroup
 constexpr int kG = 4;     // lanes per variable (vote, saturation) and per constraint (ready test)
+constexpr int kSatW = 4;  // weights per lane prefetched by the saturation (rows up to kG * kSatW elements)
 
 // LDS bytes of a workgroup for systems of at most nv variables, nc constraints and nnz elements
 __host__ __device__ inline size_t batch_lds_bytes(int nv, int nc, int nnz) {
@@ -30,7 +32,7 @@ __host__ __device__ inline size_t batch_lds_bytes(int nv, int nc, int nnz) {
              sizeof(unsigned long long) * 3 * size_t(nc) +                         // decrement records
              sizeof(int32_t) * size_t(nc) +                                        // scale exponents
              sizeof(uint16_t) * (size_t(nv) + 1 + size_t(nc) + 1 + 2 * size_t(nnz) + size_t(nv)) +
-             2 * size_t(nc) + size_t(nv);
+             3 * size_t(nc) + size_t(nv);
   return (b + 15) / 16 * 16;
 }
 
@@ -52,9 +54,10 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
   uint16_t* l_cc = l_cp + (max_nc + 1);                           // [max_nnz] CSR local constraint
   uint16_t* l_cv = l_cc + max_nnz;                                // [max_nnz] CSC local variable
   uint16_t* v_vote = l_cv + max_nnz;                              // [max_nv]
-  uint8_t* c_st = reinterpret_cast<uint8_t*>(v_vote + max_nv);    // 0 live, 1 out, 2 ready this round
+  uint8_t* c_st = reinterpret_cast<uint8_t*>(v_vote + max_nv);    // 0 live, 1 out
   uint8_t* c_fl = c_st + max_nc;                                  // FATPIPE
-  uint8_t* v_st = c_fl + max_nc;  // 0 live, 1 done, 2 fixed at its bound this round, 3 saturated this round
+  uint8_t* c_nr = c_fl + max_nc;  // 1 = blocked this round: a live variable on it votes elsewhere or hit its bound
+  uint8_t* v_st = c_nr + max_nc;  // 0 live, 1 done
   int rounds_max = 0;
   for (int64_t sy = blockIdx.x; sy < nsys; sy += gridDim.x) {
     const int64_t vb = var_off[sy], cb = cnst_off[sy];
@@ -83,9 +86,15 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
       const int b = l_cp[c], e = l_cp[c + 1];
       const bool fat = s.cflags[cb + c] & 1;
       double acc = 0.0;
-      for (int k = b; k < e; k++) {
-        const double u = s.csc_u[kb + k];
-        acc = fat ? fmax(acc, u) : acc + u;
+      for (int k0 = b; k0 < e; k0 += 4) {  // four loads in flight, added in CSC order
+        double u[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          u[i] = k0 + i < e ? s.csc_u[kb + k0 + i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (k0 + i < e)
+            acc = fat ? fmax(acc, u[i]) : acc + u[i];
       }
       const double bound = s.cbound[cb + c];
       const bool part = bound > bound * prec;
@@ -99,11 +108,14 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
       c_q[3 * c] = c_q[3 * c + 1] = c_q[3 * c + 2] = 0;
       c_st[c] = alive ? 0 : 1;
       c_fl[c] = fat;
+      c_nr[c] = 0;
     }
     __syncthreads();
     int round = 0;
     for (;; round++) {
-      // ---- V: votes and bound fixes, G lanes per variable ----
+      // ---- V: votes and bound fixes, G lanes per variable; every live variable marks the constraints it
+      // blocks (c_nr): the ones it does not vote for, or all of them when it is fixed at its bound.  A
+      // live constraint nothing blocks is a local minimum: it saturates in S (ready test, maxmin.cpp:578) ----
       for (int v = threadIdx.x / kG; v < nv; v += kBB / kG) {  // uniform within each G-lane group
         const int g = threadIdx.x & (kG - 1);
         const bool in = v_st[v] == 0;
@@ -136,10 +148,11 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
         } else if (vbd > 0 && vbd * p < minr) {  // maxmin.cpp:587-589
           if (g == 0) {
             v_x[v] = vbd;
-            v_st[v] = 2;
+            v_st[v] = 1;
           }
           for (int j = jb + g; j < je; j += kG) {
             const int c = l_cc[j];
+            c_nr[c] = 1;
             const double w = s.csr_w[eb + j];
             if (c_st[c] == 1)
               continue;
@@ -149,46 +162,44 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
               atomicAdd(&c_q[3 * c + 1], dec_q(w / p, cexp_use(c_exp[c])));
             }
           }
-        } else if (g == 0) {
-          v_vote[v] = uint16_t(t);
+        } else {
+          if (g == 0)
+            v_vote[v] = uint16_t(t);
+          for (int j = jb + g; j < je; j += kG) {
+            const int c = l_cc[j];
+            if (c != t)
+              c_nr[c] = 1;
+          }
         }
       }
       __syncthreads();
-      // ---- R: local minima, G lanes per constraint ----
-      for (int c = threadIdx.x / kG; c < nc; c += kBB / kG) {
-        const int g = threadIdx.x & (kG - 1);
-        const bool in = c_st[c] == 0;
-        bool rdy = true;
-        if (in)
-          for (int k = l_cp[c] + g; k < l_cp[c + 1]; k += kG) {
-            const int v = l_cv[k];
-            const int st = v_st[v];
-            rdy &= !(st == 2 || (st == 0 && v_vote[v] != c));
-          }
-#pragma unroll
-        for (int o = 1; o < kG; o <<= 1)
-          rdy &= __shfl_xor(int(rdy), o, kWave) != 0;
-        if (in && rdy && g == 0)
-          c_st[c] = 2;
-      }
-      __syncthreads();
-      // ---- S: saturation of the ready constraints' variables, G lanes per variable ----
+      // ---- S: saturation of the unblocked constraints' variables, G lanes per variable ----
       for (int v = threadIdx.x / kG; v < nv; v += kBB / kG) {
         const int g = threadIdx.x & (kG - 1);
         if (v_st[v] != 0)
           continue;
         const int t = v_vote[v];
-        if (c_st[t] != 2)
+        if (c_nr[t])  // (t is live: v voted for it this round)
           continue;
         const double p = v_pen[v];
         const double x = c_rat[t] / p;
+        const int jb = l_vp[v] + g, je = l_vp[v + 1];
+        double wv[kSatW];  // the group's weights, loads in flight together
+#pragma unroll
+        for (int i = 0; i < kSatW; i++)
+          wv[i] = jb + i * kG < je ? s.csr_w[eb + jb + i * kG] : 0.0;
         if (g == 0) {
           v_x[v] = x;
-          v_st[v] = 3;
+          v_st[v] = 1;
         }
-        for (int j = l_vp[v] + g; j < l_vp[v + 1]; j += kG) {
+        for (int j = jb, i = 0; j < je; j += kG, i++) {
           const int c = l_cc[j];
-          const double w = s.csr_w[eb + j];
+          double w = 0.0;
+#pragma unroll
+          for (int k = 0; k < kSatW; k++)
+            w = i == k ? wv[k] : w;
+          if (i >= kSatW)
+            w = s.csr_w[eb + j];
           if (c == t || c_st[c] == 1)
             continue;
           atomicAdd(&c_q[3 * c + 2], 1ull);
@@ -199,17 +210,17 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
         }
       }
       __syncthreads();
-      // ---- U: constraint update (update_wave's arithmetic) ----
+      // ---- U: constraint update (update_groups' arithmetic); unblocked live constraints saturated ----
       int alive = 0;
       for (int c = threadIdx.x; c < nc; c += kBB) {
-        const int st = c_st[c];
-        if (st == 1)
+        if (c_st[c] == 1)
           continue;
-        if (st == 2) {  // saturated (maxmin.cpp:608-615)
+        if (!c_nr[c]) {  // saturated (maxmin.cpp:608-615)
           c_st[c] = 1;
           c_rat[c] = dinf();
           continue;
         }
+        c_nr[c] = 0;
         const unsigned long long qz = c_q[3 * c + 2];
         if (qz == 0) {
           alive = 1;
@@ -243,9 +254,6 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
           alive = 1;
         }
       }
-      for (int v = threadIdx.x; v < nv; v += kBB)
-        if (v_st[v] >= 2)
-          v_st[v] = 1;
       if (!__syncthreads_or(alive))  // light table empty (maxmin.cpp:680)
         break;
     }
