@@ -121,8 +121,28 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
   }
 }
 
+// The floor of a row that voted for a constraint of key mk: while the target's key stays strictly below
+// it, the vote stands even if the target's ratio moved (keys never decrease).  It is the min key over the
+// row's OTHER constraints (sk) and, for a bounded variable, the key of its level bound * penalty (key[t] <
+// key(b*p) implies ratio[t] < b*p: the bound test of maxmin.cpp:587 stays false).  0 marks a "sensitive"
+// row whose vote depends on the target's exact ratio (a key-level tie with another constraint or with the
+// bound level), re-evaluated whenever the target is touched.
+__device__ __forceinline__ unsigned row_floor(unsigned sk, unsigned mk, double vb, double p) {
+  unsigned fl = sk;
+  if (vb > 0)
+    fl = min(fl, (unsigned)ratio_key(vb * p));
+  return fl <= mk ? 0u : fl;
+}
+
+// FATPIPE constraints (maxmin.cpp:625-658): usage = max of w/p over the unfixed elements.  A fixed element
+// pushes its w/p into the record's duse slot with an unsigned max of the (non-negative) double's bits;
+// mm_update recomputes the max over the CSC only when a removed element reached the current usage — the
+// max over the remaining elements is unchanged otherwise.
+__device__ __forceinline__ unsigned long long fat_bits(double u) { return (unsigned long long)__double_as_longlong(u); }
+
 // Decrements of a fixed variable's element j (maxmin.cpp:601-606) into the constraint's record, as
-// fixed-point integers (CstRec); FATPIPE constraints only count.  One lane issues all three (rare paths).
+// fixed-point integers (CstRec); FATPIPE constraints get the count and the removed w/p (fat_bits).  One lane
+// issues them all (rare path: bound fixes in the vote).
 __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double xv, double p) {
   const int32_t c = s.csr_c[j];
   if (s.key[c] == kDeadKey)
@@ -130,11 +150,13 @@ __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double 
   unsigned long long* r = &s.cst[c].drem;
   s.ctouch[c] = 1;  // receives decrements this round (mm_update reads its record)
   atomicAdd(&r[2], 1ull);  // fixed elements leaving c (mm_update subtracts them from nvote)
+  const double w = s.csr_w[j];
   if (!(s.cflags[c] & 1)) {
-    const double w = s.csr_w[j];
     const int32_t ce = s.cexp[c];
     atomicAdd(&r[0], dec_q(w * xv, cexp_rem(ce)));
     atomicAdd(&r[1], dec_q(w / p, cexp_use(ce)));
+  } else {
+    atomicMax(&r[1], fat_bits(w / p));
   }
 }
 
@@ -242,8 +264,8 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
           sk = min(sk, (unsigned)key[c]);
       }
       sk = grp_umin<G>(sk);
-      if (live && !bounded && g == 0)  // 0 = "sensitive" row (bounded, or key-level tie: see vote_row)
-        s.skey[buf][row] = (vb > 0 || sk == mk) ? 0 : uint16_t(sk);
+      if (live && !bounded && g == 0)  // the row's floor, 0 = "sensitive" (see vote_row)
+        s.skey[buf][row] = uint16_t(row_floor(sk, mk, vb, p));
       int mult_new = h0 && c0 == newt, mult_old = h0 && c0 == t;
       for (uint32_t j = j0 + G; j < e; j += G) {
         const int32_t c = ccol[j];
@@ -403,11 +425,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     if (c != newt)
       sk = min(sk, (unsigned)key[c]);
   }
-  // skey = the row's floor: the min key over its OTHER constraints (keys never decrease, so while the
-  // target's key stays below it the vote stands even if the target's ratio moved).  0 marks a
-  // "sensitive" row whose vote depends on the target's exact ratio — a bounded variable (the bound test
-  // reads it) or a key-level tie broken by exact ratios — re-evaluated whenever the target is touched.
-  skey[row] = (vb > 0 || sk == mk) ? 0 : uint16_t(sk);
+  skey[row] = uint16_t(row_floor(sk, mk, vb, p));
   if (newt == t)
     return;
   int mult_new = 0;
@@ -682,7 +700,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
         const double w = s.csr_w[kk[u]];
         const int32_t ce = s.cexp[cc[u]];
         a0[u] = (long long)dec_q(w * ox, cexp_rem(ce));
-        a1[u] = (long long)dec_q(w / op, cexp_use(ce));
+        a1[u] = fat[u] ? (long long)fat_bits(w / op) : (long long)dec_q(w / op, cexp_use(ce));
       }
     }
 #pragma unroll
@@ -699,6 +717,8 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
         const long long e1 = __shfl(a1[u], e, kWave);
         if (ec >= 0 && q < 3 && (!ef || q == 2))
           atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
+        if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
+          atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
       }
     }
   }
@@ -935,8 +955,10 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     const bool live = live0 && !sat;
     const bool tch = live && tf[k] == 1;
     const bool fat = tch && (fl[k] & 1);
-    double fuse = 0.0;
-    unsigned long long fm = __ballot(fat);
+    // FATPIPE: recompute only when a removed element reached the usage (fat_bits in duse)
+    const bool fre = fat && !(__longlong_as_double((long long)qy[k]) < use[k]);
+    double fuse = use[k];
+    unsigned long long fm = __ballot(fre);
     while (fm) {  // wave-uniform: FATPIPE usage over the still-unfixed elements (maxmin.cpp:625-658)
       const int l = __ffsll((long long)fm) - 1;
       fm &= fm - 1;
