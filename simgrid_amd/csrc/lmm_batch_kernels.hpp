@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
       c_use[c] = usage;
       c_bnd[c] = bound;
       c_rat[c] = alive ? bound / usage : dinf();
-      c_exp[c] = alive ? int32_t((uint32_t(uint16_t(dec_scale(usage))) << 16) | uint16_t(dec_scale(bound))) : 0;
+      c_exp[c] = cexp_pack(alive ? dec_scale(bound) : 0, alive ? dec_scale(usage) : 0, fat, !alive);
       c_q[3 * c] = c_q[3 * c + 1] = c_q[3 * c + 2] = 0;
       c_st[c] = alive ? 0 : 1;
       c_fl[c] = fat;

@@ -69,9 +69,17 @@ __device__ __forceinline__ unsigned long long dec_q(double d, int s) {
 __device__ __forceinline__ double dec_val(unsigned long long q, int s) {
   return __builtin_amdgcn_ldexp(double((long long)q), -s);
 }
-// packed per-constraint scale exponents: low 16 bits srem, high 16 bits suse
-__device__ __forceinline__ int cexp_rem(int32_t e) { return int(int16_t(e & 0xFFFF)); }
-__device__ __forceinline__ int cexp_use(int32_t e) { return int(int16_t(uint32_t(e) >> 16)); }
+// Packed per-constraint word (cexp): bits 0-11 srem, 12-23 suse (signed: dec_scale stays within +-1000),
+// bit 24 FATPIPE, bit 25 out of the light table.  A saturation pushing into constraint c reads this one word
+// (scales, policy, liveness) instead of three arrays.
+constexpr int32_t kCexpFat = 1 << 24;
+constexpr int32_t kCexpDead = 1 << 25;
+__host__ __device__ __forceinline__ int32_t cexp_pack(int srem, int suse, bool fat, bool dead) {
+  return int32_t((uint32_t(srem) & 0xFFFu) | ((uint32_t(suse) & 0xFFFu) << 12)) | (fat ? kCexpFat : 0) |
+         (dead ? kCexpDead : 0);
+}
+__device__ __forceinline__ int cexp_rem(int32_t e) { return int32_t(uint32_t(e) << 20) >> 20; }
+__device__ __forceinline__ int cexp_use(int32_t e) { return int32_t(uint32_t(e) << 8) >> 20; }
 
 // Relaxed agent-scope load: always a vector (global) load, never the scalar cache — for words other
 // workgroups write inside a persistent launch (MI355X_MICROARCH.md, inter-workgroup visibility).
@@ -113,7 +121,7 @@ struct Dev {
   double* rem;      // [nC]
   double* use;      // [nC]
   CstRec* cst;      // [nC] maxmin: per-constraint record (one 64-B line, see CstRec)
-  int32_t* cexp;    // [nC] maxmin: fixed-point scale exponents of the decrements (cexp_rem / cexp_use)
+  int32_t* cexp;    // [nC] maxmin: scale exponents of the decrements, FATPIPE and out flags (cexp_pack)
   // [nC] maxmin: alive elements whose variable votes for ANOTHER constraint (dense: mm_ready reads it
   // for every alive constraint each round); ready iff 0.  Vote moves add/subtract the moving
   // variable's multiplicity, fixed elements leave through the record's count in mm_update.

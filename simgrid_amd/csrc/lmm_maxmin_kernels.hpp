@@ -88,7 +88,7 @@ __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64
       s.cst[c] = rec;
       // fixed-point scales of this solve's decrements (CstRec): a round never removes more than the
       // remaining (<= bound) or the usage (<= initial usage) from a constraint
-      s.cexp[c] = alive ? int32_t((uint32_t(uint16_t(dec_scale(usage))) << 16) | uint16_t(dec_scale(bound))) : 0;
+      s.cexp[c] = cexp_pack(alive ? dec_scale(bound) : 0, alive ? dec_scale(usage) : 0, fat, !alive);
       s.nvote[c] = int32_t(e - b);  // no element votes yet
       s.chg[c] = uint16_t(0xFFFF);
       s.key[c] = alive ? ratio_key(r) : uint16_t(kDeadKey);
@@ -145,14 +145,14 @@ __device__ __forceinline__ unsigned long long fat_bits(double u) { return (unsig
 // issues them all (rare path: bound fixes in the vote).
 __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double xv, double p) {
   const int32_t c = s.csr_c[j];
-  if (s.key[c] == kDeadKey)
+  const int32_t ce = s.cexp[c];
+  if (ce & kCexpDead)
     return;
   unsigned long long* r = &s.cst[c].drem;
   s.ctouch[c] = 1;  // receives decrements this round (mm_update reads its record)
   atomicAdd(&r[2], 1ull);  // fixed elements leaving c (mm_update subtracts them from nvote)
   const double w = s.csr_w[j];
-  if (!(s.cflags[c] & 1)) {
-    const int32_t ce = s.cexp[c];
+  if (!(ce & kCexpFat)) {
     atomicAdd(&r[0], dec_q(w * xv, cexp_rem(ce)));
     atomicAdd(&r[1], dec_q(w / p, cexp_use(ce)));
   } else {
@@ -692,13 +692,13 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       const double op = __shfl(lp, ol[u], kWave);
       fat[u] = false;
       a0[u] = a1[u] = 0;
-      if (cc[u] >= 0 && (cc[u] == c || s.key[cc[u]] == kDeadKey))
+      const int32_t ce = cc[u] >= 0 ? s.cexp[cc[u]] : kCexpDead;  // scales, policy and liveness in one word
+      if (cc[u] >= 0 && (cc[u] == c || (ce & kCexpDead)))
         cc[u] = -1;
       if (cc[u] >= 0) {
         s.ctouch[cc[u]] = 1;  // receives decrements this round (mm_update reads its record)
-        fat[u] = s.cflags[cc[u]] & 1;
+        fat[u] = ce & kCexpFat;
         const double w = s.csr_w[kk[u]];
-        const int32_t ce = s.cexp[cc[u]];
         a0[u] = (long long)dec_q(w * ox, cexp_rem(ce));
         a1[u] = fat[u] ? (long long)fat_bits(w / op) : (long long)dec_q(w / op, cexp_use(ce));
       }
@@ -922,14 +922,12 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
   unsigned long long qx[K], qy[K], qz[K];
   double rem[K], use[K], bnd[K];
   int32_t ce[K], nv[K];
-  uint8_t fl[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int64_t c = base0 + k * stride + lane;
     qx[k] = qy[k] = qz[k] = 0;
     rem[k] = use[k] = bnd[k] = 0.0;
     ce[k] = nv[k] = 0;
-    fl[k] = 0;
     if (okey[k] != kDeadKey && tf[k] == 1) {  // an untouched constraint keeps its record as it is
       const CstRec* rec = s.cst + c;
       qx[k] = rec->drem;
@@ -940,7 +938,6 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       bnd[k] = rec->bound;
       ce[k] = s.cexp[c];
       nv[k] = s.nvote[c];
-      fl[k] = s.cflags[c];
     }
   }
   int alive = 0;
@@ -954,7 +951,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     const bool sat = live0 && tf[k] == 2;
     const bool live = live0 && !sat;
     const bool tch = live && tf[k] == 1;
-    const bool fat = tch && (fl[k] & 1);
+    const bool fat = tch && (ce[k] & kCexpFat);
     // FATPIPE: recompute only when a removed element reached the usage (fat_bits in duse)
     const bool fre = fat && !(__longlong_as_double((long long)qy[k]) < use[k]);
     double fuse = use[k];
@@ -976,6 +973,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     CstRec* rec = s.cst + c;
     if (sat) {
       s.key[c] = kDeadKey;
+      s.cexp[c] = kCexpDead;
       s.chg[c] = uint16_t(round);
       s.ctouch[c] = 0;
       rec->ratio = dinf();
@@ -1005,6 +1003,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
         if (!(u0 > prec) || !(r0 > bnd[k] * prec)) {
           rec->ratio = dinf();
           s.key[c] = kDeadKey;
+          s.cexp[c] = kCexpDead;
           changed = true;
         } else {
           const double r = r0 / u0;
