@@ -156,6 +156,11 @@ struct Dev {
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };
 
+// Alive-row variable ids carry the variable's "bounded" flag in the sign bit (set at every solve's init),
+// so the re-vote of an unbounded variable skips its bound and penalty gathers.
+__device__ __forceinline__ int rvar(int32_t cv) { return cv & 0x7FFFFFFF; }
+__device__ __forceinline__ bool rbounded(int32_t cv) { return cv < 0; }
+
 constexpr int kStatRounds = 4096;  // rounds covered by the profiling counters
 constexpr int32_t kUnvoted = -1;   // row target: not evaluated yet
 constexpr int32_t kRetired = -2;   // row target: variable fixed or dropped (skip until compaction)

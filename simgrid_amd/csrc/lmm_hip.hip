@@ -1238,11 +1238,11 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   Dev d = c->d;
   d.vstat = nullptr;
   const bool bits = int64_t(d.nC) <= int64_t(kPBitWords) * 64;
-  // registers per row in the re-vote: 8, or 12 for longer mean rows (C4's LV08 routes: 11.7 elements)
+  // registers per row in the re-vote: 8, or 10 for longer mean rows (C4's LV08 routes: 11.7 elements)
   const bool r16 = c->group > 8;
-  const void* kern = bits ? (r16 ? reinterpret_cast<const void*>(&mm_persist<true, 12>)
+  const void* kern = bits ? (r16 ? reinterpret_cast<const void*>(&mm_persist<true, 10>)
                                  : reinterpret_cast<const void*>(&mm_persist<true, 8>))
-                          : (r16 ? reinterpret_cast<const void*>(&mm_persist<false, 12>)
+                          : (r16 ? reinterpret_cast<const void*>(&mm_persist<false, 10>)
                                  : reinterpret_cast<const void*>(&mm_persist<false, 8>));
   if (!c->pbar)
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->pbar), BAR_WORDS * sizeof(unsigned)));

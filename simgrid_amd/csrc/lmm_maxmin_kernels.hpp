@@ -110,6 +110,7 @@ __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t
     s.x[v] = 0.0;
     s.vstate[v] = 0;
     s.rtgt[0][v] = kUnvoted;
+    const_cast<int32_t*>(s.cvar[0])[v] = int32_t(v) | (s.vbound[v] > 0 ? int32_t(0x80000000u) : 0);
   }
 }
 
@@ -202,7 +203,7 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
       const int src = pos < 0 ? 0 : pos;
       const int t = __shfl(lt, src, kWave);
       const int64_t row = base + src;
-      const int v = pos >= 0 ? cvar[row] : 0;
+      const int v = pos >= 0 ? rvar(cvar[row]) : 0;
       bool need = pos >= 0;
       if (need && s.vstate[v] != 0) {  // fixed by mm_saturate since: retire the row
         if (g == 0)
@@ -339,11 +340,13 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   uint16_t* __restrict__ skey = s.skey[buf];
   const uint16_t* __restrict__ key = s.key;
   const int t = rtgt[row];
-  const int v = cvar[row];
+  const int32_t cv = cvar[row];
+  const int v = rvar(cv);
   const uint32_t b = crow[row], e = crow[row + 1];
   const int32_t vst = s.vstate[v];
-  const double vb = s.vbound[v];
-  const double p = s.pen[v];
+  const bool bnd = rbounded(cv);
+  const double vb = bnd ? s.vbound[v] : -1.0;
+  const double p = bnd ? s.pen[v] : 1.0;  // read below only when vb > 0
   if (vst != 0) {  // fixed by a saturation since: retire the row
     rtgt[row] = kRetired;
     return;
@@ -1118,7 +1121,7 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int* sh) {  // exclu
 }
 
 __device__ __forceinline__ bool row_alive(const Dev& s, int in, int64_t row) {
-  return s.vstate[s.cvar[in][row]] == 0;
+  return s.vstate[rvar(s.cvar[in][row])] == 0;
 }
 
 __global__ void __launch_bounds__(kBlock) cmp_count(Dev s, int in) {
@@ -1219,20 +1222,20 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
   int32_t* __restrict__ ocol = const_cast<int32_t*>(s.ccol[out]);
   for (int k = 0; k < kRowsPerThread; k++) {
     const int64_t row = base + int64_t(k) * kBlock + threadIdx.x;
-    int32_t v = -1;
+    int32_t v = 0;  // (bounded flag kept)
+    bool al = false;
     uint32_t b = 0, e = 0;
     if (row < nrows) {
       v = s.cvar[in][row];
-      if (s.vstate[v] == 0) {
+      al = s.vstate[rvar(v)] == 0;
+      if (al) {
         b = s.crow[in][row];
         e = s.crow[in][row + 1];
-      } else {
-        v = -1;
       }
     }
-    int xr = v >= 0, xe = int(e - b), tr, te;
+    int xr = al, xe = int(e - b), tr, te;
     block_scan_pair(xr, xe, tr, te);
-    if (v >= 0) {
+    if (al) {
       const int o = pr + xr;
       ovar[o] = v;
       s.rtgt[out][o] = s.rtgt[in][row];

@@ -202,7 +202,7 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
   int nr = 0, ne = 0;  // pass 1
   for (int64_t row = lo + threadIdx.x; row < hi; row += kPB)
-    if (s.vstate[s.cvar[in][row]] == 0) {
+    if (s.vstate[rvar(s.cvar[in][row])] == 0) {
       nr++;
       ne += int(s.crow[in][row + 1] - s.crow[in][row]);
     }
@@ -230,18 +230,18 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
   __syncthreads();
   for (int64_t b0 = lo; b0 < hi; b0 += kPB) {  // pass 2, workgroup-uniform
     const int64_t row = b0 + threadIdx.x;
-    int32_t v = -1;
+    int32_t v = 0;  // (bounded flag kept)
+    bool al = false;
     uint32_t b = 0, e = 0;
     if (row < hi) {
       v = s.cvar[in][row];
-      if (s.vstate[v] == 0) {
+      al = s.vstate[rvar(v)] == 0;
+      if (al) {
         b = s.crow[in][row];
         e = s.crow[in][row + 1];
-      } else {
-        v = -1;
       }
     }
-    int xr = v >= 0, xe = int(e - b);
+    int xr = al, xe = int(e - b);
     int ir = xr, ie = xe;  // inclusive wave scans
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -263,7 +263,7 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
       tr += sh[2 * i];
       te += sh[2 * i + 1];
     }
-    if (v >= 0) {
+    if (al) {
       const uint32_t o = rbase + uint32_t(orr + ir - xr);
       const uint32_t dst = ebase + uint32_t(oe + ie - xe);
       ovar[o] = v;
