@@ -68,6 +68,36 @@ __global__ void push_b2(const int* __restrict__ idx, const double* __restrict__ 
   }
 }
 
+// B as the product issues it (u64 fixed-point adds, agent scope), and E: the same into a per-XCD replica of the
+// records with WORKGROUP-scope atomics (performed in the XCD's own L2?), replicas summed afterwards.
+__device__ __forceinline__ unsigned xcc_id_() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v & 7u;
+}
+template <int kScope>
+__global__ void push_u64(const int* __restrict__ idx, const double* __restrict__ w, long n, unsigned long long* rec,
+                         long nc) {
+  const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int q = threadIdx.x & 3;
+  unsigned long long* base = kScope == __HIP_MEMORY_SCOPE_WORKGROUP ? rec + 4 * nc * long(xcc_id_()) : rec;
+  for (long t = tid; t < 4 * n; t += (long)gridDim.x * blockDim.x) {
+    const long i = t >> 2;
+    const int c = idx[i];
+    const double x = w[i];
+    const unsigned long long v = q == 0 ? (unsigned long long)(x * 1024) : q == 1 ? (unsigned long long)(x * 4096) : 1ull;
+    if (q < 3)
+      __hip_atomic_fetch_add(&base[4 * long(c) + q], v, __ATOMIC_RELAXED, kScope);
+  }
+}
+__global__ void sum_cnt(const unsigned long long* rec, long nc, int nrep, unsigned long long* out) {
+  unsigned long long s = 0;
+  for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < nc; c += (long)gridDim.x * blockDim.x)
+    for (int r = 0; r < nrep; r++)
+      s += rec[4 * nc * r + 4 * c + 2];
+  atomicAdd(out, s);
+}
+
 __global__ void store_d(const int* __restrict__ idx, const double* __restrict__ w, long n, double* tab) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     tab[idx[i]] = w[i];
@@ -137,6 +167,28 @@ int main() {
     printf("grid %5d  %ld elems -> %ld cnsts: A 3 arrays %.3f ms (%.2e el/s)  B 4-lane record %.3f ms (%.2e el/s)"
            "  C 1-lane record %.3f ms  B2 2-lane pair %.3f ms  D plain store %.3f ms\n",
            grid, n, nc, ta, n / ta * 1e3, tb, n / tb * 1e3, tc, tb2, td);
+  }
+  {
+    unsigned long long *rep, *cnt;
+    CHK(hipMalloc(&rep, 8 * nc * 32));
+    CHK(hipMalloc(&cnt, 8));
+    for (int grid : {2048, 8192}) {
+      CHK(hipMemset(rep, 0, 8 * nc * 32));
+      float tf = time([&] { push_u64<__HIP_MEMORY_SCOPE_AGENT><<<grid, block>>>(d_idx, d_w, n, rep, nc); });
+      CHK(hipMemset(cnt, 0, 8));
+      sum_cnt<<<1024, 256>>>(rep, nc, 1, cnt);
+      unsigned long long hf = 0;
+      CHK(hipMemcpy(&hf, cnt, 8, hipMemcpyDeviceToHost));
+      CHK(hipMemset(rep, 0, 8 * nc * 32));
+      float te = time([&] { push_u64<__HIP_MEMORY_SCOPE_WORKGROUP><<<grid, block>>>(d_idx, d_w, n, rep, nc); });
+      CHK(hipMemset(cnt, 0, 8));
+      sum_cnt<<<1024, 256>>>(rep, nc, 8, cnt);
+      unsigned long long he = 0;
+      CHK(hipMemcpy(&he, cnt, 8, hipMemcpyDeviceToHost));
+      printf("grid %5d u64 quad pushes: agent scope %.3f ms (%.2e el/s, count %llu / %ld)  workgroup scope into"
+             " per-XCD replicas %.3f ms (%.2e el/s, count %llu / %ld)\n",
+             grid, tf, n / tf * 1e3, hf, 4 * n, te, n / te * 1e3, he, 4 * n);
+    }
   }
   {
     std::vector<int> hv(n);

@@ -31,6 +31,10 @@ enum : int {
   CTL_PALIVE0 = 17,  // persistent maxmin: constraints alive after round r's update, per round parity (2 words)
   CTL_ERR = 19,      // persistent kernels: 1 = grid-barrier timeout, 2 = round guard
   CTL_RESEVAL = 20,  // persistent maxmin (profiling): rows re-evaluated by the vote, summed over the solve
+  // multi-launch maxmin: the buffers in use live on the device, so a compaction needs no host round trip
+  CTL_BUF = 21,    // alive-row buffer of the next vote (0 = the CSR, 1 / 2 = compaction targets)
+  CTL_CB = 22,     // alive-constraint list in use (0 / 1)
+  CTL_CMPGO = 23,  // the last compaction count found the rewrite worth it (cmp_scan -> cmp_write, mm_flip)
   CTL_WORDS = 32
 };
 

@@ -66,7 +66,8 @@ struct lmmhip_ctx {
   hipStream_t own_stream = nullptr;  // the context's own stream (lmmhip_ctx_set_stream(nullptr))
   Dev d{};
   std::vector<void*> allocs;  // owned device allocations
-  int32_t* h_ctl = nullptr;   // pinned mirror of the control words
+  int32_t* h_ctl = nullptr;   // pinned mirror of the control words (+ 2 slots: pipelined polls of solve_maxmin)
+  hipEvent_t ev_poll[2] = {nullptr, nullptr};  // completion of the pipelined control-word copies
   bool uploaded = false;
   bool profiling = false;
   int group = 8;  // lanes per row in mm_vote (power of two >= mean row length, <= 64)
@@ -192,7 +193,11 @@ int lmmhip_ctx_create(int device, lmmhip_ctx** out) {
     e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   c->stream = c->own_stream;
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&c->h_ctl, CTL_WORDS * sizeof(int32_t), hipHostMallocDefault);
+    e = hipHostMalloc((void**)&c->h_ctl, 3 * CTL_WORDS * sizeof(int32_t), hipHostMallocDefault);
+  if (e == hipSuccess)
+    e = hipEventCreateWithFlags(&c->ev_poll[0], hipEventDisableTiming);
+  if (e == hipSuccess)
+    e = hipEventCreateWithFlags(&c->ev_poll[1], hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipEventCreate(&c->ev0);
   if (e == hipSuccess)
@@ -238,6 +243,9 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipHostFree(c->pin_rst);
   if (c->h_ctl)
     (void)hipHostFree(c->h_ctl);
+  for (hipEvent_t ev : c->ev_poll)
+    if (ev)
+      (void)hipEventDestroy(ev);
   if (c->vstat)
     (void)hipFree(c->vstat);
   if (c->pbar)
@@ -1103,7 +1111,9 @@ static int poll_ctl(lmmhip_ctx* c) {
   return 0;
 }
 
-static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
+// The alive-row buffer in use is read by the vote on the device (ctl CTL_BUF); nrows (an upper bound of its
+// rows, refreshed at every poll) only sizes the grid-stride variants' grids.
+static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
   const Dev& d = c->d;
   const int G = c->group;
   const int grid = grid_for(nrows, kBlock);  // one lane per row in the work-queue scan
@@ -1112,22 +1122,22 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int buf) {
   case 8:  // short rows: one lane per row (more gathers in flight per wave)
     if (int64_t(d.nC) <= int64_t(kBitWords) * 64) {
       if (c->profiling && c->vote_diag) {  // measurement: bitmap load alone, filter alone (slot 7)
-        LAUNCH(7, r + 1000000, (mm_vote_lane<kVBlock, true, 2>), c->n_cu, kVBlock, d, buf, int(r));
-        LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, buf, int(r));
+        LAUNCH(7, r + 1000000, (mm_vote_lane<kVBlock, true, 2>), c->n_cu, kVBlock, d, int(r));
+        LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
       }
-      LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, buf, int(r));
+      LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, int(r));
     } else {
-      LAUNCH(2, r, (mm_vote_lane<kBlock, false>), grid, kBlock, d, buf, int(r));
+      LAUNCH(2, r, (mm_vote_lane<kBlock, false>), grid, kBlock, d, int(r));
     }
     break;
   case 16:
-    LAUNCH(2, r, mm_vote<16>, grid, kBlock, d, buf, int(r));
+    LAUNCH(2, r, mm_vote<16>, grid, kBlock, d, int(r));
     break;
   case 32:
-    LAUNCH(2, r, mm_vote<32>, grid, kBlock, d, buf, int(r));
+    LAUNCH(2, r, mm_vote<32>, grid, kBlock, d, int(r));
     break;
   default:
-    LAUNCH(2, r, mm_vote<64>, grid, kBlock, d, buf, int(r));
+    LAUNCH(2, r, mm_vote<64>, grid, kBlock, d, int(r));
     break;
   }
   return 0;
@@ -1146,7 +1156,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int gC = grid_for(d.nC, kBlock);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, mm_init_vars, grid_for(d.nV, kBlock), kBlock, d);
-  LAUNCH(1, -1, mm_clist, gC, kBlock, d, 0, 0, 1);
+  LAUNCH(1, -1, mm_clist, std::min(gC, 2 * c->n_cu), kBlock, d, 1);
   HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
   // Launch-width caps (tuning knobs, environment; 0 = uncapped): fewer blocks cut the fixed per-round
   // cost of the grid-stride round kernels once the alive set is small.
@@ -1156,63 +1166,70 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
   // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
   // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
+  // Both decide and switch buffers on the device (ctl CTL_BUF / CTL_CB): no host round trip.
   const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 32);
   const int cmp_pct = env_int("LMMHIP_COMPACT_PCT", 75);
   const int cl_every = env_int("LMMHIP_CLIST_EVERY", 8);
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
+  // Host view of the sizes (upper bounds: rows and constraints only leave), refreshed at every poll; they
+  // size grids only, the kernels read the exact counts from the control words.
   int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
-  int buf = 0, cb = 0, chunk = 2;
+  // Termination polls are pipelined: the control words after chunk k are copied into a pinned slot behind
+  // an event, chunk k+1 is queued, then the host waits for chunk k's copy — the GPU never idles on the
+  // host.  A chunk queued after the last round is a run of launches that return at once (CTL_DONE).
+  int chunk = 2, slot = 0;
+  bool pending = false;
+  int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
   for (;;) {
     const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
-      if (int rc = launch_vote(c, r, nrows, buf))
+      if (int rc = launch_vote(c, r, nrows))
         return rc;
-      LAUNCH(3, r, mm_ready, gL, kBlock, d, cb);
+      LAUNCH(3, r, mm_ready, gL, kBlock, d);
       if (c->sat_waves == 1)
-        LAUNCH(4, r, mm_saturate<1>, capped(gL, cap_sat), kBlock, d, int(r), cb, gL);
+        LAUNCH(4, r, mm_saturate<1>, capped(gL, cap_sat), kBlock, d, int(r), gL);
       else if (c->sat_waves == 2)
-        LAUNCH(4, r, mm_saturate<2>, capped(grid_for(2 * ncl, kBlock), cap_sat), kBlock, d, int(r), cb, gL);
+        LAUNCH(4, r, mm_saturate<2>, capped(grid_for(2 * ncl, kBlock), cap_sat), kBlock, d, int(r), gL);
       else
-        LAUNCH(4, r, mm_saturate<4>, capped(grid_for(4 * ncl, kBlock), cap_sat), kBlock, d, int(r), cb, gL);
+        LAUNCH(4, r, mm_saturate<4>, capped(grid_for(4 * ncl, kBlock), cap_sat), kBlock, d, int(r), gL);
       LAUNCH(5, r, mm_update, gU, kBlock, d, int(r), prec);
     }
     LAUNCH(6, r, mm_done, 1, kBlock, d, gU);
-    if (int rc = poll_ctl(c))
-      return rc;
-    if (c->h_ctl[CTL_DONE])
-      break;
-    if (r > max_rounds)
-      return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
+    bool cl = false, cm = false;
     if (r - last_clist >= cl_every && ncl > 4096) {  // alive-constraint list (order not preserved)
-      const int out = cb ^ 1;
-      HIPCHK(hipMemsetAsync(d.ctl + CTL_NCL0 + out, 0, sizeof(int32_t), c->stream));
-      LAUNCH(6, r, mm_clist, gL, kBlock, d, cb, out, 0);
-      cb = out;
+      LAUNCH(6, r, mm_clist, std::min(gL, 2 * c->n_cu), kBlock, d, 0);
       last_clist = r;
-      if (int rc = poll_ctl(c))
-        return rc;
-      ncl = c->h_ctl[CTL_NCL0 + cb];
+      cl = true;
     }
     if (r - last_compact >= cmp_every && nrows > 4096) {  // order-preserving compaction of the alive rows
-      const int out = buf == 1 ? 2 : 1;
       const int nblk = int((nrows + kCompactRows - 1) / kCompactRows);
-      LAUNCH(6, r, cmp_count, nblk, kBlock, d, buf);
-      LAUNCH(6, r, cmp_scan, 1, 1024, d, nblk, out);
-      if (int rc = poll_ctl(c))
-        return rc;
-      const int64_t alive_rows = c->h_ctl[CTL_NROWS + out];
-      if (alive_rows * 100 < nrows * cmp_pct) {  // worth rewriting
-        LAUNCH(6, r, cmp_write, nblk, kBlock, d, buf, out);
-        nrows = alive_rows;
-        buf = out;
-      }
+      LAUNCH(6, r, cmp_count, nblk, kBlock, d);
+      LAUNCH(6, r, cmp_scan, 1, 1024, d, nblk, cmp_pct);
+      LAUNCH(6, r, cmp_write, nblk, kBlock, d);
       last_compact = r;
+      cm = true;
     }
+    if (cl || cm)
+      LAUNCH(6, r, mm_flip, 1, 1, d, int(cl), int(cm));
+    HIPCHK(hipMemcpyAsync(hc[slot], d.ctl, CTL_WORDS * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
+    if (pending) {  // the previous chunk's words (this chunk is queued behind them)
+      HIPCHK(hipEventSynchronize(c->ev_poll[slot ^ 1]));
+      const int32_t* h = hc[slot ^ 1];
+      if (h[CTL_DONE])
+        break;
+      ncl = h[CTL_NCL0 + h[CTL_CB]];
+      nrows = h[CTL_NROWS + h[CTL_BUF]];
+    }
+    pending = true;
+    slot ^= 1;
+    if (r > max_rounds)
+      return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
     if (chunk < 16)
       chunk *= 2;
   }
-  return 0;
+  return poll_ctl(c);  // (the queued tail has run: final words for the stats)
 }
 
 static int engine_of(const lmmhip_ctx* c) {

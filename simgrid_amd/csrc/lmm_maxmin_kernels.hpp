@@ -163,9 +163,10 @@ __device__ __forceinline__ void push_decrement(const Dev& s, uint32_t j, double 
 
 // Round phase 1 — (re-)vote.  G lanes per alive row; loops are wave-uniform so the group shuffles
 // always see their whole group.
-template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int buf, int round) {
+template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int round) {
   if (s.ctl[CTL_DONE])  // light table empty (maxmin.cpp:680), detected by mm_done
     return;
+  const int buf = s.ctl[CTL_BUF];
   __shared__ int st_rows, st_elems;  // profiling counters (LDS, one store per block)
   if (s.vstat && threadIdx.x == 0)
     st_rows = st_elems = 0;
@@ -307,18 +308,71 @@ template <int G> __global__ void __launch_bounds__(kBlock) mm_vote(Dev s, int bu
   }
 }
 
-// Alive-constraint list: built at init, re-compacted with the rows (order not preserved).
-__global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int in, int out, int from_all) {
+// Alive-constraint list: built at init (from_all: every constraint id into list 0), then re-compacted from the
+// list in use (ctl CTL_CB) into the other one (order not preserved; mm_flip switches).  One contiguous range
+// per block: count, ONE atomic per block for its output range, write (a counter per 256 entries cost ~44 us
+// of contended atomics on C2).
+__global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int from_all) {
+  if (!from_all && s.ctl[CTL_DONE])
+    return;
+  __shared__ int wsum[kBlock / kWave];
+  __shared__ int base_sh;
+  const int in = from_all ? 0 : s.ctl[CTL_CB], out = from_all ? 0 : in ^ 1;
   const int64_t n = from_all ? s.nC : s.ctl[CTL_NCL0 + in];
-  for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
-    const int64_t i = base + threadIdx.x;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = int64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int cnt = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+    const int32_t c = from_all ? int32_t(i) : s.clist[in][i];
+    cnt += s.key[c] != kDeadKey;
+  }
+  cnt = grp_isum<kWave>(cnt);
+  if (lane == 0)
+    wsum[w] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int k = 0; k < kBlock / kWave; k++)
+      t += wsum[k];
+    base_sh = t ? atomicAdd(&s.ctl[CTL_NCL0 + out], t) : 0;
+  }
+  __syncthreads();
+  int pos = base_sh;
+  for (int64_t b0 = lo; b0 < hi; b0 += kBlock) {  // block-uniform
+    const int64_t i = b0 + threadIdx.x;
     int32_t c = -1;
-    if (i < n)
+    if (i < hi)
       c = from_all ? int32_t(i) : s.clist[in][i];
     const bool alive = c >= 0 && s.key[c] != kDeadKey;
-    const int pos = block_append(alive, &s.ctl[CTL_NCL0 + out]);
+    const unsigned long long m = __ballot(alive);
+    __syncthreads();
+    if (lane == 0)
+      wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = pos, tot = 0;
+    for (int k = 0; k < kBlock / kWave; k++) {
+      off += k < w ? wsum[k] : 0;
+      tot += wsum[k];
+    }
     if (alive)
-      s.clist[out][pos] = c;
+      s.clist[out][off + __popcll(m & ((1ull << lane) - 1))] = c;
+    pos += tot;
+  }
+}
+
+// After a list re-compaction and / or a row compaction: switch the buffers in use (one thread).
+__global__ void mm_flip(Dev s, int clist, int rows) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (clist) {
+    const int in = s.ctl[CTL_CB];
+    s.ctl[CTL_CB] = in ^ 1;
+    s.ctl[CTL_NCL0 + in] = 0;  // the old list's counter: the next re-compaction's output
+  }
+  if (rows && s.ctl[CTL_CMPGO]) {
+    const int in = s.ctl[CTL_BUF];
+    s.ctl[CTL_BUF] = in == 1 ? 2 : 1;
   }
 }
 
@@ -332,13 +386,13 @@ constexpr int kFilt = 8;  // rows per lane per filter step (their loads in fligh
 // rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
 template <int R>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
-                                         int* st_elems) {
+                                         int* st_elems, const uint16_t* __restrict__ key) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
   const uint32_t* __restrict__ crow = s.crow[buf];
   const int32_t* __restrict__ ccol = s.ccol[buf];
   int32_t* __restrict__ rtgt = s.rtgt[buf];
   uint16_t* __restrict__ skey = s.skey[buf];
-  const uint16_t* __restrict__ key = s.key;
+  // (key: s.key, or its copy in LDS — persistent engine, small systems)
   const int t = rtgt[row];
   const int32_t cv = cvar[row];
   const int v = rvar(cv);
@@ -347,6 +401,8 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   const bool bnd = rbounded(cv);
   const double vb = bnd ? s.vbound[v] : -1.0;
   const double p = bnd ? s.pen[v] : 1.0;  // read below only when vb > 0
+  // (the row's gathers wait for the variable's state: a fixed variable's row — every variable once, when
+  // its saturated target dies — retires without them; measured cheaper on C2 than issuing them early)
   if (vst != 0) {  // fixed by a saturation since: retire the row
     rtgt[row] = kRetired;
     return;
@@ -363,81 +419,92 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 #pragma unroll
   for (int i = 0; i < R; i++)
     kk[i] = cc[i] >= 0 ? key[cc[i]] : kDeadKey;
+  const unsigned kt = t >= 0 ? key[t] : kDeadKey;
+  // Elements beyond the first R: three passes (min key; count / old multiplicity / candidate; the other
+  // keys / new multiplicity), plus the exact-ratio pass on key ties or bounded variables, each with its
+  // loads unrolled so that they are in flight together.
   unsigned mk = kDeadKey;
 #pragma unroll
   for (int i = 0; i < R; i++)
     mk = min(mk, kk[i]);
+#pragma unroll 4
   for (uint32_t j = b + R; j < e; j++)
     mk = min(mk, (unsigned)key[ccol[j]]);
-  int nmin = 0;
-#pragma unroll
-  for (int i = 0; i < R; i++)
-    nmin += kk[i] == mk;
-  for (uint32_t j = b + R; j < e; j++)
-    nmin += key[ccol[j]] == mk;
   if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
     s.vstate[v] = round + 1;  // fixed / dropped in this round
     rtgt[row] = kRetired;
     return;
   }
+  int nmin = 0, mult_old = 0, newt = INT_MAX;  // newt: the smallest id at the minimal key
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    nmin += kk[i] == mk;
+    mult_old += cc[i] == t;
+    if (kk[i] == mk)
+      newt = min(newt, cc[i]);
+  }
+#pragma unroll 4
+  for (uint32_t j = b + R; j < e; j++) {
+    const int32_t c = ccol[j];
+    const unsigned k = key[c];
+    nmin += k == mk;
+    mult_old += c == t;
+    if (k == mk)
+      newt = min(newt, c);
+  }
   double minr = dinf();
-  if (nmin > 1 || vb > 0) {
+  if (nmin > 1 || vb > 0) {  // exact ratios at the minimal key: lexicographic min of (ratio, id)
+    newt = INT_MAX;
 #pragma unroll
     for (int i = 0; i < R; i++)
-      if (kk[i] == mk)
-        minr = fmin(minr, s.cst[cc[i]].ratio);
+      if (kk[i] == mk) {
+        const double r = s.cst[cc[i]].ratio;
+        if (r < minr || (r == minr && cc[i] < newt)) {
+          minr = r;
+          newt = cc[i];
+        }
+      }
     for (uint32_t j = b + R; j < e; j++) {
       const int32_t c = ccol[j];
-      if (key[c] == mk)
-        minr = fmin(minr, s.cst[c].ratio);
+      if (key[c] == mk) {
+        const double r = s.cst[c].ratio;
+        if (r < minr || (r == minr && c < newt)) {
+          minr = r;
+          newt = c;
+        }
+      }
     }
   }
-  int mult_old = 0;
-#pragma unroll
-  for (int i = 0; i < R; i++)
-    mult_old += cc[i] == t;
-  for (uint32_t j = b + R; j < e; j++)
-    mult_old += ccol[j] == t;
   if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
     s.vstate[v] = round + 1;  // fixed / dropped in this round
     s.x[v] = vb;
     rtgt[row] = kRetired;
-    if (t >= 0 && key[t] != kDeadKey)
+    if (t >= 0 && kt != kDeadKey)
       atomicAdd(&s.nvote[t], mult_old);
     for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
       push_decrement(s, j, vb, p);
     return;
   }
-  int newt = INT_MAX;
-#pragma unroll
-  for (int i = 0; i < R; i++)
-    if (kk[i] == mk && (nmin == 1 || s.cst[cc[i]].ratio == minr))
-      newt = min(newt, cc[i]);
-  for (uint32_t j = b + R; j < e; j++) {
-    const int32_t c = ccol[j];
-    if (key[c] == mk && (nmin == 1 || s.cst[c].ratio == minr))
-      newt = min(newt, c);
-  }
   unsigned sk = kDeadKey;  // min key over the other constraints of the row
+  int mult_new = 0;
 #pragma unroll
-  for (int i = 0; i < R; i++)
+  for (int i = 0; i < R; i++) {
     if (cc[i] != newt)
       sk = min(sk, kk[i]);
+    mult_new += cc[i] == newt;
+  }
+#pragma unroll 4
   for (uint32_t j = b + R; j < e; j++) {
     const int32_t c = ccol[j];
+    const unsigned k = key[c];
     if (c != newt)
-      sk = min(sk, (unsigned)key[c]);
+      sk = min(sk, k);
+    mult_new += c == newt;
   }
   skey[row] = uint16_t(row_floor(sk, mk, vb, p));
   if (newt == t)
     return;
-  int mult_new = 0;
-#pragma unroll
-  for (int i = 0; i < R; i++)
-    mult_new += cc[i] == newt;
-  for (uint32_t j = b + R; j < e; j++)
-    mult_new += ccol[j] == newt;
-  if (t >= 0 && key[t] != kDeadKey)
+  if (t >= 0 && kt != kDeadKey)
     atomicAdd(&s.nvote[t], mult_old);
   atomicSub(&s.nvote[newt], mult_new);
   rtgt[row] = newt;
@@ -460,7 +527,8 @@ constexpr int kDiagSlot = kMaxBlocks - 4;  // vstat block slots kDiagSlot.. hold
 
 template <bool kBits, int R, int F, int kDiag>
 __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
-                                          const uint64_t* bits, int* qw, int* st_rows, int* st_elems) {
+                                          const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
+                                          const uint16_t* __restrict__ key) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave, nw = blockDim.x / kWave;
   const int64_t ngr = (hi - lo + kWave - 1) / kWave;
   const int64_t gpw = (ngr + nw - 1) / nw;
@@ -468,7 +536,6 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   const int64_t whi = wlo + gpw * kWave < hi ? wlo + gpw * kWave : hi;
   const int32_t* __restrict__ rtgt = s.rtgt[buf];
   const uint16_t* __restrict__ skey = s.skey[buf];
-  const uint16_t* __restrict__ key = s.key;
   const uint16_t prev = uint16_t(round - 1);
   const unsigned long long below = (1ull << lane) - 1;
   int qn = 0, nq = 0;
@@ -525,13 +592,13 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
         if (kDiag == 0)
-          vote_row<R>(s, buf, round, row, st_rows, st_elems);
+          vote_row<R>(s, buf, round, row, st_rows, st_elems, key);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   if (kDiag == 0 && lane < qn)
-    vote_row<R>(s, buf, round, qw[lane], st_rows, st_elems);
+    vote_row<R>(s, buf, round, qw[lane], st_rows, st_elems, key);
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
     for (int k = 0; k < 3; k++) {
@@ -546,20 +613,34 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
 constexpr int kBitWords = 17408;  // LDS bitmap capacity of the multi-launch vote: 1,114,112 constraints
 
 // The changed-constraint bitmap into LDS (16 B per thread per step).
+#ifndef LMM_BITS_UNROLL
+#define LMM_BITS_UNROLL 1  // steps with their loads in flight together (build knob, measurement)
+#endif
 template <int B> __device__ __forceinline__ void load_bits(const Dev& s, uint64_t* bits) {
   const int n16 = (s.nC + 127) / 128;
   const uint4* __restrict__ src = reinterpret_cast<const uint4*>(s.chgbits);
   uint4* dst = reinterpret_cast<uint4*>(bits);
-  for (int i = threadIdx.x; i < n16; i += B)
-    dst[i] = src[i];
+  constexpr int kU = LMM_BITS_UNROLL;
+  for (int i0 = threadIdx.x; i0 < n16; i0 += kU * B) {
+    uint4 t[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (i0 + u * B < n16)
+        t[u] = src[i0 + u * B];
+#pragma unroll
+    for (int u = 0; u < kU; u++)
+      if (i0 + u * B < n16)
+        dst[i0 + u * B] = t[u];
+  }
 }
 
 // Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
 // to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
-template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int buf, int round) {
+template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (s.ctl[CTL_DONE])
     return;
+  const int buf = s.ctl[CTL_BUF];
   __shared__ int st_rows, st_elems;
   __shared__ int q[(B / kWave) * kQW];  // per-wave queues of rows to re-vote
   __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
@@ -585,7 +666,7 @@ template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B)
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
   if (lo < hi)
     vote_waves<kBits, 8, kFilt, kDiag>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW, &st_rows,
-                                       &st_elems);
+                                       &st_elems, s.key);
   if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
@@ -600,9 +681,10 @@ template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B)
 // of `ready` (LDS counter, no global atomic); bready[b] = segment length.
 __device__ __forceinline__ int64_t chunk_of(int64_t n, int nblocks) { return (n + nblocks - 1) / nblocks; }
 
-__global__ void __launch_bounds__(kBlock) mm_ready(Dev s, int cb) {
+__global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
   if (s.ctl[CTL_DONE])
     return;
+  const int cb = s.ctl[CTL_CB];
   __shared__ int cnt;
   if (threadIdx.x == 0)
     cnt = 0;
@@ -642,7 +724,11 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
   int32_t lv = -1;
+  double lp = 1.0, lx = 0.0;
+  uint32_t rb = 0, re = 0;
   if (j < ce) {
+    // (penalty and row are read for claimed variables only: issuing them with the state costs C2 more
+    // random reads than the round trip it saves)
     lv = s.csc_v[j];
     if (s.vstate[lv] != 0)
       lv = -1;
@@ -651,15 +737,14 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     else if (atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
       lv = -1;
   }
-  double lp = 1.0, lx = 0.0;
-  uint32_t rb = 0;
   int len = 0;
   if (lv >= 0) {
     lp = s.pen[lv];
+    rb = s.var_ptr[lv];
+    re = s.var_ptr[lv + 1];
     lx = r / lp;
     s.x[lv] = lx;
-    rb = s.var_ptr[lv];
-    len = int(s.var_ptr[lv + 1] - rb);
+    len = int(re - rb);
   }
   int incl = len;  // inclusive wave scan of the row lengths
 #pragma unroll
@@ -675,6 +760,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     int32_t cc[kSatU];
     uint32_t kk[kSatU];
     int ol[kSatU];
+    double ww[kSatU];
 #pragma unroll
     for (int u = 0; u < kSatU; u++) {  // owner lanes and element indices, then independent gathers
       const int f = f0 + u * kWave + lane;
@@ -686,6 +772,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       ol[u] = o;
       kk[u] = uint32_t(__shfl(int(rb), o, kWave)) + uint32_t(f - pre[o]);
       cc[u] = f < total ? s.csr_c[kk[u]] : -1;
+      ww[u] = f < total ? s.csr_w[kk[u]] : 0.0;  // with the constraint id: one round trip
     }
     long long a0[kSatU], a1[kSatU];  // fixed-point decrements (CstRec)
     bool fat[kSatU];
@@ -701,7 +788,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       if (cc[u] >= 0) {
         s.ctouch[cc[u]] = 1;  // receives decrements this round (mm_update reads its record)
         fat[u] = ce & kCexpFat;
-        const double w = s.csr_w[kk[u]];
+        const double w = ww[u];
         a0[u] = (long long)dec_q(w * ox, cexp_rem(ce));
         a1[u] = fat[u] ? (long long)fat_bits(w / op) : (long long)dec_q(w / op, cexp_use(ce));
       }
@@ -845,9 +932,10 @@ template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int3
 // K waves per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
 // counts in LDS (parallel: 8 segments per thread, wave shuffles, one LDS exchange) and maps its waves
 // onto the ready list by binary search.
-template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int cb, int ready_blocks) {
+template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, int round, int ready_blocks) {
   if (s.ctl[CTL_DONE])
     return;
+  const int cb = s.ctl[CTL_CB];
   __shared__ int pre[kMaxBlocks + 1];
   __shared__ int wsum[kBlock / kWave];
   __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
@@ -1124,7 +1212,10 @@ __device__ __forceinline__ bool row_alive(const Dev& s, int in, int64_t row) {
   return s.vstate[rvar(s.cvar[in][row])] == 0;
 }
 
-__global__ void __launch_bounds__(kBlock) cmp_count(Dev s, int in) {
+__global__ void __launch_bounds__(kBlock) cmp_count(Dev s) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int in = s.ctl[CTL_BUF];
   __shared__ int sh[2 * kBlock];
   const int64_t nrows = s.ctl[CTL_NROWS + in];
   const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
@@ -1144,7 +1235,12 @@ __global__ void __launch_bounds__(kBlock) cmp_count(Dev s, int in) {
   }
 }
 
-__global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int out) {
+// Exclusive scan of the per-block counts, totals into the output buffer's words, and the decision: rewrite
+// only when fewer than pct % of the scanned rows are alive (CTL_CMPGO).
+__global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int pct) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int in = s.ctl[CTL_BUF], out = in == 1 ? 2 : 1;
   __shared__ int sa[1024], sb[1024];
   const int t = threadIdx.x;
   const int per = (nblk + 1023) / 1024;
@@ -1172,9 +1268,13 @@ __global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int out) {
     rb += cb;
   }
   if (t == 1023) {
-    s.ctl[CTL_NROWS + out] = sa[t];
-    s.ctl[CTL_NELEM + out] = sb[t];
-    const_cast<uint32_t*>(s.crow[out])[sa[t]] = uint32_t(sb[t]);
+    const int go = int64_t(sa[t]) * 100 < int64_t(s.ctl[CTL_NROWS + in]) * pct;
+    s.ctl[CTL_CMPGO] = go;
+    if (go) {
+      s.ctl[CTL_NROWS + out] = sa[t];
+      s.ctl[CTL_NELEM + out] = sb[t];
+      const_cast<uint32_t*>(s.crow[out])[sa[t]] = uint32_t(sb[t]);
+    }
   }
 }
 
@@ -1212,7 +1312,10 @@ __device__ __forceinline__ void block_scan_pair(int& a, int& b, int& ta, int& tb
 
 // Rows of a block are visited k-major (row = base + k * kBlock + thread) so that neighbouring lanes
 // read and write neighbouring rows; the output keeps the input order.
-__global__ void __launch_bounds__(kBlock) cmp_write(Dev s, int in, int out) {
+__global__ void __launch_bounds__(kBlock) cmp_write(Dev s) {
+  if (s.ctl[CTL_DONE] || !s.ctl[CTL_CMPGO])
+    return;
+  const int in = s.ctl[CTL_BUF], out = in == 1 ? 2 : 1;
   const int64_t nrows = s.ctl[CTL_NROWS + in];
   const int64_t base = int64_t(blockIdx.x) * kCompactRows;
   int pr = s.bsum[2 * blockIdx.x], pe = s.bsum[2 * blockIdx.x + 1];

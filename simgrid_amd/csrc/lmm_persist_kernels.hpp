@@ -169,6 +169,8 @@ template <bool kBits> union PLds {
 // by vote_waves (every wave on its own share, no workgroup barrier after the bitmap load).
 template <bool kBits, int R>
 __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds<kBits>& L, bool count) {
+  if (threadIdx.x == 0)
+    L.st0 = 0;
   if (kBits)
     load_bits<kPB>(s, L.bits);
   __syncthreads();
@@ -178,9 +180,14 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
   int nq = 0;
   if (lo < hi)
     nq = vote_waves<kBits, R, kPFilt, 0>(s, buf, round, lo, hi, L.bits, L.q + (threadIdx.x / kWave) * kQW, &L.st0,
-                                         &L.st1);
-  if (count && (threadIdx.x & (kWave - 1)) == 0 && nq)
-    atomicAdd(&s.ctl[CTL_RESEVAL], nq);
+                                         &L.st1, s.key);
+  if (count) {  // (profiling) one add per workgroup: a per-wave add to one word cost ~6 us per round on C4
+    if ((threadIdx.x & (kWave - 1)) == 0 && nq)
+      atomicAdd(&L.st0, nq);
+    __syncthreads();
+    if (threadIdx.x == 0 && L.st0)
+      atomicAdd(&s.ctl[CTL_RESEVAL], L.st0);
+  }
 }
 
 // S: ready test fused with saturation over every constraint (identity ids), sat_block (the ready

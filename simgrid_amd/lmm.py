@@ -13,6 +13,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "liblmm_amd.so")
+# measurement only (A/B of two builds in one GPU call): LMM_AMD_LIB names another build of the same library
+LIB_PATH = os.environ.get("LMM_AMD_LIB") or LIB_PATH
 
 P, D, I, I64, U64 = ct.c_void_p, ct.c_double, ct.c_int, ct.c_int64, ct.c_uint64
 PI, PD, PI64 = ct.POINTER(I), ct.POINTER(D), ct.POINTER(I64)
