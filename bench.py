@@ -432,16 +432,19 @@ def run_config(args):
         s = lmm.System(False, lmm.System.FAIR_BOTTLENECK)
         s.gen_platform_flows(lmm.platform_params(model=lmm.L07, n_flows=flows, seed=1, **C5_PLATFORM),
                              want_vars=False)
-        f = M.export_flat(s)
-        del s
-        sub, _ = M.shard_variables(f, world)[rank]
-        shards = [M.DeviceFbShard(sub)]
-        nV_total, nC_total = len(f.penalty), len(f.cbound)
-        del f
         work_vars, scaling = flows, "strong"
         desc = dict(workload=f"C5: {flows} L07 flows on dragonfly {C5_PLATFORM['topo_parameters']} (4096 hosts), "
-                             "FairBottleneck", flows=flows,
-                    parallelism=f"variables sharded x{world}, 2 all-reduces per round")
+                             "FairBottleneck", flows=flows)
+        if world > 1:  # variables sharded over the ranks, the per-round reductions all-reduced
+            f = M.export_flat(s)
+            del s
+            sub, _ = M.shard_variables(f, world)[rank]
+            shards = [M.DeviceFbShard(sub)]
+            nV_total, nC_total = len(f.penalty), len(f.cbound)
+            del f
+            desc["parallelism"] = f"variables sharded x{world}, 2 all-reduces per round"
+        else:  # one GPU: the drop-in FairBottleneck::solve path (element order of the reference, bit-identical)
+            desc["parallelism"] = "one context (System::solve, fbk_update_seq)"
     if batch is not None:
         nV, nC, nnz = batch.n_var, batch.n_cnst, batch.nnz
     elif shards is None:

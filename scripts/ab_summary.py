@@ -5,8 +5,11 @@ import sys
 
 tag, i = sys.argv[1], sys.argv[2]
 out = [tag]
-for w in ("c2", "c4"):
-    d = json.load(open(f"gpurun_out/ab_{i}_{w}.json"))
+for w in ("c2", "c3", "c4", "c5"):
+    try:
+        d = json.load(open(f"gpurun_out/ab_{i}_{w}.json"))
+    except OSError:
+        continue
     out.append(f"{w} {d['ms_per_step']} ms ({d['config'].get('device_rounds')} rounds)")
 try:
     p = json.load(open(f"gpurun_out/ab_{i}_c2prof.json"))

@@ -119,6 +119,7 @@ struct Dev {
   int32_t* vstate;  // [nV] maxmin: 0 alive, r+1 = fixed or dropped in round r (claimed with atomicCAS)
   double* vtmp;     // [nV] fair bottleneck: mu
   uint8_t* vst;     // [nV] fair bottleneck: 1 listed / 0 not
+  uint32_t* vstb;   // [nV/32 + 1] fair bottleneck: vst packed 32 per word for fbk_count (fb_pack_vst)
   // per-constraint state
   double* ratio;    // [nC] remaining/usage, +inf when out of the light table
   uint16_t* key;    // [nC] round-down 16-bit key of ratio, kDeadKey when out
@@ -156,6 +157,7 @@ struct Dev {
   int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag), all-reduce SUM
   double* xsum;              // [nC] sum of w*mu per shared constraint, all-reduce SUM
   double* xmin;              // [nC] min of w*mu per FATPIPE constraint, all-reduce MIN
+  double* fbd;               // [nnz] one context: w*mu of every shared constraint's element, CSC order
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };

@@ -45,6 +45,29 @@ __device__ __forceinline__ uint32_t chunk_end(const Dev& s, int q, int c) {
   return e < ce ? e : ce;
 }
 
+// The listed flags packed 32 per word (vstb) before the count: its gathers then hit a table of nV / 8 bytes
+// (1.25 MB at C5's 10^7 flows: resident in every XCD's L2) instead of the nV-byte flags.
+__global__ void __launch_bounds__(kBlock) fb_pack_vst(Dev s) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int64_t nw = (int64_t(s.nV) + 31) / 32;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nw; i += int64_t(gridDim.x) * kBlock) {
+    uint32_t m = 0;
+    const int64_t v0 = i * 32;
+    if (v0 + 32 <= s.nV) {
+      const uint4 a = reinterpret_cast<const uint4*>(s.vst + v0)[0], b = reinterpret_cast<const uint4*>(s.vst + v0)[1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int k = 0; k < 32; k++)
+        m |= uint32_t(((w[k >> 2] >> (8 * (k & 3))) & 0xFF) != 0) << k;
+    } else {
+      for (int k = 0; v0 + k < s.nV; k++)
+        m |= uint32_t(s.vst[v0 + k] != 0) << k;
+    }
+    s.vstb[i] = m;
+  }
+}
+
 // :67-74 — listed variables (w > 0: every flattened element) of each chunk of a listed constraint
 __global__ void __launch_bounds__(kBlock) fbk_count(Dev s) {
   if (s.ctl[CTL_DONE])
@@ -54,9 +77,19 @@ __global__ void __launch_bounds__(kBlock) fbk_count(Dev s) {
   for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < s.nch; q += gridDim.x * wpb) {
     const int c = s.ch_cnst[q];
     int nb = 0;
-    if (s.ratio[c] == 0.0)
-      for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave)
-        nb += s.vst[s.csc_v[j]];
+    if (s.ratio[c] == 0.0) {
+      const uint32_t e = chunk_end(s, q, c);
+      for (uint32_t j0 = s.ch_beg[q] + lane; j0 < e; j0 += 4 * kWave) {  // 4 gathers in flight per lane
+        int32_t vv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          vv[k] = j0 + k * kWave < e ? s.csc_v[j0 + k * kWave] : -1;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (vv[k] >= 0)
+            nb += (s.vstb[vv[k] >> 5] >> (vv[k] & 31)) & 1;
+      }
+    }
     nb = grp_isum<kWave>(nb);
     if (lane == 0)
       s.pcnt[q] = nb;
@@ -116,9 +149,24 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
     if (!s.vst[v])
       continue;
-    double inc = DBL_MAX;
-    for (uint32_t j = s.var_ptr[v]; j < s.var_ptr[v + 1]; j++)
-      inc = fmin(inc, s.use[s.csr_c[j]] / s.csr_w[j]);
+    double inc = DBL_MAX;  // (a min: any order gives the same value)
+    const uint32_t b = s.var_ptr[v], e = s.var_ptr[v + 1];
+    for (uint32_t j0 = b; j0 < e; j0 += 4) {  // 4 elements' loads in flight together
+      int32_t cc[4];
+      double ww[4], uu[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        cc[k] = j0 + k < e ? s.csr_c[j0 + k] : -1;
+        ww[k] = j0 + k < e ? s.csr_w[j0 + k] : 1.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        uu[k] = cc[k] >= 0 ? s.use[cc[k]] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (cc[k] >= 0)
+          inc = fmin(inc, uu[k] / ww[k]);
+    }
     const double vb = s.vbound[v];
     double x = s.x[v];
     if (vb > 0)
@@ -137,17 +185,48 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
 }
 
 // :107-127 — per chunk of a listed constraint: sum (or FATPIPE: min) of w*mu over ALL its elements
-// (the stale mu of variables that already left the list included)
-__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
+// (the stale mu of variables that already left the list included).  fat_only (one context): the shared
+// constraints' sums are not needed — fbk_update_seq takes their elements one at a time itself — so only
+// FATPIPE chunks are reduced (one pass of w * mu gathers per round less).
+// fat_only also writes the shared constraints' increments w * mu in CSC order into fbd (element-parallel,
+// all gathers of the round spread over the chip), which fbk_update_seq then streams.
+__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int fat_only) {
   if (s.ctl[CTL_DONE])
     return;
   const int lane = threadIdx.x & (kWave - 1);
   const int wpb = kBlock / kWave;
   for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < s.nch; q += gridDim.x * wpb) {
     const int c = s.ch_cnst[q];
+    const bool fat = s.cflags[c] & 1;
     if (s.ratio[c] != 0.0)
       continue;
-    const bool fat = s.cflags[c] & 1;
+    if (fat_only && !fat) {
+      // only the elements of variables listed this round: a delisted variable's mu (vtmp) no longer
+      // moves, so its increment written in its last listed round still holds (every variable is listed in
+      // round 0, a listed constraint was listed in every earlier round); vstb = the flags before fb_var_inc
+      const uint32_t e = chunk_end(s, q, c);
+      for (uint32_t j0 = s.ch_beg[q] + lane; j0 < e; j0 += 4 * kWave) {  // 4 gathers in flight per lane
+        int32_t vv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t j = j0 + k * kWave;
+          vv[k] = j < e ? s.csc_v[j] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (vv[k] >= 0 && !((s.vstb[vv[k] >> 5] >> (vv[k] & 31)) & 1))
+            vv[k] = -1;
+        double dv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          dv[k] = vv[k] >= 0 ? s.csc_w[j0 + k * kWave] * s.vtmp[vv[k]] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (vv[k] >= 0)
+            s.fbd[j0 + k * kWave] = dv[k];
+      }
+      continue;
+    }
     double acc = fat ? dinf() : 0.0;
     for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave) {
       const double d = s.csc_w[j] * s.vtmp[s.csc_v[j]];
@@ -161,7 +240,7 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
 
 // per constraint: chunk partials in chunk order -> xsum (shared) / xmin (FATPIPE); the other one
 // gets the neutral element of its all-reduce
-__global__ void __launch_bounds__(kBlock) fbk_accc(Dev s) {
+__global__ void __launch_bounds__(kBlock) fbk_accc(Dev s, int fat_only) {
   if (s.ctl[CTL_DONE])
     return;
   for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
@@ -170,7 +249,7 @@ __global__ void __launch_bounds__(kBlock) fbk_accc(Dev s) {
       if (s.cflags[c] & 1)
         for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
           mn = fmin(mn, s.pacc[q]);
-      else
+      else if (!fat_only)
         for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
           sum += s.pacc[q];
     }
@@ -216,14 +295,24 @@ __global__ void __launch_bounds__(kBlock) fbk_update(Dev s, double prec) {
 // remaining ends a few ulps of its bound away from 0, and whether that residue is below the precision
 // (erasure, :129) depends on the rounding of this exact chain — a tree sum is more accurate and erases
 // constraints the reference keeps (C5 at 1e6 flows: 28 of them in round 0, a different fixed point for
-// 12 % of the flows).  One wave per constraint: lanes gather 64 increments into LDS, lane 0 chains them.
-// FATPIPE as fbk_update.
+// 12 % of the flows).  One wave per constraint; FATPIPE as fbk_update.
+//
+// The chain is the critical path (C5's global dragonfly links hold ~1.6e5 elements), so it is fed without
+// waiting: the increments were computed element-parallel by fbk_acc (fbd, CSC order); the lanes stream
+// kSeqP x 64 of them into LDS and issue the loads of the next kSeqP x 64 before lane 0 chains the current
+// ones (a gather per element here left the long chains waiting on memory under load: 4.3 ms per round).  And when every increment of a batch is >= 0 the clamp is taken
+// once at its end: fl(r - d) <= r for d >= 0, so the unclamped remaining only decreases; the clamped chain
+// equals it until its first value below the precision and is 0 from there on (0 - d < precision), i.e. the
+// clamped result is 0 exactly when the unclamped end value is below the precision, and that end value
+// otherwise.  A batch holding a negative (or NaN) increment takes the clamp at every step.
+constexpr int kSeqP = 8;  // 64-element blocks per batch
+
 __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
   if (s.ctl[CTL_DONE])
     return;
-  __shared__ double dl[kBlock];
+  __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
   const int lane = threadIdx.x & (kWave - 1);
-  double* d = dl + (threadIdx.x - lane);
+  double* d = dl[threadIdx.x / kWave];
   for (int64_t c = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; c < s.nC;
        c += int64_t(gridDim.x) * (kBlock / kWave)) {  // wave-uniform
     if (lane == 0)
@@ -242,17 +331,70 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
       if (rem < prec)
         rem = 0.0;
     } else {
-      const uint32_t ce = s.cnst_ptr[c + 1];
-      for (uint32_t base = s.cnst_ptr[c]; base < ce; base += kWave) {  // wave-uniform
-        const uint32_t j = base + lane;
-        d[lane] = j < ce ? s.csc_w[j] * s.vtmp[s.csc_v[j]] : 0.0;
+      const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
+      double nx[kSeqP];
+#pragma unroll
+      for (int p = 0; p < kSeqP; p++) {
+        const uint32_t j = cb + p * kWave + lane;
+        nx[p] = j < ce ? s.fbd[j] : 0.0;
+      }
+      for (uint32_t base = cb; base < ce; base += kSeqP * kWave) {  // wave-uniform
+        bool nonneg = true;
+#pragma unroll
+        for (int p = 0; p < kSeqP; p++) {
+          d[p * kWave + lane] = nx[p];
+          nonneg &= nx[p] >= 0.0;
+        }
+        nonneg = __all(nonneg);
+        const uint32_t nb = base + kSeqP * kWave;
+#pragma unroll
+        for (int p = 0; p < kSeqP; p++) {  // the next batch's loads, in flight during the chain
+          const uint32_t j = nb + p * kWave + lane;
+          nx[p] = j < ce ? s.fbd[j] : 0.0;
+        }
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
-          const int n = int(ce - base < uint32_t(kWave) ? ce - base : uint32_t(kWave));
-          for (int k = 0; k < n; k++) {
-            rem -= d[k];
+          const int n = int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave));
+          if (nonneg) {
+            // 16 increments per step, the next 16 read from LDS while these are chained (slots past n
+            // hold 0.0: r - 0 == r); two register sets used in turn, so nothing is copied between steps
+            const double2* dd = reinterpret_cast<const double2*>(d);
+            double2 ra[8], rb[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++)
+              ra[t] = dd[t];
+            for (int k = 0; k < n; k += 32) {
+              if (k + 16 < n) {
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                  rb[t] = dd[(k + 16) / 2 + t];
+              }
+#pragma unroll
+              for (int t = 0; t < 8; t++) {
+                rem -= ra[t].x;
+                rem -= ra[t].y;
+              }
+              if (k + 16 >= n)
+                break;
+              if (k + 32 < n) {
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                  ra[t] = dd[(k + 32) / 2 + t];
+              }
+#pragma unroll
+              for (int t = 0; t < 8; t++) {
+                rem -= rb[t].x;
+                rem -= rb[t].y;
+              }
+            }
             if (rem < prec)
               rem = 0.0;
+          } else {
+            for (int k = 0; k < n; k++) {
+              rem -= d[k];
+              if (rem < prec)
+                rem = 0.0;
+            }
           }
         }
         __builtin_amdgcn_wave_barrier();

@@ -109,6 +109,7 @@ struct lmmhip_ctx {
   std::vector<void*> act_allocs;
   int32_t* xnb_own = nullptr;  // the context's own exchange buffers (unsharded solves)
   double *xsum_own = nullptr, *xmin_own = nullptr;
+  int64_t fbd_cap = 0;  // elements of d.fbd (allocated by the first one-context FairBottleneck solve)
   // resident System mirror (lmmhip_res_*, lmm_resident_kernels.hpp): outlives uploads, freed with the
   // context.  Mirror arrays keep their contents when they grow; scratch buffers do not.
   struct Scr {
@@ -147,6 +148,7 @@ static void free_all(lmmhip_ctx* c) {
   c->uploaded = false;
   c->xnb_own = nullptr;
   c->xsum_own = c->xmin_own = nullptr;
+  c->fbd_cap = 0;
   c->fb_shard = false;
   c->res_flat = false;
 }
@@ -293,7 +295,8 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   rc |= dalloc(c, &d.x, nV);
   rc |= dalloc(c, &d.fixr, nV);
   rc |= dalloc(c, &d.vtmp, nV);
-  rc |= dalloc(c, &d.vst, nV);
+  rc |= dalloc(c, &d.vst, int64_t(nV) + 32);  // (+32: read 32 flags at a time by fb_pack_vst)
+  rc |= dalloc(c, &d.vstb, (int64_t(nV) + 31) / 32 + 1);
   rc |= dalloc(c, &d.ratio, nC);
   rc |= dalloc(c, &d.key, nC);
   rc |= dalloc(c, &d.rem, nC);
@@ -1164,6 +1167,10 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat);
   auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
+  // mm_saturate: waves per ready constraint and the grid's block cap (measurement knobs)
+  const int sat_k = env_int("LMMHIP_SAT_WAVES", c->sat_waves);
+  const int sat_max = env_int("LMMHIP_SAT_GRID_MAX", kMaxBlocks);
+  auto sat_grid = [&](int64_t n) { return int(std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, sat_max))); };
   // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
   // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
   // Both decide and switch buffers on the device (ctl CTL_BUF / CTL_CB): no host round trip.
@@ -1187,12 +1194,12 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d);
-      if (c->sat_waves == 1)
-        LAUNCH(4, r, mm_saturate<1>, capped(gL, cap_sat), kBlock, d, int(r), gL);
-      else if (c->sat_waves == 2)
-        LAUNCH(4, r, mm_saturate<2>, capped(grid_for(2 * ncl, kBlock), cap_sat), kBlock, d, int(r), gL);
+      if (sat_k == 1)
+        LAUNCH(4, r, mm_saturate<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gL);
+      else if (sat_k == 2)
+        LAUNCH(4, r, mm_saturate<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gL);
       else
-        LAUNCH(4, r, mm_saturate<4>, capped(grid_for(4 * ncl, kBlock), cap_sat), kBlock, d, int(r), gL);
+        LAUNCH(4, r, mm_saturate<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gL);
       LAUNCH(5, r, mm_update, gU, kBlock, d, int(r), prec);
     }
     LAUNCH(6, r, mm_done, 1, kBlock, d, gU);
@@ -1356,14 +1363,15 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
   const int gV = grid_for(d.nV, kBlock);
   switch (phase) {
   case 0:
+    LAUNCH(2, r, fb_pack_vst, grid_for((int64_t(d.nV) + 31) / 32, kBlock), kBlock, d);
     LAUNCH(2, r, fbk_count, gQ, kBlock, d);
     LAUNCH(2, r, fbk_nb, gC, kBlock, d, par);
     break;
   case 1:
     LAUNCH(3, r, fbk_share, gC, kBlock, d, par);
     LAUNCH(3, r, fb_var_inc, gV, kBlock, d, par, int(r));
-    LAUNCH(4, r, fbk_acc, gQ, kBlock, d);
-    LAUNCH(4, r, fbk_accc, gC, kBlock, d);
+    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(!c->fb_shard));
+    LAUNCH(4, r, fbk_accc, gC, kBlock, d, int(!c->fb_shard));
     break;
   case 2:
     if (c->fb_shard)  // shards: the summed increments come through the exchange buffer
@@ -1381,6 +1389,11 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
 
 static int solve_fair(lmmhip_ctx* c, double prec) {
   c->fb_shard = false;
+  if (c->fbd_cap < c->d.nnz) {  // increments in CSC order (fbk_acc -> fbk_update_seq)
+    if (int rc = dalloc(c, &c->d.fbd, c->d.nnz))
+      return rc;
+    c->fbd_cap = c->d.nnz;
+  }
   c->d.xnb = c->xnb_own;
   c->d.xsum = c->xsum_own;
   c->d.xmin = c->xmin_own;
