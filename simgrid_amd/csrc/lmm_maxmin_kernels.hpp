@@ -1323,6 +1323,8 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s) {
   int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
   uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
   int32_t* __restrict__ ocol = const_cast<int32_t*>(s.ccol[out]);
+  __shared__ int sh_pre[kBlock];
+  __shared__ uint32_t sh_beg[kBlock];
   for (int k = 0; k < kRowsPerThread; k++) {
     const int64_t row = base + int64_t(k) * kBlock + threadIdx.x;
     int32_t v = 0;  // (bounded flag kept)
@@ -1344,10 +1346,24 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s) {
       s.rtgt[out][o] = s.rtgt[in][row];
       s.skey[out][o] = s.skey[in][row];
       orow[o] = uint32_t(pe + xe);
-      int32_t* dst = ocol + pe + xe;
-      for (uint32_t j = b; j < e; j++)
-        *dst++ = icol[j];
     }
+    // the step's elements land in one contiguous output range [pe, pe + te): copied by the whole block,
+    // element f from the row whose exclusive prefix is the last one <= f (coalesced stores, the loads
+    // follow the rows in order) instead of one row per thread
+    sh_pre[threadIdx.x] = xe;
+    sh_beg[threadIdx.x] = b;
+    __syncthreads();
+    for (int f = threadIdx.x; f < te; f += kBlock) {
+      // the last row whose prefix is <= f: it holds f (a dead / empty row shares its prefix with the next
+      // row, so the last one with that prefix is never empty while f < te)
+      int r = 0;
+#pragma unroll
+      for (int st = kBlock / 2; st > 0; st >>= 1)
+        if (r + st < kBlock && sh_pre[r + st] <= f)
+          r += st;
+      ocol[pe + f] = icol[sh_beg[r] + uint32_t(f - sh_pre[r])];
+    }
+    __syncthreads();
     pr += tr;
     pe += te;
   }
