@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --dropin-steps 0 $*"
-PARTS=${PARTS:-"trace c3 c4 pmc"}  # subset to run (e.g. PARTS="c4 pmc")
+PARTS=${PARTS:-"trace c3 c5 pmc c4"}  # subset to run (e.g. PARTS="c4 pmc")
 has() { case " $PARTS " in *" $1 "*) return 0;; *) return 1;; esac; }
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 if has trace; then
@@ -14,7 +14,7 @@ if has trace; then
     -- python3 $BENCH > gpurun_out/rp_trace.log 2>&1
   rc=$?; echo "trace rc=$rc" >> gpurun_out/rp_trace.log; if fatal $rc; then exit $rc; fi
 fi
-for w in c3 c4; do  # the batch kernel (C3) and the persistent engine (C4): one dispatch per solve
+for w in c3 c5; do  # the batch kernel (C3: one dispatch per solve) and the FairBottleneck kernels (C5)
   has $w || continue
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_$w -o run \
     -- python3 bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/rp_trace_$w.log 2>&1
@@ -30,4 +30,11 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
     -- ./scripts/ubench_gather > gpurun_out/rp_cal_$ctr.log 2>&1
   rc=$?; echo "cal $ctr rc=$rc" >> gpurun_out/rp_cal_$ctr.log; if fatal $rc; then exit $rc; fi
 done
+# the persistent engine (C4) last: rocprofv3 has crashed in its exit handler after writing this trace
+# (SIGSEGV in the tool's teardown, outputs complete), and nothing may run after a crash in one call
+if has c4; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_c4 -o run \
+    -- python3 bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/rp_trace_c4.log 2>&1
+  rc=$?; echo "trace c4 rc=$rc" >> gpurun_out/rp_trace_c4.log
+fi
 exit 0

@@ -380,7 +380,10 @@ __global__ void mm_flip(Dev s, int clist, int rows) {
 // row targets (one lane per row, kFilt rows in flight per lane) and queues the rows that need a
 // re-vote in LDS; each full queue of kBlock rows is then resolved one lane per row, with up to kReg
 // independent gathers in flight, so the rare slow rows no longer stall whole waves of fast ones.
-constexpr int kFilt = 8;  // rows per lane per filter step (their loads in flight together)
+#ifndef LMM_KFILT
+#define LMM_KFILT 8
+#endif
+constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads in flight together; build knob)
 
 // Re-vote of one row, one lane: the first R elements in registers (their loads in flight together), longer
 // rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
