@@ -30,7 +30,9 @@ SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_ready"
 SLOT_KERNELS = {"mm_vote": ("mm_vote_lane", "mm_vote"), "mm_saturate": ("mm_saturate",),
                 "mm_update": ("mm_update",), "mm_ready": ("mm_ready",), "compaction": ("cmp_write",),
                 "mm_init_cnsts": ("mm_init_cnsts",), "mm_init_vars": ("mm_init_vars",)}
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
+# the newest rocprofv3 PMC summary (scripts/parse_rocprof.py) of the default C2 run
+TRAFFIC_JSON = next((p for p in (os.path.join(ROOT, "profiles", f"r0{k}_traffic.json") for k in (2, 1))
+                     if os.path.exists(p)), None)
 
 
 def log(*a):

@@ -59,7 +59,29 @@ def main():
         e["hbm_bytes_per_launch"] = int(e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"])
     cal = {short(n): dict(fetch_bytes=v[0] / v[1], write_bytes=cal_w.get(n, [0, 1])[0] / max(cal_w.get(n, [0, 1])[1], 1))
            for n, v in cal_f.items()}
-    out = dict(kernels=kernels, calibration=cal,
+    # counter bytes against the algorithmic bytes of bench.py's per-kernel model (gpurun_out/prof_c2.json, the
+    # per-launch profile of the same workload): raw FETCH + WRITE, and with FETCH doubled (the gfx950 correction
+    # for wide streaming reads, MI355X_MICROARCH.md HBM; random gathers are counted per 64-B request, so the
+    # truth lies between the two for kernels that mix both)
+    ratios = {}
+    pj = os.path.join(OUT, "prof_c2.json")
+    if os.path.exists(pj):
+        with open(pj) as f:
+            pk = json.load(f)["per_kernel"]
+        for bench_name, rp_name in (("mm_vote", "mm_vote_lane"), ("mm_ready", "mm_ready"),
+                                    ("mm_saturate", "mm_saturate"), ("mm_update", "mm_update"),
+                                    ("mm_init_cnsts", "mm_init_cnsts")):
+            if bench_name not in pk or rp_name not in kernels:
+                continue
+            alg = pk[bench_name]["alg_bytes"] / max(pk[bench_name]["launches"], 1)
+            e = kernels[rp_name]
+            raw = e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
+            cor = 2 * e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
+            ratios[rp_name] = dict(alg_bytes_per_launch=int(alg), counter_bytes_per_launch=int(raw),
+                                   counter_bytes_fetch_x2=int(cor), ratio_raw=round(raw / alg, 2) if alg else None,
+                                   ratio_fetch_x2=round(cor / alg, 2) if alg else None,
+                                   avg_us=round(pk[bench_name]["avg_us"], 2))
+    out = dict(kernels=kernels, counter_vs_algorithmic=ratios, calibration=cal,
                calibration_note="stream_idx reads 320e6 B (int32 x 8e7); gather<T> gathers 8e7 elements "
                                 "at random from 1e6 / 4e6 / 1e7-entry tables; atomics/scatter touch 8e7 random elements")
     with open(os.path.join(prof, f"{tag}_traffic.json"), "w") as f:
@@ -67,6 +89,9 @@ def main():
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
         print(f"{k:24s} launches {e['launches']:5d}  fetch/launch {e['fetch_bytes_per_launch']/1e6:9.2f} MB"
               f"  write/launch {e['write_bytes_per_launch']/1e6:9.2f} MB")
+    for k, r in ratios.items():
+        print(f"{k:24s} alg {r['alg_bytes_per_launch']/1e6:8.2f} MB  counters {r['ratio_raw']}x (fetch x2: "
+              f"{r['ratio_fetch_x2']}x)  {r['avg_us']} us")
 
 
 if __name__ == "__main__":
