@@ -821,10 +821,10 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     return rc;
   if (fair)
     RS_LAUNCH(rs_rowlen_fair, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
-  else
-    RS_LAUNCH(rs_rowlen, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
+  else  // (max-min: CSC offsets from the sorted ids below, no degree atomics)
+    RS_LAUNCH(rs_rowlen, nvs, nvs, r, pos, lany, dcl, vm, rl, static_cast<int64_t*>(nullptr));
   if ((rc = dev_scan(c, vm, dv, nvs + 1)) || (rc = dev_scan(c, rl, ro, nvs + 1)) ||
-      (rc = dev_scan(c, cdeg, cptr, nl + 1)))
+      (fair && (rc = dev_scan(c, cdeg, cptr, nl + 1))))
     return rc;
   const int64_t nC = read_i64(c, dcl + nl, &rc);
   const int64_t nV = read_i64(c, dv + nvs, &rc);
@@ -866,7 +866,10 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
             rowid, kidx);
   const uint32_t nnz32 = uint32_t(nnz);
   HIPCHK(hipMemcpyAsync(fb.vp + nV, &nnz32, sizeof(nnz32), hipMemcpyHostToDevice, c->stream));
-  RS_LAUNCH(rs_ptr32, nC, nC, cptr, fb.cp);
+  if (fair)
+    RS_LAUNCH(rs_ptr32, nC, nC, cptr, fb.cp);
+  else if (!nnz)
+    HIPCHK(hipMemsetAsync(fb.cp, 0, size_t(nC + 1) * sizeof(uint32_t), c->stream));
   if (fair)
     RS_LAUNCH(rs_chunks, nC, nC, cptr, nck, cch, kFbChunk, fb.cch, fb.chc, fb.chb);
   else
@@ -882,6 +885,8 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
       return rc;
     HIPCHK(sort_pairs_i32(t, tb, fb.csr_c, skey, kidx, sval, nnz, bits, c->stream));
     RS_LAUNCH(rs_csc, nnz, nnz, sval, rowid, fb.csr_w, fb.csc_v, fb.csc_w);
+    if (!fair)
+      RS_LAUNCH(rs_cptr_sorted, nnz, nnz, nC, skey, fb.cp);
   }
   HIPCHK(hipStreamSynchronize(c->stream));  // before the host's list buffer is released
   if ((rc = finish_flat(c, nV, nC, nnz)))

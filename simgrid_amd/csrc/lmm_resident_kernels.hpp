@@ -39,6 +39,8 @@ struct ResDev {
 constexpr uint8_t kResElemEnabled = 1;
 constexpr uint8_t kResCnstFatpipe = 1;
 
+constexpr int kRsU = 8;  // slab elements per unrolled step of the flatten passes (their gathers in flight)
+
 __global__ void __launch_bounds__(kBlock)
     rs_apply_e(int64_t n, const int64_t* __restrict__ id, const int32_t* __restrict__ cn,
                const double* __restrict__ w, const uint8_t* __restrict__ fl, ResDev r) {
@@ -124,16 +126,30 @@ __global__ void __launch_bounds__(kBlock)
     int64_t mk = 0;
     const int64_t b = r.v_ebase[v];
     const int n = r.v_n[v];
-    for (int i = 0; i < n; i++) {
-      if (!(r.e_fl[b + i] & kResElemEnabled))
-        continue;
-      const int32_t p = pos[r.e_cnst[b + i]];
-      if (p < 0)
-        continue;
-      rst = 1;
-      if (r.e_w[b + i] > 0 && lpart[p]) {
-        mk = 1;
-        lany[p] = 1;
+    for (int i0 = 0; i0 < n; i0 += kRsU) {  // kRsU elements' loads in flight together
+      int32_t p[kRsU];
+      uint8_t fl[kRsU];
+#pragma unroll
+      for (int u = 0; u < kRsU; u++) {
+        p[u] = i0 + u < n ? r.e_cnst[b + i0 + u] : -1;
+        fl[u] = i0 + u < n ? r.e_fl[b + i0 + u] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kRsU; u++)
+        if (!(fl[u] & kResElemEnabled))
+          p[u] = -1;
+#pragma unroll
+      for (int u = 0; u < kRsU; u++)
+        p[u] = p[u] >= 0 ? pos[p[u]] : -1;
+#pragma unroll
+      for (int u = 0; u < kRsU; u++) {
+        if (p[u] < 0)
+          continue;
+        rst = 1;
+        if (r.e_w[b + i0 + u] > 0 && lpart[p[u]]) {
+          mk = 1;
+          lany[p[u]] = 1;
+        }
       }
     }
     vrst[v] = rst;
@@ -143,6 +159,8 @@ __global__ void __launch_bounds__(kBlock)
 
 // Row lengths of the member variables (elements with w > 0 on a part constraint, in slot order, no
 // enabled-list test: System::flatten_maxmin) and the per-constraint degrees (dense ids = dcl).
+// cdeg == nullptr: row lengths only (max-min: the CSC offsets come from the sorted constraint ids,
+// rs_cptr_sorted, instead of one atomic per element — 8e7 of them at C2).
 __global__ void __launch_bounds__(kBlock)
     rs_rowlen(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
               const int64_t* __restrict__ dcl, const int64_t* __restrict__ vm, int64_t* rl, int64_t* cdeg) {
@@ -155,15 +173,38 @@ __global__ void __launch_bounds__(kBlock)
     if (vm[v]) {
       const int64_t b = r.v_ebase[v];
       const int n = r.v_n[v];
-      for (int i = 0; i < n; i++) {
-        const int32_t p = pos[r.e_cnst[b + i]];
-        if (p >= 0 && lany[p] && r.e_w[b + i] > 0) {
-          cnt++;
-          atomicAdd(reinterpret_cast<unsigned long long*>(cdeg + dcl[p]), 1ull);
-        }
+      for (int i0 = 0; i0 < n; i0 += kRsU) {  // kRsU elements' loads in flight together
+        int32_t p[kRsU];
+#pragma unroll
+        for (int u = 0; u < kRsU; u++)
+          p[u] = i0 + u < n ? r.e_cnst[b + i0 + u] : -1;
+#pragma unroll
+        for (int u = 0; u < kRsU; u++)
+          p[u] = p[u] >= 0 ? pos[p[u]] : -1;
+#pragma unroll
+        for (int u = 0; u < kRsU; u++)
+          if (p[u] >= 0 && lany[p[u]] && r.e_w[b + i0 + u] > 0) {
+            cnt++;
+            if (cdeg)
+              atomicAdd(reinterpret_cast<unsigned long long*>(cdeg + dcl[p[u]]), 1ull);
+          }
       }
     }
     rl[v] = cnt;
+  }
+}
+
+// CSC offsets from the stably sorted dense constraint ids sk[0..nnz): element j starts constraint sk[j] and
+// every empty one between it and the previous element's constraint; the last element closes the rest.
+__global__ void __launch_bounds__(kBlock)
+    rs_cptr_sorted(int64_t nnz, int64_t nc, const int32_t* __restrict__ sk, uint32_t* cptr) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < nnz; j += int64_t(gridDim.x) * kBlock) {
+    const int64_t k = sk[j], prev = j == 0 ? -1 : sk[j - 1];
+    for (int64_t c = prev + 1; c <= k; c++)
+      cptr[c] = uint32_t(j);
+    if (j == nnz - 1)
+      for (int64_t c = k + 1; c <= nc; c++)
+        cptr[c] = uint32_t(nnz);
   }
 }
 
@@ -283,15 +324,30 @@ __global__ void __launch_bounds__(kBlock)
     cvar0[i] = int32_t(i);
     const int64_t b = r.v_ebase[v];
     const int n = r.v_n[v];
-    for (int j = 0; j < n; j++) {
-      const int32_t p = pos[r.e_cnst[b + j]];
-      if (p >= 0 && lany[p] && r.e_w[b + j] > 0) {
-        csr_c[k] = int32_t(dcl[p]);
-        csr_w[k] = r.e_w[b + j];
-        rowid[k] = int32_t(i);
-        kidx[k] = int32_t(k);
-        k++;
+    for (int j0 = 0; j0 < n; j0 += kRsU) {  // kRsU elements' loads in flight together, slab order kept
+      int32_t p[kRsU];
+      double w[kRsU];
+#pragma unroll
+      for (int u = 0; u < kRsU; u++) {
+        p[u] = j0 + u < n ? r.e_cnst[b + j0 + u] : -1;
+        w[u] = j0 + u < n ? r.e_w[b + j0 + u] : 0.0;
       }
+#pragma unroll
+      for (int u = 0; u < kRsU; u++)
+        p[u] = p[u] >= 0 ? pos[p[u]] : -1;
+      int64_t dc[kRsU];
+#pragma unroll
+      for (int u = 0; u < kRsU; u++)
+        dc[u] = p[u] >= 0 && w[u] > 0 && lany[p[u]] ? dcl[p[u]] : -1;
+#pragma unroll
+      for (int u = 0; u < kRsU; u++)
+        if (dc[u] >= 0) {
+          csr_c[k] = int32_t(dc[u]);
+          csr_w[k] = w[u];
+          rowid[k] = int32_t(i);
+          kidx[k] = int32_t(k);
+          k++;
+        }
     }
   }
 }
