@@ -42,6 +42,19 @@ __global__ void __launch_bounds__(kBlock) mm_dup_check(Dev s) {
         s.cdup[s.csr_c[i]] = 1;
       continue;
     }
+    if (e - b <= 16) {  // the row in registers, its loads in flight together
+      int32_t cc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        cc[i] = b + i < e ? s.csr_c[b + i] : -1 - i;
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+#pragma unroll
+        for (int j = i + 1; j < 16; j++)
+          if (cc[i] >= 0 && cc[i] == cc[j])
+            s.cdup[cc[i]] = 1;
+      continue;
+    }
     for (uint32_t i = b; i < e; i++)
       for (uint32_t j = i + 1; j < e; j++)
         if (s.csr_c[i] == s.csr_c[j])
