@@ -1187,12 +1187,16 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // Host view of the sizes (upper bounds: rows and constraints only leave), refreshed at every poll; they
   // size grids only, the kernels read the exact counts from the control words.
   int64_t r = 0, last_compact = 0, last_clist = 0, nrows = d.nV, ncl = d.nC;
-  // Termination polls are pipelined: the control words after chunk k are copied into a pinned slot behind
-  // an event, chunk k+1 is queued, then the host waits for chunk k's copy — the GPU never idles on the
-  // host.  A chunk queued after the last round is a run of launches that return at once (CTL_DONE).
+  // Termination polls are pipelined: the control words after chunk k are written into a pinned slot by a
+  // one-wave kernel (mm_ctl_out) behind an event, chunk k+1 is queued, then the host waits for chunk k's
+  // words — the GPU never idles on the host.  A chunk queued after the last round is a run of launches
+  // that return at once (CTL_DONE).
   int chunk = 2, slot = 0;
   bool pending = false;
   int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
+  int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
+  for (int k = 0; k < 2; k++)
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
   for (;;) {
     const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
@@ -1224,7 +1228,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     }
     if (cl || cm)
       LAUNCH(6, r, mm_flip, 1, 1, d, int(cl), int(cm));
-    HIPCHK(hipMemcpyAsync(hc[slot], d.ctl, CTL_WORDS * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
     HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
     if (pending) {  // the previous chunk's words (this chunk is queued behind them)
       HIPCHK(hipEventSynchronize(c->ev_poll[slot ^ 1]));

@@ -374,6 +374,16 @@ __global__ void __launch_bounds__(kBlock) mm_clist(Dev s, int from_all) {
   }
 }
 
+// The control words into a pinned host slot, written by the GPU itself (mapped memory, system-scope release):
+// a copy-engine transfer on the stream cost a 20-40 us gap before the next kernel at every poll (~1 ms per C2
+// solve in the rocprofv3 trace).
+__global__ void mm_ctl_out(Dev s, int32_t* dst) {
+  const int i = threadIdx.x;
+  if (i < CTL_WORDS)
+    __hip_atomic_store(dst + i, s.ctl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
 // After a list re-compaction and / or a row compaction: switch the buffers in use (one thread).
 __global__ void mm_flip(Dev s, int clist, int rows) {
   if (s.ctl[CTL_DONE])
