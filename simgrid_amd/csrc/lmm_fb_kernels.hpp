@@ -356,33 +356,34 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
         if (lane == 0) {
           const int n = int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave));
           if (nonneg) {
-            // 16 increments per step, the next 16 read from LDS while these are chained (slots past n
+            // kG increments per step, the next kG read from LDS while these are chained (slots past n
             // hold 0.0: r - 0 == r); two register sets used in turn, so nothing is copied between steps
+            constexpr int kG = 32, kH = kG / 2;
             const double2* dd = reinterpret_cast<const double2*>(d);
-            double2 ra[8], rb[8];
+            double2 ra[kH], rb[kH];
 #pragma unroll
-            for (int t = 0; t < 8; t++)
+            for (int t = 0; t < kH; t++)
               ra[t] = dd[t];
-            for (int k = 0; k < n; k += 32) {
-              if (k + 16 < n) {
+            for (int k = 0; k < n; k += 2 * kG) {
+              if (k + kG < n) {
 #pragma unroll
-                for (int t = 0; t < 8; t++)
-                  rb[t] = dd[(k + 16) / 2 + t];
+                for (int t = 0; t < kH; t++)
+                  rb[t] = dd[(k + kG) / 2 + t];
               }
 #pragma unroll
-              for (int t = 0; t < 8; t++) {
+              for (int t = 0; t < kH; t++) {
                 rem -= ra[t].x;
                 rem -= ra[t].y;
               }
-              if (k + 16 >= n)
+              if (k + kG >= n)
                 break;
-              if (k + 32 < n) {
+              if (k + 2 * kG < n) {
 #pragma unroll
-                for (int t = 0; t < 8; t++)
-                  ra[t] = dd[(k + 32) / 2 + t];
+                for (int t = 0; t < kH; t++)
+                  ra[t] = dd[(k + 2 * kG) / 2 + t];
               }
 #pragma unroll
-              for (int t = 0; t < 8; t++) {
+              for (int t = 0; t < kH; t++) {
                 rem -= rb[t].x;
                 rem -= rb[t].y;
               }
