@@ -142,43 +142,107 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
 
 // :89-105 — per listed variable: mu = min(usage/w, bound - value); value += mu; exact
 // `value == bound` drops it from the list.
+// :89-105 once the minimum of usage / w over the row is known: bound, value, exact `value == bound` delisting.
+__device__ __forceinline__ int var_inc_finish(const Dev& s, int64_t v, double inc, int round) {
+  const double vb = s.vbound[v];
+  double x = s.x[v];
+  if (vb > 0)
+    inc = fmin(inc, vb - x);
+  s.vtmp[v] = inc;
+  x += inc;
+  s.x[v] = x;
+  s.fixr[v] = round;  // last round in which v was listed
+  if (x == vb) {
+    s.vst[v] = 0;
+    return 0;
+  }
+  return 1;
+}
+
+// Wave-cooperative (waves with at least 16 listed rows): a wave takes 64 consecutive variables, whose rows are one contiguous CSR range; the lanes
+// read that range coalesced (the u-th element of 64 rows per load touched ~64 lines) and min-reduce each
+// element's usage / w into its row's slot in LDS (64-bit atomic min of the non-negative doubles' bits: the
+// same minimum as a sequential fmin).
 __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) {
   if (s.ctl[CTL_DONE])
     return;
+  __shared__ unsigned long long mn[kBlock];
+  __shared__ uint32_t rb[kBlock];
+  __shared__ uint8_t rl[kBlock];
+  const int lane = threadIdx.x & (kWave - 1);
+  unsigned long long* wmn = mn + (threadIdx.x - lane);
+  uint32_t* wrb = rb + (threadIdx.x - lane);
+  uint8_t* wrl = rl + (threadIdx.x - lane);
+  const unsigned long long kMaxBits = (unsigned long long)__double_as_longlong(DBL_MAX);
   int any = 0;
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
-    if (!s.vst[v])
+  for (int64_t base = int64_t(blockIdx.x) * kBlock + (threadIdx.x - lane); base < s.nV;
+       base += int64_t(gridDim.x) * kBlock) {  // wave-uniform
+    const int64_t v = base + lane;
+    const bool in = v < s.nV;
+    const bool listed = in && s.vst[v];
+    const uint32_t b = in ? s.var_ptr[v] : 0u, e = in ? s.var_ptr[v + 1] : 0u;
+    const int nlisted = __popcll(__ballot(listed));
+    if (nlisted == 0)
       continue;
-    double inc = DBL_MAX;  // (a min: any order gives the same value)
-    const uint32_t b = s.var_ptr[v], e = s.var_ptr[v + 1];
-    for (uint32_t j0 = b; j0 < e; j0 += 4) {  // 4 elements' loads in flight together
-      int32_t cc[4];
-      double ww[4], uu[4];
+    if (nlisted < kWave / 4) {  // few listed rows (late rounds): each listed lane reads its own row
+      if (!listed)
+        continue;
+      double inc = DBL_MAX;
+      for (uint32_t j0 = b; j0 < e; j0 += 4) {  // 4 elements' loads in flight together
+        int32_t cc[4];
+        double ww[4], uu[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        cc[k] = j0 + k < e ? s.csr_c[j0 + k] : -1;
-        ww[k] = j0 + k < e ? s.csr_w[j0 + k] : 1.0;
+        for (int k = 0; k < 4; k++) {
+          cc[k] = j0 + k < e ? s.csr_c[j0 + k] : -1;
+          ww[k] = j0 + k < e ? s.csr_w[j0 + k] : 1.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          uu[k] = cc[k] >= 0 ? s.use[cc[k]] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (cc[k] >= 0)
+            inc = fmin(inc, uu[k] / ww[k] + 0.0);
+      }
+      any |= var_inc_finish(s, v, inc, round);
+      continue;
+    }
+    const int last = int(s.nV - 1 - base < kWave - 1 ? s.nV - 1 - base : kWave - 1);
+    const uint32_t B = __shfl(b, 0, kWave), E = __shfl(e, last, kWave);
+    wmn[lane] = kMaxBits;
+    wrb[lane] = in ? b : 0xFFFFFFFFu;  // (lanes past nV never own an element)
+    wrl[lane] = listed;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t f0 = B; f0 < E; f0 += 2 * kWave) {  // wave-uniform, 2 loads per array in flight
+      int32_t cc[2];
+      double ww[2], uu[2];
+      int ow[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t f = f0 + u * kWave + lane;
+        cc[u] = f < E ? s.csr_c[f] : -1;
+        ww[u] = f < E ? s.csr_w[f] : 1.0;
+        int o = 0;  // owner: the last lane whose row starts at or before f
+#pragma unroll
+        for (int st = kWave / 2; st > 0; st >>= 1)
+          if (wrb[o + st] <= f)
+            o += st;
+        ow[u] = o;
+        if (cc[u] >= 0 && !wrl[o])
+          cc[u] = -1;
       }
 #pragma unroll
-      for (int k = 0; k < 4; k++)
-        uu[k] = cc[k] >= 0 ? s.use[cc[k]] : 0.0;
+      for (int u = 0; u < 2; u++)
+        uu[u] = cc[u] >= 0 ? s.use[cc[u]] : 0.0;
 #pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (cc[k] >= 0)
-          inc = fmin(inc, uu[k] / ww[k]);
+      for (int u = 0; u < 2; u++)
+        if (cc[u] >= 0)
+          atomicMin(&wmn[ow[u]], (unsigned long long)__double_as_longlong(uu[u] / ww[u] + 0.0));
     }
-    const double vb = s.vbound[v];
-    double x = s.x[v];
-    if (vb > 0)
-      inc = fmin(inc, vb - x);
-    s.vtmp[v] = inc;
-    x += inc;
-    s.x[v] = x;
-    if (x == vb)
-      s.vst[v] = 0;
-    else
-      any = 1;
-    s.fixr[v] = round;  // last round in which v was listed
+    __builtin_amdgcn_wave_barrier();
+    if (listed)
+      any |= var_inc_finish(s, v, __longlong_as_double((long long)wmn[lane]), round);
+    __builtin_amdgcn_wave_barrier();
   }
   if (__any(any) && (threadIdx.x & (kWave - 1)) == 0)
     s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
