@@ -380,8 +380,9 @@ def run_config(args):
         split over the ranks in nnz-balanced blocks): strong scaling, no data-path collective;
     c4  LV08 flows on a 4096-host fat tree (SMPI-style cluster, crosstraffic on), maxmin: one giant
         component, so replicas (weak scaling);
-    c5  L07 flows on a 4096-host dragonfly, FairBottleneck, variables sharded over the ranks with the
-        per-round all-reduces of multi.fb_solve_sharded (strong scaling).
+    c5  L07 flows on a 4096-host dragonfly, FairBottleneck; at N > 1 sharded over the ranks (variables and
+        owned constraints, multi.FbShardPlan: per round one all-reduce of counts and two all-gathers,
+        bit-identical to the one-context solve), strong scaling.
     One step = one full solve with the inputs resident in HBM."""
     import numpy as np
     import torch
@@ -437,14 +438,16 @@ def run_config(args):
         work_vars, scaling = flows, "strong"
         desc = dict(workload=f"C5: {flows} L07 flows on dragonfly {C5_PLATFORM['topo_parameters']} (4096 hosts), "
                              "FairBottleneck", flows=flows)
-        if world > 1:  # variables sharded over the ranks, the per-round reductions all-reduced
+        if world > 1:  # variables and owned constraints sharded over the ranks (multi.FbShardPlan)
             f = M.export_flat(s)
             del s
-            sub, _ = M.shard_variables(f, world)[rank]
-            shards = [M.DeviceFbShard(sub)]
-            nV_total, nC_total = len(f.penalty), len(f.cbound)
-            del f
-            desc["parallelism"] = f"variables sharded x{world}, 2 all-reduces per round"
+            plan = M.FbShardPlan(f, world)
+            gather = M.FbGather(plan)
+            shards = [M.DeviceFbShard(plan, rank, gather)]
+            sub_n = (shards[0].n, len(f.cbound), int(np.diff(f.var_ptr)[plan.vb[rank]:plan.vb[rank + 1]].sum()))
+            del f, plan
+            desc["parallelism"] = (f"variables + owned constraints sharded x{world}: per round 1 all-reduce"
+                                   " (counts) + 2 all-gathers (mu, remaining)")
         else:  # one GPU: the drop-in FairBottleneck::solve path (element order of the reference, bit-identical)
             desc["parallelism"] = "one context (System::solve, fbk_update_seq)"
     if batch is not None:
@@ -454,7 +457,7 @@ def run_config(args):
         st = s.last_stats()
         nV, nC, nnz = st["n_var"], st["n_cnst"], st["nnz"]
     else:
-        nV, nC, nnz = len(sub.penalty), len(sub.cbound), len(sub.cnst_idx)
+        nV, nC, nnz = sub_n
     log(f"[rank {rank}] {args.workload}: built in {time.time() - t:.1f}s: nV={nV} nC={nC} nnz={nnz}")
 
     def step():
@@ -466,7 +469,7 @@ def run_config(args):
             return s.last_stats()["rounds"]
         for sh in shards:
             sh.begin()
-        return M.fb_solve_sharded(shards, ex, nV_total, nC_total)
+        return M.fb_solve_sharded(shards, ex, gather)
 
     for _ in range(args.warmup):
         step()

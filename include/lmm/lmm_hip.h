@@ -192,18 +192,28 @@ int lmmhip_persist_profile(lmmhip_ctx* ctx, int on, int64_t* t, int64_t cap, int
  * arrival of workgroup b at barrier g, t[... + 1] = its exit. */
 int lmmhip_persist_profile_blocks(lmmhip_ctx* ctx, int64_t* t, int64_t cap, int64_t* nbar, int64_t* nblk);
 
-/* FairBottleneck with the variables sharded over ranks (simgrid_amd/multi.py).  The
- * context holds this rank's variables and EVERY constraint (constraint indices are global).  A round
- * (fair_bottleneck.cpp:59-145) is three phases; between them the caller all-reduces the exchange
- * buffers over the ranks, on the context's stream:
- *   step(0) -> xnb[0..n_cnst) listed variables per constraint, xnb[n_cnst] variables still listed;
- *              all-reduce SUM xnb
- *   step(1) -> shares, increments; xsum = sum of w*mu per shared constraint, xmin = min of w*mu per
- *              FATPIPE constraint; all-reduce SUM xsum, MIN xmin
- *   step(2) -> remaining, erasure and delisting (identical decisions on every rank)
- * xnb (int32[n_cnst+1]), xsum, xmin (double[n_cnst]) are device buffers owned by the caller.  The
- * solve is over when poll() reports done (the same round on every rank: it is decided from xnb). */
-int lmmhip_fb_shard_begin(lmmhip_ctx* ctx, double precision, int32_t* xnb, double* xsum, double* xmin);
+/* FairBottleneck sharded over ranks (simgrid_amd/multi.py FbShardPlan), bit-identical to
+ * the one-context solve and to the reference.  Each shard (one context) holds
+ *   - a block of the variables: lmmhip_upload2 of their rows with EVERY constraint (global constraint ids);
+ *   - a block of OWNED constraints (lmmhip_fb_shard_owner): each one's full element list in the reference's
+ *     enabled_element_set_ order (fair_bottleneck.cpp:111-116), as (position of the element's variable in the
+ *     gathered mu vector, weight); cpos[k] = position of constraint k's remaining in the gathered remaining
+ *     vector; n_mu / n_rem = lengths of those two vectors.
+ * A round (fair_bottleneck.cpp:59-145) is four phases; between them the caller exchanges, on the context's
+ * stream:
+ *   step(0) -> xnb[0..n_cnst) listed variables of this shard per constraint, xnb[n_cnst] = some variable of
+ *              this shard still listed;                                     all-reduce SUM xnb
+ *   step(1) -> shares, this shard's mu into xmu[mu_off .. mu_off + n_var);  all-gather xmu
+ *   step(2) -> the owned constraints' remaining (the reference's per-element double_update chain over the
+ *              gathered mu) into xrem[cpos[k]];                             all-gather xrem
+ *   step(3) -> remaining of every listed constraint from xrem, erasure, delisting of this shard's variables
+ * xnb (int32[n_cnst+1]), xmu (double[n_mu]), xrem (double[n_rem]) are device buffers owned by the caller.
+ * The solve is over when poll() reports done (the same round on every shard: decided from xnb). */
+int lmmhip_fb_shard_owner(lmmhip_ctx* ctx, int64_t n_own, const int32_t* own_cnst, const int64_t* optr,
+                          const int32_t* ovar, const double* oweight, const int32_t* cpos, int64_t n_mu,
+                          int64_t n_rem);
+int lmmhip_fb_shard_begin(lmmhip_ctx* ctx, double precision, int32_t* xnb, double* xmu, int64_t mu_off,
+                          double* xrem);
 int lmmhip_fb_shard_step(lmmhip_ctx* ctx, int phase);
 int lmmhip_fb_shard_poll(lmmhip_ctx* ctx, int* done, int64_t* rounds); /* synchronises the stream */
 

@@ -122,6 +122,11 @@ struct lmmhip_ctx* lmm_system_device_ctx(lmm_sys* s);
  * id.  Used by simgrid_amd/multi.py to split a system into connected components across GPUs. */
 int lmm_flat_export(lmm_sys* s, int64_t* counts3, int64_t* var_ptr, int32_t* cnst_idx, double* weight, double* penalty,
                     double* vbound, double* cbound, uint8_t* cflags, int64_t* var_ids);
+/* The order of each constraint's elements in that flattened system (as lmmhip_upload2's csc_order: the
+ * CSR indices of constraint 0's elements, then constraint 1's, ...): the reference's enabled_element_set_
+ * order for a FairBottleneck system (the order its per-element chain subtracts in, fair_bottleneck.cpp:
+ * 111-116), ascending CSR order for a max-min one.  nnz must equal lmm_flat_export's count. */
+int lmm_flat_export_order(lmm_sys* s, int64_t nnz, int64_t* csc_order);
 /* Solve n independent systems as one device launch sequence (disjoint union). */
 int lmm_solve_batch(lmm_sys** systems, int n);
 

@@ -359,6 +359,32 @@ int lmm_flat_export(lmm_sys* s, int64_t* counts3, int64_t* var_ptr, int32_t* cns
   }
 }
 
+int lmm_flat_export_order(lmm_sys* s, int64_t nnz, int64_t* csc_order) {
+  try {
+    System::Flat f;
+    s->sys.flatten_into(f);
+    if (int64_t(f.cnst_idx.size()) != nnz || (nnz > 0 && !csc_order)) {
+      g_err = "lmm_flat_export_order: nnz differs from the flattened system's";
+      return -1;
+    }
+    if (int64_t(f.csc_order.size()) == nnz) {
+      std::copy(f.csc_order.begin(), f.csc_order.end(), csc_order);
+      return 0;
+    }
+    std::vector<int64_t> cur(f.cbound.size() + 1, 0);  // ascending CSR order per constraint
+    for (int32_t k : f.cnst_idx)
+      cur[size_t(k) + 1]++;
+    for (size_t k = 0; k < f.cbound.size(); k++)
+      cur[k + 1] += cur[k];
+    for (int64_t j = 0; j < nnz; j++)
+      csc_order[cur[size_t(f.cnst_idx[size_t(j)])]++] = j;
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 int lmm_solve_batch(lmm_sys** systems, int n) {
   try {
     std::vector<System*> v(size_t(n > 0 ? n : 0));

@@ -154,9 +154,8 @@ struct Dev {
   int32_t* pcnt;             // [nch] listed variables per chunk
   double* pacc;              // [nch] sum / min of w*mu per chunk
   uint8_t* erased;           // [nC] erased in the current round
-  int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag), all-reduce SUM
-  double* xsum;              // [nC] sum of w*mu per shared constraint, all-reduce SUM
-  double* xmin;              // [nC] min of w*mu per FATPIPE constraint, all-reduce MIN
+  int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag); sharded: all-reduce SUM
+  double* xmin;              // [nC] one context: min of w*mu per FATPIPE constraint
   double* fbd;               // [nnz] one context: w*mu of every shared constraint's element, CSC order
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements

@@ -2,13 +2,14 @@
 //
 // One reference round (fair_bottleneck.cpp:59-145) is Jacobi-style: every constraint's share is
 // computed before any variable moves, every variable's increment before any constraint is updated.
-// The device round is the same three phases; the two per-constraint reductions between them go
-// through exchange buffers so that a variable-sharded solve (multi.py) can all-reduce
-// them across ranks between the phases:
-//   phase 0  fbk_count, fbk_nb      listed-variable count per constraint          -> xnb  (SUM)
-//   phase 1  fbk_share, fb_var_inc, fbk_acc, fbk_accc
-//                                   shares, increments, sum / min of w*mu          -> xsum (SUM), xmin (MIN)
-//   phase 2  fbk_update, fbk_unlist remaining, erasure, delisting
+// The device round is the same phases:
+//   phase 0  fb_pack_vst, fbk_count, fbk_nb   listed-variable count per constraint -> xnb
+//   phase 1  fbk_share, fb_var_inc            shares, increments mu
+//            fbk_acc, fbk_accc                (one context) increments w*mu in CSC order, FATPIPE minima
+//   phase 2  fbk_update_seq, fbk_unlist       remaining (the reference's element-by-element chain), erasure,
+//                                             delisting
+// A variable-sharded solve (multi.py) runs the same kernels for its variables plus the constraint-owner
+// kernels below (fbo_*), with the exchanges between the phases described there.
 // Element work is cut into CSC chunks of at most kFbChunk elements (one wave each), so a constraint
 // with 10^6 elements (a CPU under thousands of flows, C5) spreads over the chip instead of
 // serialising one wave; per-chunk partials are combined per constraint in chunk order, so every
@@ -248,13 +249,14 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
     s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
 }
 
-// :107-127 — per chunk of a listed constraint: sum (or FATPIPE: min) of w*mu over ALL its elements
-// (the stale mu of variables that already left the list included).  fat_only (one context): the shared
-// constraints' sums are not needed — fbk_update_seq takes their elements one at a time itself — so only
-// FATPIPE chunks are reduced (one pass of w * mu gathers per round less).
-// fat_only also writes the shared constraints' increments w * mu in CSC order into fbd (element-parallel,
-// all gathers of the round spread over the chip), which fbk_update_seq then streams.
-__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int fat_only) {
+// :107-127 — per chunk of a listed constraint.  FATPIPE: min of w*mu over ALL its elements (the stale mu of
+// variables that already left the list included) -> pacc.  Shared: the increments w * mu in CSC order into
+// fbd (element-parallel, all gathers of the round spread over the chip), which fbk_update_seq then chains
+// one at a time; only the elements of variables listed this round are rewritten: a delisted variable's mu
+// (vtmp) no longer moves, so its increment written in its last listed round still holds (every variable is
+// listed in round 0, a listed constraint was listed in every earlier round); vstb = the flags before
+// fb_var_inc.
+__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
   if (s.ctl[CTL_DONE])
     return;
   const int lane = threadIdx.x & (kWave - 1);
@@ -264,10 +266,7 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int fat_only) {
     const bool fat = s.cflags[c] & 1;
     if (s.ratio[c] != 0.0)
       continue;
-    if (fat_only && !fat) {
-      // only the elements of variables listed this round: a delisted variable's mu (vtmp) no longer
-      // moves, so its increment written in its last listed round still holds (every variable is listed in
-      // round 0, a listed constraint was listed in every earlier round); vstb = the flags before fb_var_inc
+    if (!fat) {
       const uint32_t e = chunk_end(s, q, c);
       for (uint32_t j0 = s.ch_beg[q] + lane; j0 < e; j0 += 4 * kWave) {  // 4 gathers in flight per lane
         int32_t vv[4];
@@ -291,86 +290,136 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int fat_only) {
       }
       continue;
     }
-    double acc = fat ? dinf() : 0.0;
-    for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave) {
-      const double d = s.csc_w[j] * s.vtmp[s.csc_v[j]];
-      acc = fat ? fmin(acc, d) : acc + d;
-    }
-    acc = fat ? wave_min(acc) : wave_sum(acc);
+    double acc = dinf();
+    for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave)
+      acc = fmin(acc, s.csc_w[j] * s.vtmp[s.csc_v[j]]);
+    acc = wave_min(acc);
     if (lane == 0)
       s.pacc[q] = acc;
   }
 }
 
-// per constraint: chunk partials in chunk order -> xsum (shared) / xmin (FATPIPE); the other one
-// gets the neutral element of its all-reduce
-__global__ void __launch_bounds__(kBlock) fbk_accc(Dev s, int fat_only) {
+// per FATPIPE constraint: chunk minima in chunk order -> xmin
+__global__ void __launch_bounds__(kBlock) fbk_accc(Dev s) {
   if (s.ctl[CTL_DONE])
     return;
   for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
-    double sum = 0.0, mn = dinf();
-    if (s.ratio[c] == 0.0) {
-      if (s.cflags[c] & 1)
-        for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
-          mn = fmin(mn, s.pacc[q]);
-      else if (!fat_only)
-        for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
-          sum += s.pacc[q];
-    }
-    s.xsum[c] = sum;
+    double mn = dinf();
+    if (s.ratio[c] == 0.0 && (s.cflags[c] & 1))
+      for (int q = s.c_ch[c]; q < s.c_ch[c + 1]; q++)
+        mn = fmin(mn, s.pacc[q]);
     s.xmin[c] = mn;
   }
 }
 
-// :110-140 — remaining -= sum w*mu (FATPIPE: remaining -= min(usage, min w*mu)), clamped at the
-// precision; remaining <= 0 erases the constraint.  Same inputs on every shard, same decision.
-__global__ void __launch_bounds__(kBlock) fbk_update(Dev s, double prec) {
-  if (s.ctl[CTL_DONE])
-    return;
-  for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
-    s.erased[c] = 0;
-    if (s.ratio[c] != 0.0)
-      continue;
-    double rem = s.rem[c];
-    if (s.cflags[c] & 1) {
-      double u = s.use[c];
-      if (s.cflags[c] & 2)
-        u = fmin(u, 0.0);
-      u = fmin(u, s.xmin[c]);
-      s.use[c] = u;
-      rem -= u;
-    } else {
-      rem -= s.xsum[c];
-    }
-    if (rem < prec)
-      rem = 0.0;
-    s.rem[c] = rem;
-    if (rem <= 0.0) {
-      s.ratio[c] = dinf();
-      s.erased[c] = 1;
-    }
-  }
+// :118-125 — FATPIPE: usage = min(usage, w * mu over the enabled elements) (an enabled zero-weight element,
+// cflags bit1, gives 0), remaining -= usage, clamped (double_update, surf_interface.hpp:34-44)
+__device__ __forceinline__ double fb_fat_update(const Dev& s, int64_t c, double rem, double elem_min, double prec,
+                                                double* use_out) {
+  double u = s.use[c];
+  if (s.cflags[c] & 2)
+    u = fmin(u, 0.0);
+  u = fmin(u, elem_min);
+  *use_out = u;
+  rem -= u;
+  if (rem < prec)
+    rem = 0.0;
+  return rem;
 }
 
-// :107-140 for ONE context: a shared constraint's remaining takes its elements' w * mu ONE AT A TIME in
-// the CSC order, each step a double_update (surf_interface.hpp:34-44) — the reference's own loop
-// (fair_bottleneck.cpp:111-116) operation for operation, so with the CSC in enabled_element_set_ order
-// (lmmhip_upload2) the result is bit-identical.  Not an order-free sum: the saturating constraint's
-// remaining ends a few ulps of its bound away from 0, and whether that residue is below the precision
-// (erasure, :129) depends on the rounding of this exact chain — a tree sum is more accurate and erases
-// constraints the reference keeps (C5 at 1e6 flows: 28 of them in round 0, a different fixed point for
-// 12 % of the flows).  One wave per constraint; FATPIPE as fbk_update.
+// :110-116 — a shared constraint's remaining takes its elements' increments w * mu ONE AT A TIME in the
+// CSC order (fbd[cb..ce)), each step a double_update (surf_interface.hpp:34-44) — the reference's own loop
+// operation for operation, so with the CSC in enabled_element_set_ order the result is bit-identical.  Not
+// an order-free sum: the saturating constraint's remaining ends a few ulps of its bound away from 0, and
+// whether that residue is below the precision (erasure, :129) depends on the rounding of this exact chain —
+// a tree sum is more accurate and erases constraints the reference keeps (C5 at 1e6 flows: 28 of them in
+// round 0, a different fixed point for 12 % of the flows).  Called by a whole wave; the result is lane 0's.
 //
 // The chain is the critical path (C5's global dragonfly links hold ~1.6e5 elements), so it is fed without
-// waiting: the increments were computed element-parallel by fbk_acc (fbd, CSC order); the lanes stream
-// kSeqP x 64 of them into LDS and issue the loads of the next kSeqP x 64 before lane 0 chains the current
-// ones (a gather per element here left the long chains waiting on memory under load: 4.3 ms per round).  And when every increment of a batch is >= 0 the clamp is taken
-// once at its end: fl(r - d) <= r for d >= 0, so the unclamped remaining only decreases; the clamped chain
-// equals it until its first value below the precision and is 0 from there on (0 - d < precision), i.e. the
-// clamped result is 0 exactly when the unclamped end value is below the precision, and that end value
-// otherwise.  A batch holding a negative (or NaN) increment takes the clamp at every step.
+// waiting: the lanes stream kSeqP x 64 increments into LDS (`d`, kSeqP * 64 doubles of this wave) and issue
+// the loads of the next kSeqP x 64 before lane 0 chains the current ones.  And when every increment of a
+// batch is >= 0 the clamp is taken once at its end: fl(r - d) <= r for d >= 0, so the unclamped remaining
+// only decreases; the clamped chain equals it until its first value below the precision and is 0 from there
+// on (0 - d < precision), i.e. the clamped result is 0 exactly when the unclamped end value is below the
+// precision, and that end value otherwise.  A batch holding a negative (or NaN) increment takes the clamp
+// at every step.
 constexpr int kSeqP = 8;  // 64-element blocks per batch
 
+__device__ __forceinline__ double fb_chain(const double* __restrict__ fbd, uint32_t cb, uint32_t ce, double rem,
+                                           double prec, double* d, int lane) {
+  double nx[kSeqP];
+#pragma unroll
+  for (int p = 0; p < kSeqP; p++) {
+    const uint32_t j = cb + p * kWave + lane;
+    nx[p] = j < ce ? fbd[j] : 0.0;
+  }
+  for (uint32_t base = cb; base < ce; base += kSeqP * kWave) {  // wave-uniform
+    bool nonneg = true;
+#pragma unroll
+    for (int p = 0; p < kSeqP; p++) {
+      d[p * kWave + lane] = nx[p];
+      nonneg &= nx[p] >= 0.0;
+    }
+    nonneg = __all(nonneg);
+    const uint32_t nb = base + kSeqP * kWave;
+#pragma unroll
+    for (int p = 0; p < kSeqP; p++) {  // the next batch's loads, in flight during the chain
+      const uint32_t j = nb + p * kWave + lane;
+      nx[p] = j < ce ? fbd[j] : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      const int n = int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave));
+      if (nonneg) {
+        // kG increments per step, the next kG read from LDS while these are chained (slots past n
+        // hold 0.0: r - 0 == r); two register sets used in turn, so nothing is copied between steps
+        constexpr int kG = 32, kH = kG / 2;
+        const double2* dd = reinterpret_cast<const double2*>(d);
+        double2 ra[kH], rb[kH];
+#pragma unroll
+        for (int t = 0; t < kH; t++)
+          ra[t] = dd[t];
+        for (int k = 0; k < n; k += 2 * kG) {
+          if (k + kG < n) {
+#pragma unroll
+            for (int t = 0; t < kH; t++)
+              rb[t] = dd[(k + kG) / 2 + t];
+          }
+#pragma unroll
+          for (int t = 0; t < kH; t++) {
+            rem -= ra[t].x;
+            rem -= ra[t].y;
+          }
+          if (k + kG >= n)
+            break;
+          if (k + 2 * kG < n) {
+#pragma unroll
+            for (int t = 0; t < kH; t++)
+              ra[t] = dd[(k + 2 * kG) / 2 + t];
+          }
+#pragma unroll
+          for (int t = 0; t < kH; t++) {
+            rem -= rb[t].x;
+            rem -= rb[t].y;
+          }
+        }
+        if (rem < prec)
+          rem = 0.0;
+      } else {
+        for (int k = 0; k < n; k++) {
+          rem -= d[k];
+          if (rem < prec)
+            rem = 0.0;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  return rem;
+}
+
+// :107-140 for ONE context: one wave per listed constraint, shared ones through fb_chain over fbd (written by
+// fbk_acc), FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0 erases the constraint (:129).
 __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
   if (s.ctl[CTL_DONE])
     return;
@@ -385,85 +434,12 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
       continue;
     double rem = s.rem[c];
     if (s.cflags[c] & 1) {
-      double u = s.use[c];
-      if (s.cflags[c] & 2)
-        u = fmin(u, 0.0);
-      u = fmin(u, s.xmin[c]);
+      double u;
+      rem = fb_fat_update(s, c, rem, s.xmin[c], prec, &u);
       if (lane == 0)
         s.use[c] = u;
-      rem -= u;
-      if (rem < prec)
-        rem = 0.0;
     } else {
-      const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
-      double nx[kSeqP];
-#pragma unroll
-      for (int p = 0; p < kSeqP; p++) {
-        const uint32_t j = cb + p * kWave + lane;
-        nx[p] = j < ce ? s.fbd[j] : 0.0;
-      }
-      for (uint32_t base = cb; base < ce; base += kSeqP * kWave) {  // wave-uniform
-        bool nonneg = true;
-#pragma unroll
-        for (int p = 0; p < kSeqP; p++) {
-          d[p * kWave + lane] = nx[p];
-          nonneg &= nx[p] >= 0.0;
-        }
-        nonneg = __all(nonneg);
-        const uint32_t nb = base + kSeqP * kWave;
-#pragma unroll
-        for (int p = 0; p < kSeqP; p++) {  // the next batch's loads, in flight during the chain
-          const uint32_t j = nb + p * kWave + lane;
-          nx[p] = j < ce ? s.fbd[j] : 0.0;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          const int n = int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave));
-          if (nonneg) {
-            // kG increments per step, the next kG read from LDS while these are chained (slots past n
-            // hold 0.0: r - 0 == r); two register sets used in turn, so nothing is copied between steps
-            constexpr int kG = 32, kH = kG / 2;
-            const double2* dd = reinterpret_cast<const double2*>(d);
-            double2 ra[kH], rb[kH];
-#pragma unroll
-            for (int t = 0; t < kH; t++)
-              ra[t] = dd[t];
-            for (int k = 0; k < n; k += 2 * kG) {
-              if (k + kG < n) {
-#pragma unroll
-                for (int t = 0; t < kH; t++)
-                  rb[t] = dd[(k + kG) / 2 + t];
-              }
-#pragma unroll
-              for (int t = 0; t < kH; t++) {
-                rem -= ra[t].x;
-                rem -= ra[t].y;
-              }
-              if (k + kG >= n)
-                break;
-              if (k + 2 * kG < n) {
-#pragma unroll
-                for (int t = 0; t < kH; t++)
-                  ra[t] = dd[(k + 2 * kG) / 2 + t];
-              }
-#pragma unroll
-              for (int t = 0; t < kH; t++) {
-                rem -= rb[t].x;
-                rem -= rb[t].y;
-              }
-            }
-            if (rem < prec)
-              rem = 0.0;
-          } else {
-            for (int k = 0; k < n; k++) {
-              rem -= d[k];
-              if (rem < prec)
-                rem = 0.0;
-            }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
+      rem = fb_chain(s.fbd, s.cnst_ptr[c], s.cnst_ptr[c + 1], rem, prec, d, lane);
     }
     if (lane == 0) {
       s.rem[c] = rem;
@@ -471,6 +447,119 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
         s.ratio[c] = dinf();
         s.erased[c] = 1;
       }
+    }
+  }
+}
+
+// ---- variable-sharded solve, constraint owners (simgrid_amd/multi.py FbShardPlan) ----
+// Every shard holds a block of the variables (CSR rows, and a CSC of ALL constraints restricted to them:
+// counts, delisting) and OWNS a block of the constraints: their full element lists in the reference's
+// enabled_element_set_ order, with each element's variable given as its position in the gathered mu
+// vector.  A round is four phases, the caller exchanging between them:
+//   0  counts of the shard's listed variables per constraint      -> xnb      all-reduce SUM (integers: exact)
+//   1  shares (replicated constraint state), the shard's mu      -> xmu      all-gather
+//   2  owned constraints: increments from the gathered mu, the    -> xrem     all-gather
+//      reference's per-element double_update chain (fb_chain)
+//   3  remaining of every listed constraint from xrem, erasure, delisting of the shard's variables
+// Every floating-point operation is the one-context solve's, on the same operands in the same order, so the
+// result is bit-identical to it (and to the reference) whatever the number of shards.
+struct FbOwner {
+  int32_t nc;             // owned constraints
+  int32_t nch;            // their chunks (kFbChunk elements)
+  int64_t mu_off;         // position of this shard's first variable in xmu
+  const int32_t* oc;      // [nc] global id of each owned constraint
+  const uint32_t* optr;   // [nc+1] element offsets
+  const int32_t* ovar;    // [onnz] position of the element's variable in xmu
+  const double* ow;       // [onnz] weight
+  const int32_t* och_o;   // [nch] owned-constraint index of each chunk
+  const uint32_t* och_b;  // [nch] first element of each chunk
+  const int32_t* cpos;    // [nC] position of each constraint's remaining in xrem
+  double* fbd;            // [onnz] increments w * mu (owned CSC order)
+  double* xmu;            // gathered mu (caller's buffer)
+  double* xrem;           // gathered remaining (caller's buffer)
+};
+
+// phase 1 tail: this shard's mu into its block of the gathered vector (a delisted variable keeps its
+// last mu: its increment still counts, fair_bottleneck.cpp:111-116)
+__global__ void __launch_bounds__(kBlock) fbo_put_mu(Dev s, FbOwner o) {
+  if (s.ctl[CTL_DONE])
+    return;
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock)
+    o.xmu[o.mu_off + v] = s.vtmp[v];
+}
+
+// phase 2a: increments of the owned listed constraints' elements (every element: the gathered mu of a
+// delisted variable is its last one), one wave per chunk
+__global__ void __launch_bounds__(kBlock) fbo_acc(Dev s, FbOwner o) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wpb = kBlock / kWave;
+  for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < o.nch; q += gridDim.x * wpb) {
+    const int i = o.och_o[q];
+    if (s.ratio[o.oc[i]] != 0.0)
+      continue;
+    const uint32_t b = o.och_b[q], ce = o.optr[i + 1];
+    const uint32_t e = b + kFbChunk < ce ? b + kFbChunk : ce;
+    for (uint32_t j0 = b + lane; j0 < e; j0 += 4 * kWave) {  // 4 gathers in flight per lane
+      int32_t vv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        vv[k] = j0 + k * kWave < e ? o.ovar[j0 + k * kWave] : -1;
+      double dv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        dv[k] = vv[k] >= 0 ? o.ow[j0 + k * kWave] * o.xmu[vv[k]] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (vv[k] >= 0)
+          o.fbd[j0 + k * kWave] = dv[k];
+    }
+  }
+}
+
+// phase 2b: one wave per owned constraint: its new remaining (listed: the chain / FATPIPE update; else
+// unchanged) into xrem
+__global__ void __launch_bounds__(kBlock) fbo_chain(Dev s, FbOwner o, double prec) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  double* d = dl[threadIdx.x / kWave];
+  for (int64_t i = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; i < o.nc;
+       i += int64_t(gridDim.x) * (kBlock / kWave)) {  // wave-uniform
+    const int c = o.oc[i];
+    double rem = s.rem[c];
+    if (s.ratio[c] == 0.0) {
+      const uint32_t cb = o.optr[i], ce = o.optr[i + 1];
+      if (s.cflags[c] & 1) {  // :118-125, the minimum over every element (chunk order irrelevant: fmin)
+        double mn = dinf();
+        for (uint32_t j = cb + lane; j < ce; j += kWave)
+          mn = fmin(mn, o.fbd[j]);
+        double u;
+        rem = fb_fat_update(s, c, rem, wave_min(mn), prec, &u);
+      } else {
+        rem = fb_chain(o.fbd, cb, ce, rem, prec, d, lane);
+      }
+    }
+    if (lane == 0)
+      o.xrem[o.cpos[c]] = rem;
+  }
+}
+
+// phase 3a: every listed constraint takes its owner's remaining; remaining <= 0 erases it (:129-131)
+__global__ void __launch_bounds__(kBlock) fbo_apply(Dev s, FbOwner o) {
+  if (s.ctl[CTL_DONE])
+    return;
+  for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
+    s.erased[c] = 0;
+    if (s.ratio[c] != 0.0)
+      continue;
+    const double rem = o.xrem[o.cpos[c]];
+    s.rem[c] = rem;
+    if (rem <= 0.0) {
+      s.ratio[c] = dinf();
+      s.erased[c] = 1;
     }
   }
 }

@@ -105,10 +105,14 @@ struct lmmhip_ctx {
   int64_t fb_round = 0;
   double fb_prec = 0;
   bool fb_shard = false;
+  FbOwner fbo{};                   // sharded solve: the owned constraints (lmmhip_fb_shard_owner)
+  bool fbo_ready = false;
+  int64_t fbo_nmu = 0;  // length of the gathered mu vector the owned elements index
+  std::vector<void*> fbo_allocs;
   ActDev act{};                        // model-side action state (lmm_step_kernels.hpp)
   std::vector<void*> act_allocs;
   int32_t* xnb_own = nullptr;  // the context's own exchange buffers (unsharded solves)
-  double *xsum_own = nullptr, *xmin_own = nullptr;
+  double* xmin_own = nullptr;
   int64_t fbd_cap = 0;  // elements of d.fbd (allocated by the first one-context FairBottleneck solve)
   // resident System mirror (lmmhip_res_*, lmm_resident_kernels.hpp): outlives uploads, freed with the
   // context.  Mirror arrays keep their contents when they grow; scratch buffers do not.
@@ -140,14 +144,23 @@ struct lmmhip_ctx {
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
 
+static void free_owner(lmmhip_ctx* c) {
+  for (void* p : c->fbo_allocs)
+    (void)hipFree(p);
+  c->fbo_allocs.clear();
+  c->fbo = FbOwner{};
+  c->fbo_ready = false;
+}
+
 static void free_all(lmmhip_ctx* c) {
   for (void* p : c->allocs)
     (void)hipFree(p);
   c->allocs.clear();
+  free_owner(c);
   c->d = Dev{};
   c->uploaded = false;
   c->xnb_own = nullptr;
-  c->xsum_own = c->xmin_own = nullptr;
+  c->xmin_own = nullptr;
   c->fbd_cap = 0;
   c->fb_shard = false;
   c->res_flat = false;
@@ -336,7 +349,6 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   rc |= dalloc(c, &d.pacc, nch);
   rc |= dalloc(c, &d.erased, nC);
   rc |= dalloc(c, &c->xnb_own, nC + 1);
-  rc |= dalloc(c, &c->xsum_own, nC);
   rc |= dalloc(c, &c->xmin_own, nC);
   if (rc) {
     free_all(c);
@@ -347,7 +359,6 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   d.ch_beg = chb;
   d.c_ch = cch;
   d.xnb = c->xnb_own;
-  d.xsum = c->xsum_own;
   d.xmin = c->xmin_own;
   d.var_ptr = vp;
   d.csr_c = csr_c;
@@ -393,6 +404,7 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
     c->uploaded = false;
     c->res_flat = false;
     c->fb_shard = false;
+    free_owner(c);  // owned constraints refer to the previous system
   }
   c->d.nV = int32_t(nV);
   c->d.nC = int32_t(nC);
@@ -1379,19 +1391,33 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
   case 1:
     LAUNCH(3, r, fbk_share, gC, kBlock, d, par);
     LAUNCH(3, r, fb_var_inc, gV, kBlock, d, par, int(r));
-    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(!c->fb_shard));
-    LAUNCH(4, r, fbk_accc, gC, kBlock, d, int(!c->fb_shard));
+    if (c->fb_shard) {  // shards: this shard's mu into the gathered vector, then the caller's all-gather
+      LAUNCH(3, r, fbo_put_mu, gV, kBlock, d, c->fbo);
+      break;
+    }
+    LAUNCH(4, r, fbk_acc, gQ, kBlock, d);
+    LAUNCH(4, r, fbk_accc, gC, kBlock, d);
     break;
   case 2:
-    if (c->fb_shard)  // shards: the summed increments come through the exchange buffer
-      LAUNCH(5, r, fbk_update, gC, kBlock, d, c->fb_prec);
-    else  // one context: element by element in the CSC order, bit-identical to the reference
-      LAUNCH(5, r, fbk_update_seq, grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec);
+    if (c->fb_shard) {  // the owned constraints' chains from the gathered mu -> xrem (all-gathered)
+      LAUNCH(4, r, fbo_acc, grid_for(c->fbo.nch, kBlock / kWave), kBlock, d, c->fbo);
+      LAUNCH(5, r, fbo_chain, grid_for(c->fbo.nc, kBlock / kWave), kBlock, d, c->fbo, c->fb_prec);
+      break;
+    }
+    // one context: element by element in the CSC order, bit-identical to the reference
+    LAUNCH(5, r, fbk_update_seq, grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec);
+    LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
+    c->fb_round++;
+    break;
+  case 3:
+    if (!c->fb_shard)
+      return fail(LMMHIP_E_ARG, "phase 3 exists only in a sharded solve");
+    LAUNCH(5, r, fbo_apply, gC, kBlock, d, c->fbo);
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
     c->fb_round++;
     break;
   default:
-    return fail(LMMHIP_E_ARG, "fair-bottleneck phase must be 0, 1 or 2");
+    return fail(LMMHIP_E_ARG, "fair-bottleneck phase must be 0..2 (one context) or 0..3 (shard)");
   }
   return 0;
 }
@@ -1404,7 +1430,6 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
     c->fbd_cap = c->d.nnz;
   }
   c->d.xnb = c->xnb_own;
-  c->d.xsum = c->xsum_own;
   c->d.xmin = c->xmin_own;
   if (int rc = fb_begin(c, prec))
     return rc;
@@ -1544,11 +1569,91 @@ int lmmhip_ctx_set_engine(lmmhip_ctx* c, int engine) {
   return 0;
 }
 
-int lmmhip_fb_shard_begin(lmmhip_ctx* c, double precision, int32_t* xnb, double* xsum, double* xmin) {
+int lmmhip_fb_shard_owner(lmmhip_ctx* c, int64_t n_own, const int32_t* own_cnst, const int64_t* optr,
+                          const int32_t* ovar, const double* oweight, const int32_t* cpos, int64_t n_mu,
+                          int64_t n_rem) {
   if (!c || !c->uploaded)
     return fail(LMMHIP_E_STATE, "no system uploaded");
-  if (!xnb || !xsum || !xmin)
+  const Dev& d = c->d;
+  if (n_own < 0 || n_own > d.nC || n_mu < 0 || n_rem < 0 || (n_own > 0 && (!own_cnst || !optr)) ||
+      (d.nC > 0 && !cpos))
+    return fail(LMMHIP_E_ARG, "bad owner arguments");
+  const int64_t onnz = n_own > 0 ? optr[n_own] : 0;
+  if (n_own > 0 && optr[0] != 0)
+    return fail(LMMHIP_E_ARG, "optr must start at 0");
+  if (onnz > INT32_MAX || (onnz > 0 && (!ovar || !oweight)))
+    return fail(LMMHIP_E_ARG, "bad owned elements");
+  std::vector<uint32_t> op(size_t(n_own) + 1, 0);
+  std::vector<int32_t> och_o;
+  std::vector<uint32_t> och_b;
+  for (int64_t i = 0; i < n_own; i++) {
+    if (own_cnst[i] < 0 || own_cnst[i] >= d.nC || optr[i + 1] < optr[i])
+      return fail(LMMHIP_E_ARG, "owned constraint id / offsets out of range");
+    op[size_t(i) + 1] = uint32_t(optr[i + 1]);
+    for (int64_t b = optr[i]; b < optr[i + 1]; b += kFbChunk) {
+      och_o.push_back(int32_t(i));
+      och_b.push_back(uint32_t(b));
+    }
+  }
+  for (int64_t j = 0; j < onnz; j++)
+    if (ovar[j] < 0 || ovar[j] >= n_mu || !(oweight[j] > 0))
+      return fail(LMMHIP_E_ARG, "owned element: variable position outside the gathered mu, or weight <= 0");
+  for (int64_t k = 0; k < d.nC; k++)
+    if (cpos[k] < 0 || cpos[k] >= n_rem)
+      return fail(LMMHIP_E_ARG, "cpos outside the gathered remaining");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  free_owner(c);
+  FbOwner& o = c->fbo;
+  auto get = [&](auto** p, int64_t n, const void* src, size_t elt) -> int {
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, size_t(n > 0 ? n : 1) * elt));
+    c->fbo_allocs.push_back(q);
+    if (src && n > 0)
+      HIPCHK(hipMemcpyAsync(q, src, size_t(n) * elt, hipMemcpyHostToDevice, c->stream));
+    *p = static_cast<std::remove_reference_t<decltype(**p)>*>(q);
+    return 0;
+  };
+  int32_t *oc, *ov, *cho, *cp;
+  uint32_t *opp, *chb;
+  double* ow;
+  int rc = 0;
+  rc |= get(&oc, n_own, own_cnst, sizeof(int32_t));
+  rc |= get(&opp, n_own + 1, op.data(), sizeof(uint32_t));
+  rc |= get(&ov, onnz, ovar, sizeof(int32_t));
+  rc |= get(&ow, onnz, oweight, sizeof(double));
+  rc |= get(&cho, int64_t(och_o.size()), och_o.data(), sizeof(int32_t));
+  rc |= get(&chb, int64_t(och_b.size()), och_b.data(), sizeof(uint32_t));
+  rc |= get(&cp, d.nC, cpos, sizeof(int32_t));
+  rc |= get(&o.fbd, onnz, nullptr, sizeof(double));
+  if (rc) {
+    free_owner(c);
+    return rc;
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  o.nc = int32_t(n_own);
+  o.nch = int32_t(och_o.size());
+  o.oc = oc;
+  o.optr = opp;
+  o.ovar = ov;
+  o.ow = ow;
+  o.och_o = cho;
+  o.och_b = chb;
+  o.cpos = cp;
+  c->fbo_ready = true;
+  c->fbo_nmu = n_mu;
+  return 0;
+}
+
+int lmmhip_fb_shard_begin(lmmhip_ctx* c, double precision, int32_t* xnb, double* xmu, int64_t mu_off, double* xrem) {
+  if (!c || !c->uploaded)
+    return fail(LMMHIP_E_STATE, "no system uploaded");
+  if (!c->fbo_ready)
+    return fail(LMMHIP_E_STATE, "lmmhip_fb_shard_owner first");
+  if (!xnb || !xmu || !xrem)
     return fail(LMMHIP_E_ARG, "null exchange buffer");
+  if (mu_off < 0 || mu_off + c->d.nV > c->fbo_nmu)
+    return fail(LMMHIP_E_ARG, "this shard's mu block lies outside the gathered mu");
   HIPCHK(hipSetDevice(c->device));
   c->pool_used = 0;
   c->launch_slot.clear();
@@ -1556,8 +1661,10 @@ int lmmhip_fb_shard_begin(lmmhip_ctx* c, double precision, int32_t* xnb, double*
   c->launch_ms.clear();
   HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
   c->d.xnb = xnb;
-  c->d.xsum = xsum;
-  c->d.xmin = xmin;
+  c->d.xmin = c->xmin_own;
+  c->fbo.xmu = xmu;
+  c->fbo.xrem = xrem;
+  c->fbo.mu_off = mu_off;
   c->fb_shard = true;
   c->last_kind = LMMHIP_KIND_FAIR_BOTTLENECK;
   return fb_begin(c, precision);

@@ -104,6 +104,7 @@ SIGNATURES = {
     "lmm_table_sizes": (I, [P, PI64]),
     "lmm_resident_drain": (I, [P, PI64, PI64, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8), ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD, PD, ct.POINTER(ct.c_int32), PD, ct.POINTER(ct.c_uint8)]),
     "lmm_flat_export": (I, [P, PI64, PI64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, ct.POINTER(ct.c_uint8), PI64]),
+    "lmm_flat_export_order": (I, [P, I64, PI64]),
     "lmm_solve_batch": (I, [ct.POINTER(P), I]),
     "lmm_system_device_ctx": (P, [P]),
     "lmm_check_certificate": (I, [P, D, PD, PI64, PI64]),
@@ -145,7 +146,9 @@ SIGNATURES = {
     "lmmhip_ctx_set_engine": (I, [P, I]),
     "lmmhip_persist_profile": (I, [P, I, PI64, I64, PI64]),
     "lmmhip_persist_profile_blocks": (I, [P, PI64, I64, PI64, PI64]),
-    "lmmhip_fb_shard_begin": (I, [P, D, P, P, P]),
+    "lmmhip_fb_shard_owner": (I, [P, I64, ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD,
+                                  ct.POINTER(ct.c_int32), I64, I64]),
+    "lmmhip_fb_shard_begin": (I, [P, D, P, P, I64, P]),
     "lmmhip_fb_shard_step": (I, [P, I]),
     "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
     "lmmhip_actions_upload": (I, [P, I64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),

@@ -10,11 +10,14 @@ the solve's data path.
   ranks by nnz, every rank solves its share (`solve_components`), and one all-reduce(SUM) of the disjoint
   per-rank value vectors assembles the result.  A random C2 system or a fat tree carrying random flows
   is one giant component: such a system is solved by replicas only.
-* FairBottleneck sharded by variables (config C5: one system, one exchange per phase): each rank holds
-  an nnz-balanced block of the variables and every constraint; a round's two per-constraint reductions
-  (listed counts; sum / min of w*mu, fair_bottleneck.cpp:65-127) are all-reduced between the phases
-  (`fb_solve_sharded`, device side: lmmhip_fb_shard_*).  Every rank takes the same erase decisions
-  from the same reduced values, so the round count is global.
+* FairBottleneck sharded over ranks (config C5: one system, an exchange between the phases of each
+  round, `FbShardPlan` + `fb_solve_sharded`, device side lmmhip_fb_shard_*): each shard holds an
+  nnz-balanced block of the variables (with every constraint) and OWNS an nnz-balanced block of the
+  constraints, i.e. their full element lists in the reference's enabled_element_set_ order.  Per round:
+  all-reduce(SUM) of the per-constraint listed counts (integers, exact), all-gather of the variables'
+  increments mu, the owners' per-element double_update chains (fair_bottleneck.cpp:107-127, operation for
+  operation), all-gather of the owned remaining values.  Every shard takes the same erase decisions from
+  the same values, and the result is bit-identical to the one-context solve and to the reference.
 * The simulation step's only cross-rank dependency is the next event date,
   `Model::next_occuring_event` (Model.cpp:40-129): one all-reduce(MIN) of a scalar (`next_event_date`).
 
@@ -29,7 +32,10 @@ import numpy as np
 
 from simgrid_amd import lmm
 
-Flat = namedtuple("Flat", "var_ptr cnst_idx weight penalty vbound cbound cflags var_ids")
+# csc_order: each constraint's elements as CSR indices, constraint-major (lmm_flat_export_order: the
+# reference's enabled_element_set_ order for FairBottleneck, whose per-element chain depends on it)
+Flat = namedtuple("Flat", "var_ptr cnst_idx weight penalty vbound cbound cflags var_ids csc_order",
+                  defaults=(None,))
 
 
 def dist_env():
@@ -100,7 +106,17 @@ def export_flat(s):
                          p(f.penalty, ct.c_double), p(f.vbound, ct.c_double), p(f.cbound, ct.c_double),
                          p(f.cflags, ct.c_uint8), p(f.var_ids, ct.c_int64)) != 0:
         raise lmm.LmmError(L.lmm_last_error().decode())
-    return f
+    order = np.empty(nnz, np.int64)
+    if L.lmm_flat_export_order(s.h, nnz, p(order, ct.c_int64)) != 0:
+        raise lmm.LmmError(L.lmm_last_error().decode())
+    return f._replace(csc_order=order)
+
+
+def csc_order_of(f):
+    """`f.csc_order`, or ascending CSR order per constraint when the flat carries none."""
+    if f.csc_order is not None:
+        return f.csc_order
+    return np.argsort(f.cnst_idx, kind="stable").astype(np.int64)
 
 
 def components(f):
@@ -130,8 +146,14 @@ def sub_flat(f, var_mask, cnst_mask):
     ci = cmap[f.cnst_idx[eidx]]
     if np.any(ci < 0):
         raise ValueError("selection is not a union of components")
+    order = None
+    if f.csc_order is not None:  # the kept elements in their old relative order (constraint ids stay monotone)
+        new_of = np.full(len(f.cnst_idx), -1, np.int64)
+        new_of[eidx] = np.arange(len(eidx), dtype=np.int64)
+        order = new_of[f.csc_order]
+        order = order[order >= 0]
     out = Flat(ptr, ci.astype(np.int32), f.weight[eidx],
-               f.penalty[vsel], f.vbound[vsel], f.cbound[csel], f.cflags[csel], f.var_ids[vsel])
+               f.penalty[vsel], f.vbound[vsel], f.cbound[csel], f.cflags[csel], f.var_ids[vsel], order)
     return out, vsel
 
 
@@ -151,9 +173,10 @@ def device_solve_flat(f, kind, precision=None, device=None):
             return a.ctypes.data_as(ct.POINTER(t))
 
         nv, nc, nnz = len(f.penalty), len(f.cbound), len(f.cnst_idx)
-        if L.lmmhip_upload(ctx, nv, nc, nnz, p(f.var_ptr, ct.c_int64), p(f.cnst_idx, ct.c_int32),
-                           p(f.weight, ct.c_double), p(f.penalty, ct.c_double), p(f.vbound, ct.c_double),
-                           p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8)) != 0 \
+        order = None if f.csc_order is None else p(np.ascontiguousarray(f.csc_order, np.int64), ct.c_int64)
+        if L.lmmhip_upload2(ctx, nv, nc, nnz, p(f.var_ptr, ct.c_int64), p(f.cnst_idx, ct.c_int32),
+                            p(f.weight, ct.c_double), p(f.penalty, ct.c_double), p(f.vbound, ct.c_double),
+                            p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8), order) != 0 \
                 or L.lmmhip_solve(ctx, kind, prec) != 0:
             raise lmm.LmmError(L.lmmhip_last_error().decode())
         x = np.empty(nv, np.float64)
@@ -244,6 +267,9 @@ class LocalExchange:
     def allreduce_(self, buf, op):
         pass
 
+    def allgather_(self, buf, n):
+        pass
+
 
 class DistExchange:
     """torch.distributed collectives on numpy data (gloo: CPU tensors, nccl/RCCL: device tensors)."""
@@ -286,6 +312,24 @@ class DistExchange:
             t = torch.as_tensor(np.asarray(buf)).to(self.device)
             self.dist.all_reduce(t, op=rop, group=self.group)
             buf[...] = t.cpu().numpy()
+
+    def allgather_(self, buf, n):
+        """In place: rank r's chunk buf[r*n : (r+1)*n] to every rank (buf holds world * n items; a torch
+        tensor on this backend's device or elsewhere, or a numpy array)."""
+        import torch
+
+        is_np = not isinstance(buf, torch.Tensor)
+        t = torch.as_tensor(buf) if is_np else buf
+        work = t if t.device.type == self.device.type else t.to(self.device)
+        mine = work[self.rank * n:(self.rank + 1) * n].clone()
+        if self.device.type == "cuda":
+            self.dist.all_gather_into_tensor(work, mine, group=self.group)
+        else:
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            self.dist.all_gather(parts, mine, group=self.group)
+            work.copy_(torch.cat(parts))
+        if work is not t:
+            t.copy_(work)
 
 
 def next_event_date(local_min, exchange):
@@ -337,46 +381,112 @@ def _fb_stream():
     return _FB_STREAMS[dev]
 
 
-class DeviceFbShard:
-    """One rank's part of a variable-sharded FairBottleneck solve on the current HIP device: its block
-    of variables and every constraint, the three phases of lmmhip_fb_shard_step, and the exchange
-    buffers as torch tensors on the device (so RCCL all-reduces them in place, stream-ordered with the
-    solver's kernels: the context launches on `stream`, by default the process's dedicated shard stream
-    `_fb_stream()`, on which fb_solve_sharded also runs the reductions)."""
+class FbShardPlan:
+    """How a FairBottleneck system (flat `f`, with its csc_order) splits over `parts` shards: shard p holds
+    the variable block [vb[p], vb[p+1]) (nnz-balanced) and owns the constraint block [cb[p], cb[p+1])
+    (balanced by element count: the owners' chains are per-element work).  The gathered vectors are padded
+    per shard: variable v of shard p sits at p * Pv + (v - vb[p]) of the mu vector, constraint k of owner q
+    at q * Pc + (k - cb[q]) of the remaining vector, so each shard's part is one contiguous chunk."""
 
-    def __init__(self, f, precision=None, stream=None):
+    def __init__(self, f, parts):
+        nv, nc = len(f.penalty), len(f.cbound)
+        self.f, self.parts, self.nv, self.nc = f, parts, nv, nc
+        self.vb = balanced_blocks(np.diff(f.var_ptr) + 1, parts)
+        cdeg = np.bincount(f.cnst_idx, minlength=nc).astype(np.int64)
+        self.cb = balanced_blocks(cdeg + 1, parts)
+        self.Pv = max(1, max(hi - lo for lo, hi in zip(self.vb, self.vb[1:])))
+        self.Pc = max(1, max(hi - lo for lo, hi in zip(self.cb, self.cb[1:])))
+        self.mu_len, self.rem_len = parts * self.Pv, parts * self.Pc
+        vpart = np.repeat(np.arange(parts), np.diff(self.vb))
+        self.vpos = (vpart * self.Pv + np.arange(nv) - np.asarray(self.vb)[vpart]).astype(np.int64)
+        cpart = np.repeat(np.arange(parts), np.diff(self.cb))
+        self.cpos = (cpart * self.Pc + np.arange(nc) - np.asarray(self.cb)[cpart]).astype(np.int32)
+        self.order = csc_order_of(f)
+        self.cptr = np.concatenate([[0], np.cumsum(cdeg)]).astype(np.int64)
+        self.rows = np.repeat(np.arange(nv, dtype=np.int64), np.diff(f.var_ptr))
+
+    def variables(self, p):
+        """(flat of shard p's variable rows with every constraint, dense indices of those variables)."""
+        mask = np.zeros(self.nv, bool)
+        mask[self.vb[p]:self.vb[p + 1]] = True
+        return sub_flat(self.f, mask, np.ones(self.nc, bool))
+
+    def owned(self, p):
+        """Shard p's owned constraints: (global ids, element offsets, element variable positions in the
+        gathered mu vector, weights), the elements in the reference's order."""
+        lo, hi = self.cb[p], self.cb[p + 1]
+        e = self.order[self.cptr[lo]:self.cptr[hi]]
+        return (np.arange(lo, hi, dtype=np.int32), (self.cptr[lo:hi + 1] - self.cptr[lo]).astype(np.int64),
+                self.vpos[self.rows[e]].astype(np.int32), np.ascontiguousarray(self.f.weight[e]))
+
+    def mu_off(self, p):
+        return p * self.Pv
+
+
+class FbGather:
+    """The gathered vectors shared by the shards of one process (each writes its own chunk): mu and
+    remaining, torch device tensors (device shards) or numpy arrays."""
+
+    def __init__(self, plan, device=True, stream=None):
+        if device:
+            import torch
+
+            with torch.cuda.stream(stream or _fb_stream()):
+                self.xmu = torch.zeros(plan.mu_len, dtype=torch.float64, device="cuda")
+                self.xrem = torch.zeros(plan.rem_len, dtype=torch.float64, device="cuda")
+        else:
+            self.xmu = np.zeros(plan.mu_len)
+            self.xrem = np.zeros(plan.rem_len)
+        self.Pv, self.Pc = plan.Pv, plan.Pc
+
+
+class DeviceFbShard:
+    """Shard p of a FairBottleneck plan on the current HIP device: its variable block (lmmhip_upload2), its
+    owned constraints (lmmhip_fb_shard_owner) and the four phases of lmmhip_fb_shard_step.  The exchange
+    buffers are torch tensors on the device (RCCL reduces / gathers them in place, stream-ordered with the
+    solver's kernels): the context launches on `stream`, by default the process's dedicated shard stream
+    `_fb_stream()`, on which fb_solve_sharded also runs the exchanges."""
+
+    def __init__(self, plan, p, gather, precision=None, stream=None):
         import torch
 
         L = lmm.lib()
-        self.L, self.n = L, len(f.penalty)
+        f, self.idx = plan.variables(p)
+        self.L, self.n, self.gather = L, len(f.penalty), gather
+        self.mu_off = plan.mu_off(p)
         self.ctx = ct.c_void_p()
         if L.lmmhip_ctx_create(torch.cuda.current_device(), ct.byref(self.ctx)) != 0:
             raise lmm.LmmError(L.lmmhip_last_error().decode())
 
-        def p(a, t):
+        def ptr(a, t):
             return a.ctypes.data_as(ct.POINTER(t))
 
         nc = len(f.cbound)
         # One torch stream shared by every shard of the process: the context's kernels and the torch-side
-        # reductions / all-reduces of the exchange buffers (fb_solve_sharded runs them on it) are then
+        # reductions / gathers of the exchange buffers (fb_solve_sharded runs them on it) are then
         # stream-ordered.  Any torch stream works, torch's default stream (handle 0) included.
         self.stream = _fb_stream() if stream is None else stream
         self._check(L.lmmhip_ctx_set_stream(self.ctx, ct.c_void_p(self.stream.cuda_stream)))
-        self._check(L.lmmhip_upload(self.ctx, self.n, nc, len(f.cnst_idx), p(f.var_ptr, ct.c_int64),
-                                    p(f.cnst_idx, ct.c_int32), p(f.weight, ct.c_double), p(f.penalty, ct.c_double),
-                                    p(f.vbound, ct.c_double), p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8)))
+        order = np.ascontiguousarray(f.csc_order, np.int64)
+        self._check(L.lmmhip_upload2(self.ctx, self.n, nc, len(f.cnst_idx), ptr(f.var_ptr, ct.c_int64),
+                                     ptr(f.cnst_idx, ct.c_int32), ptr(f.weight, ct.c_double), ptr(f.penalty, ct.c_double),
+                                     ptr(f.vbound, ct.c_double), ptr(f.cbound, ct.c_double), ptr(f.cflags, ct.c_uint8),
+                                     ptr(order, ct.c_int64)))
+        oc, optr, ovar, ow = plan.owned(p)
+        cpos = np.ascontiguousarray(plan.cpos, np.int32)
+        self._check(L.lmmhip_fb_shard_owner(self.ctx, len(oc), ptr(oc, ct.c_int32), ptr(optr, ct.c_int64),
+                                            ptr(ovar, ct.c_int32), ptr(ow, ct.c_double), ptr(cpos, ct.c_int32),
+                                            plan.mu_len, plan.rem_len))
         with torch.cuda.stream(self.stream):
             self.xnb = torch.zeros(nc + 1, dtype=torch.int32, device="cuda")
-            self.xsum = torch.zeros(nc, dtype=torch.float64, device="cuda")
-            self.xmin = torch.zeros(nc, dtype=torch.float64, device="cuda")
         self.prec = lmm.get_precision() if precision is None else precision
         self.begin()
 
     def begin(self):
         """Start a solve (fair_bottleneck.cpp:29-50 initialisation); rounds follow with step()."""
         self._check(self.L.lmmhip_fb_shard_begin(self.ctx, self.prec, ct.c_void_p(self.xnb.data_ptr()),
-                                                 ct.c_void_p(self.xsum.data_ptr()),
-                                                 ct.c_void_p(self.xmin.data_ptr())))
+                                                 ct.c_void_p(self.gather.xmu.data_ptr()), self.mu_off,
+                                                 ct.c_void_p(self.gather.xrem.data_ptr())))
 
     def _check(self, rc):
         if rc != 0:
@@ -384,9 +494,6 @@ class DeviceFbShard:
 
     def step(self, phase):
         self._check(self.L.lmmhip_fb_shard_step(self.ctx, phase))
-
-    def buffers(self, phase):
-        return [(self.xnb, "sum")] if phase == 0 else [(self.xsum, "sum"), (self.xmin, "min")]
 
     def poll(self):
         done, rounds = ct.c_int(), ct.c_int64()
@@ -405,61 +512,49 @@ class DeviceFbShard:
 
 
 def shard_variables(f, parts):
-    """Contiguous nnz-balanced variable blocks of flat `f`, every constraint kept in each: the per-rank
-    inputs of a variable-sharded FairBottleneck solve.  Returns [(flat, dense indices)]."""
-    bounds = balanced_blocks(np.diff(f.var_ptr) + 1, parts)
-    out = []
-    nv = len(f.penalty)
-    for lo, hi in zip(bounds, bounds[1:]):
-        mask = np.zeros(nv, bool)
-        mask[lo:hi] = True
-        out.append(sub_flat(f, mask, np.ones(len(f.cbound), bool)))
-    return out
+    """Contiguous nnz-balanced variable blocks of flat `f`, every constraint kept in each (the variable
+    side of an FbShardPlan).  Returns [(flat, dense indices)]."""
+    plan = FbShardPlan(f, parts)
+    return [plan.variables(p) for p in range(parts)]
 
 
-def _reduce_local(shards, phase):
-    """Combine the exchange buffers of the shards living in this process (same order every round)."""
-    if len(shards) < 2:
-        return
-    for i, (buf, op) in enumerate(shards[0].buffers(phase)):
-        acc = buf.clone() if hasattr(buf, "clone") else buf.copy()
-        for sh in shards[1:]:
-            other = sh.buffers(phase)[i][0]
-            acc = acc + other if op == "sum" else (acc.minimum(other) if hasattr(acc, "minimum")
-                                                   else np.minimum(acc, other))
-        for sh in shards:
-            sh.buffers(phase)[i][0][...] = acc
-
-
-def fb_solve_sharded(shards, exchange, n_var_total, n_cnst, poll_every=16):
-    """Drive the three-phase FairBottleneck rounds of `shards` (this process's shards: usually one per
-    rank) with the exchange buffers reduced over the local shards, then over the ranks.  Returns the
-    round count.  All ranks stop in the same round: `done` comes from the reduced counts, and the stop
-    decision itself is all-reduced."""
+def fb_solve_sharded(shards, exchange, gather, poll_every=16):
+    """Drive the four-phase FairBottleneck rounds of `shards`, this process's shards: parts
+    rank * len(shards) .. (rank + 1) * len(shards) - 1 of the plan, sharing `gather` (FbGather).
+    Between the phases: all-reduce(SUM) of the listed counts (over the local shards, then the ranks),
+    all-gather of mu, all-gather of the owned remaining values.  Returns the round count.  All ranks stop
+    in the same round: `done` comes from the reduced counts, and the stop decision is all-reduced."""
     stream = getattr(shards[0], "stream", None) if shards else None
-    if stream is not None:  # device shards: the exchange-buffer reductions run on the shards' stream
+    if stream is not None:  # device shards: the exchanges run on the shards' stream
         import torch
 
         with torch.cuda.stream(stream):
-            return _fb_rounds(shards, exchange, n_var_total, n_cnst, poll_every)
-    return _fb_rounds(shards, exchange, n_var_total, n_cnst, poll_every)
+            return _fb_rounds(shards, exchange, gather, poll_every)
+    return _fb_rounds(shards, exchange, gather, poll_every)
 
 
-def _fb_rounds(shards, exchange, n_var_total, n_cnst, poll_every):
-    max_rounds = 64 * (n_var_total + n_cnst) + 4096
+def _fb_rounds(shards, exchange, gather, poll_every):
+    lp = len(shards)
+    max_rounds = 64 * (gather.xmu.shape[0] + gather.xrem.shape[0]) + 4096
     rounds = 0
     while True:
         for _ in range(poll_every):
-            for phase in (0, 1, 2):
-                for sh in shards:
-                    sh.step(phase)
-                if phase < 2:
-                    _reduce_local(shards, phase)
-                    for buf, op in shards[0].buffers(phase):
-                        exchange.allreduce_(buf, op)
-                    for sh in shards[1:]:
-                        for (b0, _), (b, _) in zip(shards[0].buffers(phase), sh.buffers(phase)):
-                            b[...] = b0
+            for sh in shards:
+                sh.step(0)
+            acc = shards[0].xnb
+            for sh in shards[1:]:
+                acc += sh.xnb
+            exchange.allreduce_(acc, "sum")
+            for sh in shards[1:]:
+                sh.xnb[...] = acc
+            for sh in shards:
+                sh.step(1)
+            exchange.allgather_(gather.xmu, lp * gather.Pv)
+            for sh in shards:
+                sh.step(2)
+            exchange.allgather_(gather.xrem, lp * gather.Pc)
+            for sh in shards:
+                sh.step(3)
             rounds += 1
         states = [sh.poll() for sh in shards]
         done = float(all(d for d, _ in states))

@@ -1,14 +1,19 @@
-"""TEST INFRASTRUCTURE: a numpy model of one rank's part of the variable-sharded FairBottleneck round
-(the phase protocol of lmmhip_fb_shard_*, lmm_fb_kernels.hpp), so that multi.fb_solve_sharded and its
-exchanges can run on gloo without a GPU.  Restates fair_bottleneck.cpp:59-145 phase by phase."""
+"""TEST INFRASTRUCTURE: a numpy model of one shard of the constraint-owner sharded FairBottleneck round
+(the four-phase protocol of lmmhip_fb_shard_*, lmm_fb_kernels.hpp fbo_*), so that multi.fb_solve_sharded
+and its exchanges (all-reduce of counts, all-gathers of mu and of the owned remaining values) run on gloo
+without a GPU.  Restates fair_bottleneck.cpp:59-145 phase by phase; the owned constraints' remaining is the
+reference's own per-element double_update chain (:110-116, surf_interface.hpp:34-44) in a Python loop, so
+the values must equal the oracle's bit for bit."""
 import numpy as np
 
 DBL_MAX = np.finfo(np.float64).max
 
 
 class NumpyFbShard:
-    def __init__(self, f, precision):
+    def __init__(self, plan, p, gather, precision):
+        f, self.idx = plan.variables(p)
         self.prec = precision
+        self.gather = gather
         nv, nc = len(f.penalty), len(f.cbound)
         self.nv, self.nc = nv, nc
         self.rows = np.repeat(np.arange(nv), np.diff(f.var_ptr))
@@ -26,17 +31,17 @@ class NumpyFbShard:
         self.any = nv > 0
         self.done, self.rounds = False, 0
         self.xnb = np.zeros(nc + 1, np.int32)
-        self.xsum = np.zeros(nc)
-        self.xmin = np.zeros(nc)
-
-    def buffers(self, phase):
-        return [(self.xnb, "sum")] if phase == 0 else [(self.xsum, "sum"), (self.xmin, "min")]
+        self.mu_off = plan.mu_off(p)
+        self.cpos = plan.cpos
+        oc, optr, ovar, ow = plan.owned(p)
+        self.owned = [(int(c), ovar[optr[i]:optr[i + 1]], ow[optr[i]:optr[i + 1]]) for i, c in enumerate(oc)]
 
     def step(self, phase):
         if self.done:
             return
         nc, rows, cols = self.nc, self.rows, self.cols
-        if phase == 0:  # :67-74 counts of listed variables
+        g = self.gather
+        if phase == 0:  # :67-74 counts of this shard's listed variables
             live = self.listed[rows] & self.inlist[cols]
             self.xnb[:nc] = np.bincount(cols, weights=live, minlength=nc).astype(np.int32)
             self.xnb[nc] = int(self.any)
@@ -63,23 +68,30 @@ class NumpyFbShard:
             drop = lst & (self.x == self.vbound)
             self.listed[drop] = False
             self.any = bool(np.any(lst & ~drop))
-            d = self.w * self.mu[rows]  # :107-127, stale mu included
-            self.xsum[:] = np.bincount(cols, weights=d, minlength=nc)
-            self.xmin[:] = np.inf
-            np.minimum.at(self.xmin, cols, d)
-            self.xsum[~self.inlist | self.fat] = 0.0
-            self.xmin[~self.inlist | ~self.fat] = np.inf
-        else:  # :110-140
+            g.xmu[self.mu_off:self.mu_off + self.nv] = self.mu  # delisted variables keep their last mu
+        elif phase == 2:  # :107-127 on the owned constraints, from the gathered mu
+            prec = self.prec
+            for c, pos, w in self.owned:
+                r = float(self.rem[c])
+                if self.inlist[c]:
+                    d = w * g.xmu[pos]
+                    if self.fat[c]:  # :118-125
+                        u = float(self.use[c])
+                        if self.zero_w[c]:
+                            u = min(u, 0.0)
+                        u = min(u, float(d.min()))
+                        r -= u
+                        if r < prec:
+                            r = 0.0
+                    else:  # :111-116 one double_update per element, in the reference's order
+                        for x in d.tolist():
+                            r -= x
+                            if r < prec:
+                                r = 0.0
+                g.xrem[self.cpos[c]] = r
+        else:  # :129-140 every listed constraint takes its owner's remaining
             upd = self.inlist.copy()
-            fat = upd & self.fat
-            u = self.use.copy()
-            u[fat & self.zero_w] = np.minimum(u[fat & self.zero_w], 0.0)
-            u[fat] = np.minimum(u[fat], self.xmin[fat])
-            self.use[fat] = u[fat]
-            self.rem[fat] -= u[fat]
-            shared = upd & ~self.fat
-            self.rem[shared] -= self.xsum[shared]
-            self.rem[upd & (self.rem < self.prec)] = 0.0
+            self.rem[upd] = g.xrem[self.cpos[upd]]
             erased = upd & (self.rem <= 0.0)
             self.inlist[erased] = False
             self.listed[rows[erased[cols]]] = False

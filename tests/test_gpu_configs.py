@@ -209,29 +209,21 @@ def test_c5_fixed_point_properties_hold_on_the_oracle_solution():
     assert x_host.tobytes() == y.tobytes()  # bit-identical (fbk_update_seq, reference element order)
 
 
-@pytest.mark.xfail(reason="the variable-sharded FairBottleneck all-reduces per-shard SUMS of w*mu, so a saturating "
-                   "constraint's remaining is rounded differently from the reference's element-by-element chain "
-                   "and near-zero erasures can flip at C5 scale (DESIGN.md §7); the one-context solve is "
-                   "bit-identical (test_c5_1e6_flows_vs_oracle)", strict=False)
-def test_c5_sharded_matches_single_context():
-    """The variable-sharded FairBottleneck (per-round exchange of counts and sums, multi.py) against the
-    single-context solve of the same system, at 1e6 flows."""
+@pytest.mark.parametrize("parts", [2, 3, 8])
+def test_c5_sharded_matches_single_context(parts):
+    """The constraint-owner sharded FairBottleneck (multi.FbShardPlan: counts all-reduced, mu and the owned
+    remaining values all-gathered, each owner chaining its constraints in the reference's element order)
+    against the single-context solve of the same 1e6-flow system: the same bytes."""
+    from tests.test_gpu_multi import device_shard_maker
+    from tests.test_multi import sharded_fb_values
+
     s = L.System(False, L.System.FAIR_BOTTLENECK)
     _, vs = s.gen_platform_flows(L.platform_params(model=L.L07, n_flows=1_000_000, seed=2, **C5_PLATFORM))
     f = M.export_flat(s)
     s.solve()
     want = s.values_of(f.var_ids)
     shards = []
-
-    def make(sub):
-        sh = M.DeviceFbShard(sub)
-        shards.append(sh)
-        return sh
-
-    from tests.test_multi import sharded_fb_values
-
-    x = sharded_fb_values(f, M.LocalExchange(), 3, make)
+    x, _ = sharded_fb_values(f, M.LocalExchange(), parts, device_shard_maker(shards), device=True)
     for sh in shards:
         sh.close()
-    bad, worst = _close(x, want)
-    assert len(bad) == 0, (len(bad), worst)
+    assert x.tobytes() == want.tobytes(), int(np.count_nonzero(x != want))

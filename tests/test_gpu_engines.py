@@ -118,36 +118,33 @@ def test_run_to_run_identical_c3_batch():
 
 def test_fb_sharded_on_torch_default_stream():
     """lmmhip_ctx_set_stream(0) = the legacy null stream: shards on torch's default stream are ordered
-    with the torch-side reductions of fb_solve_sharded (handle 0 used to mean "own stream")."""
+    with the torch-side exchanges of fb_solve_sharded (handle 0 used to mean "own stream")."""
     import torch
 
-    from tests.test_multi import fb_pair, sharded_fb_values
+    from tests.test_gpu_multi import device_shard_maker
+    from tests.test_multi import fb_pair, oracle_dense_values, sharded_fb_values
 
     s, o, ovars = fb_pair()
     f = M.export_flat(s)
     shards = []
-
-    def make(sub):
-        sh = M.DeviceFbShard(sub, stream=torch.cuda.default_stream())
-        shards.append(sh)
-        return sh
-
-    x = sharded_fb_values(f, M.LocalExchange(), 2, make)
+    stream = torch.cuda.default_stream()
+    x, _ = sharded_fb_values(f, M.LocalExchange(), 2, device_shard_maker(shards, stream), device=True,
+                             stream=stream)
     for sh in shards:
         sh.close()
-    o.solve()
-    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
-    assert np.all(np.abs(x - want) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(want)))
+    want = oracle_dense_values(o, ovars, f)
+    assert x.tobytes() == want.tobytes()
 
 
 def test_fb_device_shards_over_gloo():
-    """DistExchange on gloo with device-resident exchange buffers (the CPU-device branch of
-    allreduce_ used np.asarray on a CUDA tensor): a world-1 gloo group in this process."""
+    """DistExchange on gloo with device-resident exchange buffers (the all-reduce and the all-gathers copy
+    through the CPU): a world-1 gloo group in this process."""
     import os
 
     import torch.distributed as dist
 
-    from tests.test_multi import fb_pair, sharded_fb_values
+    from tests.test_gpu_multi import device_shard_maker
+    from tests.test_multi import fb_pair, oracle_dense_values, sharded_fb_values
 
     s, o, ovars = fb_pair(seed=6)
     f = M.export_flat(s)
@@ -155,19 +152,11 @@ def test_fb_device_shards_over_gloo():
     os.environ.setdefault("MASTER_PORT", "29561")
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        ex = M.DistExchange()
         shards = []
-
-        def make(sub):
-            sh = M.DeviceFbShard(sub)
-            shards.append(sh)
-            return sh
-
-        x = sharded_fb_values(f, ex, 2, make)
+        x, _ = sharded_fb_values(f, M.DistExchange(), 2, device_shard_maker(shards), device=True)
         for sh in shards:
             sh.close()
     finally:
         dist.destroy_process_group()
-    o.solve()
-    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
-    assert np.all(np.abs(x - want) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(want)))
+    want = oracle_dense_values(o, ovars, f)
+    assert x.tobytes() == want.tobytes()

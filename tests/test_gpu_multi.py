@@ -26,24 +26,27 @@ def test_device_component_sharded_solve(kind):
         assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want))), world
 
 
+def device_shard_maker(shards, stream=None):
+    def make(plan, p, gather):
+        sh = M.DeviceFbShard(plan, p, gather, stream=stream)
+        shards.append(sh)
+        return sh
+
+    return make
+
+
 @pytest.mark.parametrize("local_parts", [1, 2, 3])
 def test_device_fb_sharded(local_parts):
-    """Variable-sharded FairBottleneck (lmmhip_fb_shard_*): `local_parts` device shards in this process,
-    exchange buffers reduced between the phases, against the oracle's solve."""
-    from tests.test_multi import fb_pair, sharded_fb_values
+    """Constraint-owner sharded FairBottleneck (lmmhip_fb_shard_*): `local_parts` device shards in this
+    process, counts summed and mu / remaining gathered between the phases; the oracle's values, byte for
+    byte."""
+    from tests.test_multi import fb_pair, oracle_dense_values, sharded_fb_values
 
     s, o, ovars = fb_pair()
     f = M.export_flat(s)
     shards = []
-
-    def make(sub):
-        sh = M.DeviceFbShard(sub)
-        shards.append(sh)
-        return sh
-
-    x = sharded_fb_values(f, M.LocalExchange(), local_parts, make)
+    x, _ = sharded_fb_values(f, M.LocalExchange(), local_parts, device_shard_maker(shards), device=True)
     for sh in shards:
         sh.close()
-    o.solve()
-    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
-    assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want)))
+    want = oracle_dense_values(o, ovars, f)
+    assert x.tobytes() == want.tobytes(), int(np.count_nonzero(x != want))

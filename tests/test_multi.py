@@ -153,52 +153,82 @@ def fb_pair(seed=4):
     return s, o, [O.Variable(o, ov[i]) for i in range(400)]
 
 
-def sharded_fb_values(f, exchange, local_parts, shard_cls):
-    parts = M.shard_variables(f, exchange.world * local_parts)
-    mine = parts[exchange.rank * local_parts:(exchange.rank + 1) * local_parts]
-    shards = [shard_cls(sub) for sub, _ in mine]
-    M.fb_solve_sharded(shards, exchange, len(f.penalty), len(f.cbound))
+def sharded_fb_values(f, exchange, local_parts, make_shard, device=False, stream=None):
+    """Values of the constraint-owner sharded FairBottleneck (multi.FbShardPlan over world x local_parts
+    shards, this rank's `local_parts` of them made by make_shard(plan, p, gather)), dense order of `f`."""
+    plan = M.FbShardPlan(f, exchange.world * local_parts)
+    gather = M.FbGather(plan, device=device, stream=stream)
+    parts = range(exchange.rank * local_parts, (exchange.rank + 1) * local_parts)
+    shards = [make_shard(plan, p, gather) for p in parts]
+    M.fb_solve_sharded(shards, exchange, gather)
     x = np.zeros(len(f.penalty))
-    for sh, (_, idx) in zip(shards, mine):
-        x[idx] = sh.values()
-    return exchange.sum(x)
+    for sh in shards:
+        x[sh.idx] = sh.values()
+    return exchange.sum(x), shards
 
 
-def numpy_shard(sub):
+def numpy_shard(plan, p, gather):
     from tests.fb_shard_model import NumpyFbShard
 
-    return NumpyFbShard(sub, L.get_precision())
+    return NumpyFbShard(plan, p, gather, L.get_precision())
+
+
+def oracle_dense_values(o, ovars, f):
+    o.solve()
+    return np.array([ovars[int(i)].get_value() for i in f.var_ids])
 
 
 @pytest.mark.parametrize("local_parts", [1, 3])
 def test_fb_sharded_single_process(local_parts):
     s, o, ovars = fb_pair()
     f = M.export_flat(s)
-    x = sharded_fb_values(f, M.LocalExchange(), local_parts, numpy_shard)
-    o.solve()
-    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
-    assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want)))
+    x, _ = sharded_fb_values(f, M.LocalExchange(), local_parts, numpy_shard)
+    want = oracle_dense_values(o, ovars, f)
+    # the owners chain each constraint's increments in the reference's element order: the same bytes
+    assert x.tobytes() == want.tobytes(), int(np.count_nonzero(x != want))
 
 
-def _fb_worker(rank, world, port, out_dir):
+def test_fb_plan_layout():
+    """Every element of the system is owned exactly once, in its constraint's reference order."""
+    s, _, _ = fb_pair()
+    f = M.export_flat(s)
+    assert sorted(f.csc_order.tolist()) == list(range(len(f.cnst_idx)))
+    assert np.all(np.diff(f.cnst_idx[f.csc_order]) >= 0)
+    plan = M.FbShardPlan(f, 3)
+    rows = np.repeat(np.arange(len(f.penalty)), np.diff(f.var_ptr))
+    got = []
+    for p in range(3):
+        oc, optr, ovar, ow = plan.owned(p)
+        for i, c in enumerate(oc):
+            for pos, w in zip(ovar[optr[i]:optr[i + 1]], ow[optr[i]:optr[i + 1]]):
+                got.append((int(c), int(pos), float(w)))
+    want = [(int(f.cnst_idx[e]), int(plan.vpos[rows[e]]), float(f.weight[e])) for e in f.csc_order]
+    assert got == want
+    assert len(set(plan.vpos.tolist())) == len(f.penalty) and plan.vpos.max() < plan.mu_len
+    assert len(set(plan.cpos.tolist())) == len(f.cbound) and plan.cpos.max() < plan.rem_len
+
+
+def _fb_worker(rank, world, port, out_dir, seed):
     import torch.distributed as dist
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        s, _, _ = fb_pair()
+        s, _, _ = fb_pair(seed)
         f = M.export_flat(s)
-        x = sharded_fb_values(f, M.DistExchange(), 2, numpy_shard)
+        x, _ = sharded_fb_values(f, M.DistExchange(), 2, numpy_shard)
         np.save(os.path.join(out_dir, f"fb{rank}.npy"), x)
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_world2_fb_sharded(tmp_path):
-    mp.spawn(_fb_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    s, o, ovars = fb_pair()
+@pytest.mark.parametrize("seed", [4, 7])
+def test_gloo_world2_fb_sharded(tmp_path, seed):
+    """Two gloo ranks x two numpy shards each: counts all-reduced, mu and owned remaining all-gathered;
+    the values are the oracle's, byte for byte."""
+    mp.spawn(_fb_worker, args=(2, _free_port(), str(tmp_path), seed), nprocs=2, join=True)
+    s, o, ovars = fb_pair(seed)
     f = M.export_flat(s)
-    o.solve()
-    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+    want = oracle_dense_values(o, ovars, f)
     for r in range(2):
         x = np.load(tmp_path / f"fb{r}.npy")
-        assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want)))
+        assert x.tobytes() == want.tobytes(), (r, int(np.count_nonzero(x != want)))
