@@ -26,13 +26,40 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 SLOT_NAMES = {0: "mm_init_cnsts", 1: "mm_init_vars", 2: "mm_vote", 3: "mm_ready", 4: "mm_saturate",
               5: "mm_update", 6: "compaction", 7: "vote_diag"}
-# rocprofv3 kernel names (profiles/*_traffic.json keys) behind each launch slot
-SLOT_KERNELS = {"mm_vote": ("mm_vote_lane", "mm_vote"), "mm_saturate": ("mm_saturate",),
-                "mm_update": ("mm_update",), "mm_ready": ("mm_ready",), "compaction": ("cmp_write",),
-                "mm_init_cnsts": ("mm_init_cnsts",), "mm_init_vars": ("mm_init_vars",)}
-# the newest rocprofv3 PMC summary (scripts/parse_rocprof.py) of the default C2 run
-TRAFFIC_JSON = next((p for p in (os.path.join(ROOT, "profiles", f"r0{k}_traffic.json") for k in (2, 1))
-                     if os.path.exists(p)), None)
+
+
+def traffic_json(workload):
+    """The newest rocprofv3 PMC summary of this workload (scripts/parse_rocprof.py: FETCH_SIZE and
+    WRITE_SIZE passes of `bench.py --workload <w>`, counter bytes per solve over the solve's kernels)."""
+    for k in (9, 8, 7, 6, 5, 4, 3):
+        p = os.path.join(ROOT, "profiles", f"r0{k}_traffic_{workload}.json")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def solve_traffic(workload):
+    """(HBM bytes per solve from the PMC counters with the gfx950 streaming-read correction — 2 x FETCH_SIZE +
+    WRITE_SIZE, MI355X_MICROARCH.md HBM —, the raw FETCH + WRITE, the summary's path) or Nones."""
+    p = traffic_json(workload)
+    if p is None:
+        return None, None, None
+    with open(p) as f:
+        t = json.load(f)
+    return int(t["solve_counter_bytes_fetch_x2"]), int(t["solve_counter_bytes_raw"]), os.path.relpath(p, ROOT)
+
+
+def roofline_obj(alg_bytes, ms, workload, note, gpus=1):
+    """Solve-level roofline: the algorithmic bytes of one solve (all `gpus` ranks' parts)
+    over the solve's time, against `gpus` x the HBM peak.  The PMC traffic summaries are single-GPU runs:
+    reported at N = 1 only."""
+    ach = alg_bytes / (ms * 1e-3) / 1e9
+    peak = HBM_PEAK_GBS * gpus
+    traffic, raw, src = solve_traffic(workload) if gpus == 1 else (None, None, None)
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+            "frac": round(ach / peak, 5), "traffic": traffic, "traffic_raw": raw, "traffic_source": src,
+            "traffic_unit": "bytes per solve (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE over the solve kernels)",
+            "alg_bytes": int(alg_bytes), "kernel": "whole solve", "alg_model": note}
 
 
 def log(*a):
@@ -87,6 +114,10 @@ def kernel_bytes(slot, nV, nC, av, ae, fv, fe, rv, re_):
 
 
 def main():
+    if os.environ.get("LMM_SEGV_TRACE") == "1":  # diagnostics: native backtrace of a crash (scripts/segv_trace.c)
+        import ctypes
+
+        ctypes.CDLL(os.path.join(ROOT, "scripts", "libsegv_trace.so"))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -96,7 +127,6 @@ def main():
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-div", type=int, default=10, help="CPU baseline sample = 1/div of the workload")
-    ap.add_argument("--traffic-json", default=TRAFFIC_JSON, help="per-kernel HBM bytes from a rocprofv3 --pmc pass")
     ap.add_argument("--profile-json", default=None, help="write the per-launch profile here")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2 = the BASELINE metric's config (default); c3/c4/c5 = the other SURVEY.md §8(d) configs")
@@ -189,22 +219,14 @@ def main():
                                               avg_us=float(1000 * ms[sel].mean()), alg_bytes=int(byts))
     dom = max(per_kernel, key=lambda n: per_kernel[n]["total_ms"])
     d = per_kernel[dom]
-    achieved = d["alg_bytes"] / (d["total_ms"] * 1e-3) / 1e9
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        for kname in SLOT_KERNELS.get(dom, ()):
-            if kname in tj.get("kernels", {}):
-                traffic = tj["kernels"][kname]["hbm_bytes_per_launch"]
-                break
+    kach = d["alg_bytes"] / (d["total_ms"] * 1e-3) / 1e9
     solve_alg = 56 * nnz + 24 * nV + 32 * nC
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
-                "kernel_avg_us": round(d["avg_us"], 2), "kernel_launches": d["launches"],
-                "alg_bytes_per_launch": int(d["alg_bytes"] / max(1, d["launches"])),
-                "solve_alg_bytes": int(solve_alg),
-                "solve_frac": round(solve_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    roofline = roofline_obj(solve_alg * world, ms_per_step, "c2" if args.variant == "plain" else "c2_stress",
+                            "SURVEY.md §8(d) lmm_solve: 56 nnz + 24 V + 32 C bytes per solve (x ranks)", gpus=world)
+    # secondary: the dominant kernel's own per-launch byte model (kernel_bytes) over its HIP-event time
+    roofline["dominant_kernel"] = {"name": dom, "avg_us": round(d["avg_us"], 2), "launches": d["launches"],
+                                   "alg_bytes_per_launch": int(d["alg_bytes"] / max(1, d["launches"])),
+                                   "achieved_gbs": round(kach, 1), "kernel_frac": round(kach / HBM_PEAK_GBS, 4)}
     if args.profile_json and rank == 0:
         extra = {}
         if os.environ.get("LMMHIP_VOTE_DIAG"):
@@ -255,11 +277,13 @@ def main():
             cpu_rounds = o.last_rounds
             del o
         m, sd = mean_sd(times)
+        parity = c2_sample_parity(args, div, gen_kw)
         cpu = {"value": round((args.vars // div) / m, 1), "unit": "vars/s", "cores": 1, "kind": "port",
                "sample": f"same generator at 1/{div} scale ({args.cnst // div} cnst x {args.vars // div} vars x {args.k}),"
                          f" solve() timed with steady_clock, {len(times)} reps: {m:.3f} +- {sd:.3f} s,"
                          f" {cpu_rounds} sequential rounds",
-               "reps": len(times), "solve_s_mean": round(m, 4), "solve_s_sd": round(sd, 4), **host_info()}
+               "reps": len(times), "solve_s_mean": round(m, 4), "solve_s_sd": round(sd, 4),
+               "gpu_vs_oracle": parity, **host_info()}
 
     if rank == 0:
         out = {
@@ -280,6 +304,33 @@ def main():
     del s  # free the device context while the HIP runtime is up (not in interpreter teardown)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def c2_sample_parity(args, div, gen_kw):
+    """The CPU-baseline sample (the C2 generator at 1/div scale) solved on the GPU through System::solve()
+    and by the oracle: the largest value difference and the variables outside the parity tolerance
+    (tests/lmm_cases.py: max(1e-9, 1e-6 |x_oracle|)) — parity at the size the baseline is timed on."""
+    import numpy as np
+
+    from oracle import pyoracle as O
+    from simgrid_amd import lmm
+
+    nc, nv = args.cnst // div, args.vars // div
+    o = O.System(False)
+    ov = o.gen_synthetic(nc, nv, args.k, seed=1, **gen_kw)
+    o.solve()
+    y = o.values_of(ov, nv)
+    del o, ov
+    p = lmm.System(False)
+    pv = p.gen_synthetic(nc, nv, args.k, seed=1, **gen_kw)
+    p.solve()
+    x = p.values_of(pv)
+    del p
+    diff = np.abs(x - y)
+    tol = np.maximum(1e-9, 1e-6 * np.abs(y))
+    return {"sample": f"{nc} x {nv} x {args.k}", "max_abs_diff_vs_oracle": float(diff.max()),
+            "max_rel_diff_vs_oracle": float((diff / np.maximum(np.abs(y), 1e-300)).max()),
+            "vars_outside_tolerance": int(np.count_nonzero(diff > tol)), "tolerance": "max(1e-9, 1e-6 |x|)"}
 
 
 C4_PLATFORM = dict(topology=0, topo_parameters="3;16,16,16;1,16,16;1,1,1", loopback_bw=1e8)  # FAT_TREE
@@ -480,19 +531,28 @@ def run_config(args):
     barrier()
     elapsed = time.perf_counter() - t0
     tot = np.array([nV, nnz, nC], dtype=np.float64)  # summed over ranks below
+    if args.workload == "c5":  # the reference's per-round sweeps, counted on the device over the last solve
+        w = shards[0].fb_work() if shards is not None else s.fb_work()
+        # elements and variables are split over the ranks; every rank lists every constraint: count rank 0's
+        work = np.array([w[0], w[1], w[2] if rank == 0 else 0], dtype=np.float64)
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
         tot = ex.sum(tot)
+        if args.workload == "c5":
+            work = ex.sum(work)
     ms_per_step = 1000.0 * elapsed / args.steps
     # algorithmic bytes of one solve: maxmin 56 B/element + 24 B/variable + 32 B/constraint;
-    # fair bottleneck 36 B/element + 32 B/variable + 32 B/constraint per round
-    if args.workload == "c5":  # every rank sweeps all constraints: tot[2] = world x nC
-        alg = rounds * (36 * tot[1] + 32 * tot[0] + 32 * tot[2])
+    # fair bottleneck sum over the rounds of 36 B/element + 32 B/variable + 32 B/constraint of the listed ones
+    if args.workload == "c5":
+        alg = 36 * work[0] + 32 * work[1] + 32 * work[2]
+        note = ("SURVEY.md §8(d) bottleneck_solve: sum over rounds of 36 nnz_r + 32 V_r + 32 C_r bytes, nnz_r / V_r /"
+                " C_r = elements of the listed constraints / listed variables / listed constraints (lmmhip_fb_work)")
+        desc["fb_work"] = dict(elements=int(work[0]), variables=int(work[1]), constraints=int(work[2]))
     else:
         alg = 56 * tot[1] + 24 * tot[0] + 32 * tot[2]
-    ach = alg / (ms_per_step * 1e-3) / 1e9
+        note = "SURVEY.md §8(d) lmm_solve: 56 nnz + 24 V + 32 C bytes per solve"
     if args.profile_json and rank == 0 and shards is None and batch is None:  # per-launch HIP events of one extra solve
         s.set_profiling(True)
         s.device_solve()
@@ -516,8 +576,7 @@ def run_config(args):
             "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (generators of simgrid_amd/csrc/lmm_generators.hpp / lmm_platforms.hpp)",
             "config": desc,
-            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "whole solve"},
+            "roofline": roofline_obj(alg, ms_per_step, args.workload, note, gpus=world),
             "cpu_baseline": cpu}), flush=True)
     if shards is not None:
         for sh in shards:

@@ -144,6 +144,13 @@ int lmmhip_get_saturated(lmmhip_ctx* ctx, uint8_t* saturated_out);
  * caller's id space: dense CSR indices after lmmhip_upload, host variable slots after
  * lmmhip_res_flatten (ascending).  *n = count; ids == NULL = size query; cap must be >= *n. */
 int lmmhip_get_touched_vars(lmmhip_ctx* ctx, int32_t* ids, int64_t cap, int64_t* n);
+/* Connected components of the uploaded (or resident-flattened) system's variable-constraint graph — the
+ * closure System::update_modified_set walks from one constraint (maxmin.cpp:898-922), for every component at
+ * once (components spread over GPUs).  Lock-free union-find on the device; component ids
+ * are compact, 0..*ncomp-1, in the order of each component's smallest node (variables first, then
+ * constraints, dense order): var_label[n_var], cnst_label[n_cnst] (a constraint without an element is a
+ * component of its own).  Deterministic whatever the scheduling. */
+int lmmhip_components(lmmhip_ctx* ctx, int32_t* var_label, int32_t* cnst_label, int64_t* ncomp);
 /* Device pointer of the values (for device-resident consumers, e.g. model update kernels). */
 int lmmhip_values_device_ptr(lmmhip_ctx* ctx, const double** dptr);
 
@@ -216,6 +223,11 @@ int lmmhip_fb_shard_begin(lmmhip_ctx* ctx, double precision, int32_t* xnb, doubl
                           double* xrem);
 int lmmhip_fb_shard_step(lmmhip_ctx* ctx, int phase);
 int lmmhip_fb_shard_poll(lmmhip_ctx* ctx, int* done, int64_t* rounds); /* synchronises the stream */
+/* Work of the last FairBottleneck solve (one context, or this shard's part), summed over its rounds — the
+ * per-round sweeps of fair_bottleneck.cpp:59-144 that SURVEY.md §8(d) prices at 36 B per element + 32 B per
+ * variable + 32 B per constraint: out3 = {elements of the listed constraints (this context's CSC), listed
+ * variables, listed constraints}. */
+int lmmhip_fb_work(lmmhip_ctx* ctx, int64_t* out3);
 
 /* Model-side step glue on the device, over the values of the context's last solve:
  * the actions' remains / max duration / latency stay in HBM between steps.

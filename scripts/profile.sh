@@ -1,40 +1,49 @@
 #!/bin/bash
 # rocprofv3 evidence for bench.py (run on the GPU box via gpurun).  Counter passes are separate from
-# the kernel-trace pass, as MI355X_MICROARCH.md prescribes (FETCH_SIZE and WRITE_SIZE do not fit in
-# one pass).  Output: gpurun_out/rp_*/ (CSV).  usage: scripts/profile.sh [bench args...]
+# the kernel-trace passes, one counter per pass, as MI355X_MICROARCH.md prescribes (FETCH_SIZE and
+# WRITE_SIZE do not fit in one pass).  Output: gpurun_out/rp_*/ (CSV), summarised into profiles/ by
+# scripts/parse_rocprof.py.  usage: PARTS="trace c3 c4 c5 pmc cal" scripts/profile.sh
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --dropin-steps 0 $*"
-PARTS=${PARTS:-"trace c3 c5 pmc c4"}  # subset to run (e.g. PARTS="c4 pmc")
+PARTS=${PARTS:-"trace c3 c4 c5 pmc cal"}
+PMC_WORKLOADS=${PMC_WORKLOADS:-"c2 c3 c4 c5"}
 has() { case " $PARTS " in *" $1 "*) return 0;; *) return 1;; esac; }
-fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-if has trace; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace -o run \
-    -- python3 $BENCH > gpurun_out/rp_trace.log 2>&1
-  rc=$?; echo "trace rc=$rc" >> gpurun_out/rp_trace.log; if fatal $rc; then exit $rc; fi
+# every step: its own time limit, its rc logged, and the script ends at the first failure of any kind
+run() {  # run <log> <limit s> <command...>
+  local log=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "rc=$rc" >> "$log"
+  if [ $rc -ne 0 ]; then echo "step failed (rc=$rc): $log"; tail -5 "$log"; exit $rc; fi
+}
+wl_args() {  # bench arguments of one short run of a workload
+  case $1 in
+    c2) echo "--steps $2 --warmup 1 --no-cpu-baseline --dropin-steps 0";;
+    *) echo "--workload $1 --steps $2 --warmup 1 --no-cpu-baseline";;
+  esac
+}
+if has trace; then  # C2 (the BASELINE metric's config)
+  run gpurun_out/rp_trace.log 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace -o run \
+    -- python3 bench.py $(wl_args c2 3)
 fi
-for w in c3 c5; do  # the batch kernel (C3: one dispatch per solve) and the FairBottleneck kernels (C5)
+for w in c3 c4 c5; do
   has $w || continue
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_$w -o run \
-    -- python3 bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/rp_trace_$w.log 2>&1
-  rc=$?; echo "trace $w rc=$rc" >> gpurun_out/rp_trace_$w.log; if fatal $rc; then exit $rc; fi
+  run gpurun_out/rp_trace_$w.log 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_$w \
+    -o run -- python3 bench.py $(wl_args $w 10)
 done
-for ctr in FETCH_SIZE WRITE_SIZE; do
-  has pmc || continue
-  timeout -k 10 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_$ctr -o run \
-    -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --dropin-steps 0 "$@" > gpurun_out/rp_$ctr.log 2>&1
-  rc=$?; echo "$ctr rc=$rc" >> gpurun_out/rp_$ctr.log; if fatal $rc; then exit $rc; fi
-  # calibration on known byte counts (scripts/ubench_gather.hip: 320 MB int32 stream, gathers)
-  timeout -k 10 200 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_cal_$ctr -o run \
-    -- ./scripts/ubench_gather > gpurun_out/rp_cal_$ctr.log 2>&1
-  rc=$?; echo "cal $ctr rc=$rc" >> gpurun_out/rp_cal_$ctr.log; if fatal $rc; then exit $rc; fi
-done
-# the persistent engine (C4) last: rocprofv3 has crashed in its exit handler after writing this trace
-# (SIGSEGV in the tool's teardown, outputs complete), and nothing may run after a crash in one call
-if has c4; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_c4 -o run \
-    -- python3 bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/rp_trace_c4.log 2>&1
-  rc=$?; echo "trace c4 rc=$rc" >> gpurun_out/rp_trace_c4.log
+if has pmc; then
+  for w in $PMC_WORKLOADS; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      run gpurun_out/rp_${ctr}_$w.log 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_${ctr}_$w -o run \
+        -- python3 bench.py $(wl_args $w 2)
+    done
+  done
+fi
+if has cal; then  # calibration on known byte counts (scripts/ubench_gather.hip: 320 MB int32 stream, gathers)
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    run gpurun_out/rp_cal_$ctr.log 200 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_cal_$ctr -o run \
+      -- ./scripts/ubench_gather
+  done
 fi
 exit 0

@@ -256,6 +256,15 @@ __global__ void __launch_bounds__(kBB, 8) mm_batch_lds(Dev s, const int64_t* __r
       }
       if (!__syncthreads_or(alive))  // light table empty (maxmin.cpp:680)
         break;
+      if (round > nv + 2) {  // every round fixes >= 1 variable: the invariant broke
+        rounds_max = -1;
+        break;
+      }
+    }
+    if (rounds_max < 0) {  // guard tripped: report it (mm_batch_rounds -> CTL_ERR = 2) and stop this block
+      if (threadIdx.x == 0)
+        block_rounds[blockIdx.x] = -1;
+      return;
     }
     rounds_max = round + 1 > rounds_max ? round + 1 : rounds_max;
     for (int v = threadIdx.x; v < nv; v += kBB)
@@ -279,22 +288,30 @@ __global__ void __launch_bounds__(kBlock) mm_batch_check(Dev s, const int64_t* v
 }
 
 __global__ void __launch_bounds__(kBlock) mm_batch_rounds(const int32_t* block_rounds, int n, int32_t* ctl) {
-  int m = 0;
-  for (int i = threadIdx.x; i < n; i += kBlock)
+  int m = 0, err = 0;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
     m = block_rounds[i] > m ? block_rounds[i] : m;
+    err |= block_rounds[i] < 0;
+  }
   for (int o = 32; o > 0; o >>= 1) {
     const int t = __shfl_xor(m, o, kWave);
     m = t > m ? t : m;
+    err |= __shfl_xor(err, o, kWave);
   }
-  __shared__ int wm[kBlock / kWave];
-  if ((threadIdx.x & (kWave - 1)) == 0)
+  __shared__ int wm[kBlock / kWave], we[kBlock / kWave];
+  if ((threadIdx.x & (kWave - 1)) == 0) {
     wm[threadIdx.x / kWave] = m;
+    we[threadIdx.x / kWave] = err;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < kBlock / kWave; i++)
+    for (int i = 1; i < kBlock / kWave; i++) {
       m = wm[i] > m ? wm[i] : m;
+      err |= we[i];
+    }
     ctl[CTL_ROUNDS] = m;
     ctl[CTL_LASTR] = m - 1;
+    ctl[CTL_ERR] = err ? 2 : 0;  // 2 = round guard (a block's system stopped after nv + 2 rounds)
   }
 }
 

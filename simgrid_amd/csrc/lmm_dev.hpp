@@ -35,6 +35,9 @@ enum : int {
   CTL_BUF = 21,    // alive-row buffer of the next vote (0 = the CSR, 1 / 2 = compaction targets)
   CTL_CB = 22,     // alive-constraint list in use (0 / 1)
   CTL_CMPGO = 23,  // the last compaction count found the rewrite worth it (cmp_scan -> cmp_write, mm_flip)
+  // fair bottleneck: the reference's work summed over the rounds, three uint64 words:
+  // elements of the listed constraints, listed variables, listed constraints (words 24..29)
+  CTL_FBW = 24,
   CTL_WORDS = 32
 };
 

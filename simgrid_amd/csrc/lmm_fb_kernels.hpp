@@ -111,6 +111,15 @@ __global__ void __launch_bounds__(kBlock) fbk_nb(Dev s, int par) {
     s.xnb[s.nC] = s.ctl[CTL_ANY0 + par];
 }
 
+// Per-wave sum of a work counter into ctl word pair CTL_FBW + 2 k (one atomic per wave).
+__device__ __forceinline__ void fb_work_add(const Dev& s, int k, unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v += __shfl_xor(v, o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0 && v)
+    atomicAdd(reinterpret_cast<unsigned long long*>(s.ctl + CTL_FBW) + k, v);
+}
+
 // :65-87 — usage = remaining / nb (FATPIPE: nb -> 1); nb == 0 erases the constraint.  xnb holds the
 // counts of every shard; xnb[nC] == 0 means no variable is listed anywhere: the solve is over (:145).
 __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
@@ -125,9 +134,12 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
     s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
     s.ctl[CTL_ROUNDS] += 1;
   }
+  unsigned long long ne = 0, nc = 0;  // this round's listed constraints and their elements (measurement)
   for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
     if (s.ratio[c] != 0.0)
       continue;
+    ne += s.cnst_ptr[c + 1] - s.cnst_ptr[c];
+    nc += 1;
     int nb = s.xnb[c];
     if (nb > 0 && (s.cflags[c] & 1))
       nb = 1;
@@ -139,6 +151,8 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
       s.use[c] = s.rem[c] / nb;
     }
   }
+  fb_work_add(s, 0, ne);
+  fb_work_add(s, 2, nc);
 }
 
 // :89-105 — per listed variable: mu = min(usage/w, bound - value); value += mu; exact
@@ -176,6 +190,7 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
   uint8_t* wrl = rl + (threadIdx.x - lane);
   const unsigned long long kMaxBits = (unsigned long long)__double_as_longlong(DBL_MAX);
   int any = 0;
+  unsigned long long nvl = 0;  // listed variables seen by this lane (measurement)
   for (int64_t base = int64_t(blockIdx.x) * kBlock + (threadIdx.x - lane); base < s.nV;
        base += int64_t(gridDim.x) * kBlock) {  // wave-uniform
     const int64_t v = base + lane;
@@ -183,6 +198,7 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
     const bool listed = in && s.vst[v];
     const uint32_t b = in ? s.var_ptr[v] : 0u, e = in ? s.var_ptr[v + 1] : 0u;
     const int nlisted = __popcll(__ballot(listed));
+    nvl += listed;
     if (nlisted == 0)
       continue;
     if (nlisted < kWave / 4) {  // few listed rows (late rounds): each listed lane reads its own row
@@ -247,6 +263,7 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
   }
   if (__any(any) && (threadIdx.x & (kWave - 1)) == 0)
     s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
+  fb_work_add(s, 1, nvl);
 }
 
 // :107-127 — per chunk of a listed constraint.  FATPIPE: min of w*mu over ALL its elements (the stale mu of

@@ -22,6 +22,7 @@
 #include "lmm_persist_kernels.hpp"
 #include "lmm_batch_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
+#include "lmm_cc_kernels.hpp"
 #include "lmm_scan.hpp"
 
 using namespace lmmdev;
@@ -63,7 +64,7 @@ struct FlatBufs {
 struct lmmhip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;      // the stream every launch and copy goes to
-  hipStream_t own_stream = nullptr;  // the context's own stream (lmmhip_ctx_set_stream(nullptr))
+  hipStream_t own_stream = nullptr;  // the context's own stream (back to it: lmmhip_ctx_use_own_stream)
   Dev d{};
   std::vector<void*> allocs;  // owned device allocations
   int32_t* h_ctl = nullptr;   // pinned mirror of the control words (+ 2 slots: pipelined polls of solve_maxmin)
@@ -140,6 +141,7 @@ struct lmmhip_ctx {
   int64_t res_refreshes = 0;
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
+  Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
@@ -239,7 +241,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch})
@@ -1264,9 +1266,13 @@ static int engine_of(const lmmhip_ctx* c) {
   // the profiling mode times every phase launch: it runs the multi-launch engine
   if (c->profiling)
     return LMMHIP_ENGINE_ROUNDS;
+  // LMMHIP_ENGINE=rounds|persistent overrides the context's engine; "auto" (or any other value, which is
+  // ignored) leaves the context's choice in place
   const char* e = std::getenv("LMMHIP_ENGINE");
-  if (e && *e)
-    return std::strcmp(e, "rounds") == 0 ? LMMHIP_ENGINE_ROUNDS : LMMHIP_ENGINE_PERSISTENT;
+  if (e && std::strcmp(e, "rounds") == 0)
+    return LMMHIP_ENGINE_ROUNDS;
+  if (e && std::strcmp(e, "persistent") == 0)
+    return LMMHIP_ENGINE_PERSISTENT;
   if (c->engine != LMMHIP_ENGINE_AUTO)
     return c->engine;
   // AUTO (measured): one launch per solve where the host round-trips and launches of the
@@ -1276,9 +1282,9 @@ static int engine_of(const lmmhip_ctx* c) {
   return int64_t(c->d.nV) <= kAutoPersistVars ? LMMHIP_ENGINE_PERSISTENT : LMMHIP_ENGINE_ROUNDS;
 }
 
-// One cooperative launch per solve (lmm_persist_kernels.hpp): one 1024-thread workgroup per CU, all
-// resident (hipLaunchCooperativeKernel checks the grid against the occupancy query); every barrier
-// wait is bounded, so a fault in the protocol ends the launch with CTL_ERR instead of hanging the GPU.
+// One persistent launch per solve (lmm_persist_kernels.hpp): one 1024-thread workgroup per CU, all
+// resident (the occupancy query admits exactly one per CU); every barrier wait is bounded, so a fault in
+// the protocol ends the launch with CTL_ERR instead of hanging the GPU.
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   Dev d = c->d;
   d.vstat = nullptr;
@@ -1314,7 +1320,15 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   }
   int sysf = env_int("LMMHIP_PERSIST_SYSFENCE", 0);
   void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf};
-  HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
+  // A plain launch on the context's stream: the occupancy query above guarantees one workgroup per CU, so the
+  // n_cu workgroups are co-resident once the stream's earlier work has drained, and every barrier wait is
+  // bounded (CTL_ERR) should they not be.  hipLaunchCooperativeKernel (LMMHIP_PERSIST_COOP=1) runs the same
+  // kernel through the runtime's device-wide cooperative queue, whose teardown at process exit crashed inside
+  // the HSA runtime under rocprofv3 (SIGSEGV in libamdhip64's exit handler).
+  if (env_int("LMMHIP_PERSIST_COOP", 0))
+    HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
+  else
+    HIPCHK(hipLaunchKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
   c->stats.kernel_launches[2] += 1;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->ev1_done = true;
@@ -1363,7 +1377,11 @@ static int solve_maxmin_batch(lmmhip_ctx* c, double prec) {
   c->ev1_done = true;
   hipLaunchKernelGGL(mm_batch_rounds, dim3(1), dim3(kBlock), 0, c->stream, c->bt_rounds, int(grid), d.ctl);
   HIPCHK(hipGetLastError());
-  return poll_ctl(c);
+  if (int rc = poll_ctl(c))
+    return rc;
+  if (c->h_ctl[CTL_ERR] == 2)
+    return fail(LMMHIP_E_NOCONVERGE, "batch maxmin round guard tripped");
+  return 0;
 }
 
 static int fb_begin(lmmhip_ctx* c, double prec) {
@@ -1675,6 +1693,22 @@ int lmmhip_fb_shard_step(lmmhip_ctx* c, int phase) {
     return fail(LMMHIP_E_STATE, "lmmhip_fb_shard_begin first");
   HIPCHK(hipSetDevice(c->device));
   return fb_phase(c, phase);
+}
+
+int lmmhip_fb_work(lmmhip_ctx* c, int64_t* out3) {
+  if (!c || !out3)
+    return fail(LMMHIP_E_ARG, "null argument");
+  if (c->last_kind != LMMHIP_KIND_FAIR_BOTTLENECK)
+    return fail(LMMHIP_E_STATE, "the last solve was not a FairBottleneck solve");
+  HIPCHK(hipSetDevice(c->device));
+  if (int rc = poll_ctl(c))
+    return rc;
+  for (int k = 0; k < 3; k++) {
+    uint64_t v;
+    std::memcpy(&v, c->h_ctl + CTL_FBW + 2 * k, sizeof v);
+    out3[k] = int64_t(v);
+  }
+  return 0;
 }
 
 int lmmhip_fb_shard_poll(lmmhip_ctx* c, int* done, int64_t* rounds) {
@@ -2086,6 +2120,52 @@ int lmmhip_get_saturated(lmmhip_ctx* c, uint8_t* sat) {
     HIPCHK(hipMemcpyAsync(sat, o, size_t(c->d.nC), hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int lmmhip_components(lmmhip_ctx* c, int32_t* var_label, int32_t* cnst_label, int64_t* ncomp) {
+  if (!c || !c->uploaded)
+    return fail(LMMHIP_E_STATE, "no system uploaded");
+  if (!ncomp || (c->d.nV && !var_label) || (c->d.nC && !cnst_label))
+    return fail(LMMHIP_E_ARG, "null output");
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t nv = c->d.nV, n = int64_t(c->d.nV) + int64_t(c->d.nC);
+  *ncomp = 0;
+  if (n == 0)
+    return 0;
+  int32_t *par = nullptr, *out = nullptr;
+  int64_t *flag = nullptr, *rank = nullptr;
+  if (int rc = scratch(c, c->cc_par, n, &par))
+    return rc;
+  if (int rc = scratch(c, c->cc_flag, n, &flag))
+    return rc;
+  if (int rc = scratch(c, c->cc_rank, n, &rank))
+    return rc;
+  if (int rc = scratch(c, c->cc_out, n, &out))
+    return rc;
+  hipLaunchKernelGGL(cc_init, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, c->stream, par, n);
+  HIPCHK(hipGetLastError());
+  if (nv > 0) {
+    hipLaunchKernelGGL(cc_hook, dim3(grid_for(nv, kBlock)), dim3(kBlock), 0, c->stream, c->d, par);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(cc_root, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, c->stream, par, n, flag);
+  HIPCHK(hipGetLastError());
+  if (int rc = dev_scan(c, flag, rank, n))
+    return rc;
+  hipLaunchKernelGGL(cc_label, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, c->stream, par, rank, nv, n, out,
+                     out + nv);
+  HIPCHK(hipGetLastError());
+  int rc = 0;
+  const int64_t last = read_i64(c, rank + n - 1, &rc) + read_i64(c, flag + n - 1, &rc);
+  if (rc)
+    return rc;
+  if (nv)
+    HIPCHK(hipMemcpyAsync(var_label, out, size_t(nv) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  if (n > nv)
+    HIPCHK(hipMemcpyAsync(cnst_label, out + nv, size_t(n - nv) * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *ncomp = last;
   return 0;
 }
 

@@ -48,7 +48,8 @@ int CnstRec::slack() const {
 // flatten, which hands the device each constraint's elements in the reference's list order
 // (flatten_fair): the bit-identical element-by-element remaining update needs it.
 System::System(bool selective_update, SolverKind kind)
-    : selective_(selective_update), kind_(kind), resident_(resident_default && kind == SolverKind::MAXMIN) {}
+    : selective_(selective_update), kind_(kind), resident_(resident_default && kind == SolverKind::MAXMIN),
+      engine_(solver_engine) {}
 
 System::~System() {
   if (ctx_)
@@ -60,7 +61,7 @@ lmmhip_ctx* System::ctx() {
     int rc = lmmhip_ctx_create(-1, &ctx_);
     if (rc)
       fatal(std::string("cannot create HIP context: ") + lmmhip_last_error());
-    if ((rc = lmmhip_ctx_set_engine(ctx_, solver_engine)))
+    if ((rc = lmmhip_ctx_set_engine(ctx_, engine_)))
       fatal(std::string("cannot select the max-min engine: ") + lmmhip_last_error());
   }
   return ctx_;

@@ -244,6 +244,7 @@ private:
 
   // resident mode: delta log (dirty flags + lists of ids)
   bool resident_ = false, res_full_ = true, res_prepared_ = false;
+  int engine_;  // maxmin/solver at construction (applied when the device context is created)
   std::vector<Id> act_cache_;  // active_constraint_set in list order (resident non-selective solves)
   bool act_cache_ok_ = false;
   std::vector<uint8_t> res_de_, res_dv_, res_dc_;

@@ -151,6 +151,8 @@ SIGNATURES = {
     "lmmhip_fb_shard_begin": (I, [P, D, P, P, I64, P]),
     "lmmhip_fb_shard_step": (I, [P, I]),
     "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
+    "lmmhip_fb_work": (I, [P, PI64]),
+    "lmmhip_components": (I, [P, PI, PI, PI64]),
     "lmmhip_actions_upload": (I, [P, I64, ct.POINTER(ct.c_int32), PD, PD, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
     "lmmhip_next_event_full": (I, [P, I, PD]),
     "lmmhip_update_actions_full": (I, [P, I, D, D, D, PI64]),
@@ -395,6 +397,20 @@ class System:
         return dict(rounds=c[0], n_var=c[1], n_cnst=c[2], nnz=c[3], device_ms=m[0], flatten_ms=m[1],
                     upload_ms=m[2], fetch_ms=m[3], delta_records=lib().lmm_last_delta_records(self.h))
 
+    def components(self):
+        """Connected components of the system the next solve() runs on (its device flatten, lmm_prepare):
+        (label per dense variable, label per dense constraint, count) — see ctx_components."""
+        self.prepare()
+        st = self.last_stats()
+        return ctx_components(self.device_ctx(), st["n_var"], st["n_cnst"])
+
+    def fb_work(self):
+        """The last FairBottleneck solve's work summed over its rounds (lmmhip_fb_work): (elements of the
+        listed constraints, listed variables, listed constraints) — SURVEY.md §8(d)'s nnz_r, V_r, C_r."""
+        w = (I64 * 3)()
+        _check_hip(lib().lmmhip_fb_work(self.device_ctx(), w))
+        return w[0], w[1], w[2]
+
     # resident mode (include/lmm/lmm_system.h, lmm_set_resident): HBM mirror + delta log + device flatten
     def set_resident(self, on=True):
         _check(lib().lmm_set_resident(self.h, int(bool(on))))
@@ -615,6 +631,15 @@ class System:
         out = np.empty(len(ids), dtype=np.float64)
         lib().lmm_get_values(self.h, ids.ctypes.data_as(PI64), len(ids), out.ctypes.data_as(PD))
         return out
+
+
+def ctx_components(ctx, nv, nc):
+    """lmmhip_components on a device context holding an uploaded / flattened system of nv variables and nc
+    constraints: (var labels, cnst labels, count), compact ids in the order of each component's smallest
+    node (variables first, then constraints)."""
+    vl, cl, n = np.empty(nv, np.int32), np.empty(nc, np.int32), I64()
+    _check_hip(lib().lmmhip_components(ctx, vl.ctypes.data_as(PI), cl.ctypes.data_as(PI), ct.byref(n)))
+    return vl, cl, n.value
 
 
 def solve_batch(systems):

@@ -5,8 +5,9 @@ the solve's data path.
   systems per rank balanced by nnz (`balanced_blocks`); each rank solves its block as one device launch
   sequence (`lmm.solve_batch`).  Weak scaling, nothing exchanged during the solve.
 * Connected components of one system: the closure System::update_modified_set walks
-  (maxmin.cpp:898-922) splits a system into independent sub-systems.  `components` labels them from the
-  flattened device input (`export_flat`, i.e. lmm_flat_export), `pack_components` bin-packs them on the
+  (maxmin.cpp:898-922) splits a system into independent sub-systems.  `device_components` labels them on
+  the device (lmmhip_components, union-find over the flattened system; `System.components()` labels a
+  System's own device flatten), `pack_components` bin-packs them on the
   ranks by nnz, every rank solves its share (`solve_components`), and one all-reduce(SUM) of the disjoint
   per-rank value vectors assembles the result.  A random C2 system or a fat tree carrying random flows
   is one giant component: such a system is solved by replicas only.
@@ -119,9 +120,36 @@ def csc_order_of(f):
     return np.argsort(f.cnst_idx, kind="stable").astype(np.int64)
 
 
-def components(f):
-    """Connected components of the variable-constraint graph: (label per variable, label per
-    constraint, count).  Constraints without an element get labels of their own."""
+def device_components(f, device=None):
+    """Connected components of flat `f`'s variable-constraint graph on the device (lmmhip_components:
+    lock-free union-find, maxmin.cpp:898-922's closure for every component at once): (label per variable,
+    label per constraint, count), labels in the order of each component's smallest node (variables first)."""
+    L = lmm.lib()
+    if device is None:
+        import torch
+
+        device = torch.cuda.current_device()
+    ctx = ct.c_void_p()
+    if L.lmmhip_ctx_create(device, ct.byref(ctx)) != 0:
+        raise lmm.LmmError(L.lmmhip_last_error().decode())
+    try:
+        def p(a, t):
+            return a.ctypes.data_as(ct.POINTER(t))
+
+        nv, nc, nnz = len(f.penalty), len(f.cbound), len(f.cnst_idx)
+        if L.lmmhip_upload(ctx, nv, nc, nnz, p(f.var_ptr, ct.c_int64), p(f.cnst_idx, ct.c_int32),
+                           p(f.weight, ct.c_double), p(f.penalty, ct.c_double), p(f.vbound, ct.c_double),
+                           p(f.cbound, ct.c_double), p(f.cflags, ct.c_uint8)) != 0:
+            raise lmm.LmmError(L.lmmhip_last_error().decode())
+        return lmm.ctx_components(ctx, nv, nc)
+    finally:
+        L.lmmhip_ctx_destroy(ctx)
+
+
+def components_host(f):
+    """Connected components of the variable-constraint graph on the host (scipy): (label per variable,
+    label per constraint, count).  Constraints without an element get labels of their own.  The checker of
+    the device labelling and the labeler of the CPU-only tests; the product path is device_components."""
     from scipy.sparse import coo_matrix
     from scipy.sparse.csgraph import connected_components
 
@@ -341,12 +369,12 @@ def next_event_date(local_min, exchange):
 
 # ---- sharded solves ---------------------------------------------------------------------------
 
-def solve_components(f, kind, exchange, solve_flat=None):
+def solve_components(f, kind, exchange, solve_flat=None, labeler=None):
     """Solve flattened system `f` (identical on every rank) with its connected components spread over
     the ranks.  Returns the dense value vector (all ranks get all values).  `solve_flat(sub, kind)`
-    defaults to the device solver."""
+    defaults to the device solver, `labeler(f)` to the device labelling (device_components)."""
     solve_flat = solve_flat or device_solve_flat
-    var_lab, cnst_lab, n = components(f)
+    var_lab, cnst_lab, n = (labeler or device_components)(f)
     nnz = np.bincount(np.repeat(var_lab, np.diff(f.var_ptr)), minlength=n) + np.bincount(var_lab, minlength=n)
     owner = pack_components(nnz, exchange.world)
     mine = owner == exchange.rank
@@ -499,6 +527,12 @@ class DeviceFbShard:
         done, rounds = ct.c_int(), ct.c_int64()
         self._check(self.L.lmmhip_fb_shard_poll(self.ctx, ct.byref(done), ct.byref(rounds)))
         return bool(done.value), rounds.value
+
+    def fb_work(self):
+        """This shard's part of the solve's work (lmmhip_fb_work): (elements, variables, constraints)."""
+        w = (ct.c_int64 * 3)()
+        self._check(self.L.lmmhip_fb_work(self.ctx, w))
+        return w[0], w[1], w[2]
 
     def values(self):
         x = np.empty(self.n, np.float64)

@@ -50,3 +50,76 @@ def test_device_fb_sharded(local_parts):
         sh.close()
     want = oracle_dense_values(o, ovars, f)
     assert x.tobytes() == want.tobytes(), int(np.count_nonzero(x != want))
+
+
+def canonical(var_lab, cnst_lab):
+    """Labels renamed by first occurrence over [variables, constraints] (the device's own numbering:
+    components in the order of their smallest node)."""
+    lab = np.concatenate([var_lab, cnst_lab]).astype(np.int64)
+    _, first, inv = np.unique(lab, return_index=True, return_inverse=True)
+    rank = np.empty(len(first), np.int64)
+    rank[np.argsort(first, kind="stable")] = np.arange(len(first))
+    return rank[inv]
+
+
+def component_systems():
+    from simgrid_amd import lmm as L
+
+    out = [("medium+dragonfly maxmin", build_pair(0)[0]), ("dragonfly L07", build_pair(1)[0])]
+    s = L.System(False)  # C4-style: LV08 flows on the fat tree (one giant component + idle links)
+    s.gen_platform_flows(L.platform_params(model=L.LV08, n_flows=20_000, seed=3, topology=0,
+                                           topo_parameters="3;16,16,16;1,16,16;1,1,1", loopback_bw=1e8))
+    out.append(("fat tree LV08", s))
+    s = L.System(False)  # sparse random: many small components (k = 1 and 2 elements per variable)
+    s.gen_synthetic(50_000, 30_000, 1, seed=4)
+    s.gen_synthetic(50_000, 20_000, 2, seed=5)
+    out.append(("sparse synthetic", s))
+    return out
+
+
+def test_device_components_match_scipy():
+    """lmmhip_components (device union-find) against scipy's connected_components on the same flattened
+    systems: identical labels up to renaming (the device numbering is scipy's renamed by first occurrence)."""
+    for name, s in component_systems():
+        f = M.export_flat(s)
+        dv, dc, dn = M.device_components(f)
+        hv, hc, hn = M.components_host(f)
+        assert dn == hn, (name, dn, hn)
+        assert np.array_equal(np.concatenate([dv, dc]), canonical(hv, hc)), name
+        sv, sc, sn = s.components()  # the System's own device flatten, no export
+        assert sn == dn and np.array_equal(sv, dv) and np.array_equal(sc, dc), name
+
+
+def _gloo_worker(rank, world, port, kind, out_dir):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        s, _, _ = build_pair(kind)
+        f = M.export_flat(s)
+        x = M.solve_components(f, kind, M.DistExchange())  # device labels, device sub-solves
+        np.save(os.path.join(out_dir, f"x{rank}.npy"), x)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_gloo_world2_device_components(kind, tmp_path):
+    """The component-sharded solve of test_multi.py's gloo world-2 run with the product path on both ranks:
+    components labelled on the device, each rank's share solved on the device."""
+    import torch.multiprocessing as mp
+
+    from tests.test_multi import _free_port
+
+    mp.spawn(_gloo_worker, args=(2, _free_port(), kind, str(tmp_path)), nprocs=2, join=True)
+    s, o, ovars = build_pair(kind)
+    f = M.export_flat(s)
+    o.solve()
+    want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
+    for r in range(2):
+        x = np.load(tmp_path / f"x{r}.npy")
+        assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want))), r

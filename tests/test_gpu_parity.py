@@ -243,6 +243,47 @@ def test_synthetic_midsize_vs_oracle(variant):
     assert np.all(np.abs(x - y) <= tol), float(np.max(np.abs(x - y)))
 
 
+def saturated_dense(f, x, prec):
+    """Saturated constraints (maxmin.cpp print()'s test, `bound - usage <= bound * prec`) of the flattened
+    system `f` (multi.export_flat) under the dense variable values `x`: usage = sum (FATPIPE: max) of w x."""
+    rows = np.repeat(np.arange(len(f.penalty)), np.diff(f.var_ptr))
+    wx = f.weight * x[rows]
+    use = np.bincount(f.cnst_idx, weights=wx, minlength=len(f.cbound))
+    fat = (f.cflags & 1).astype(bool)
+    if fat.any():
+        mx = np.zeros(len(f.cbound))
+        np.maximum.at(mx, f.cnst_idx, wx)
+        use = np.where(fat, mx, use)
+    return np.flatnonzero(~(f.cbound - use > f.cbound * prec))
+
+
+@pytest.mark.parametrize("variant", ["plain", "stress"])
+def test_synthetic_c2_tenth_vs_oracle(variant):
+    """The C2 generator at 1/10 scale (1e5 x 1e6 x 8, the bench's CPU-baseline sample: ~45k sequential
+    reference rounds, maxmin.cpp:560-680) on the device against the oracle: every variable within
+    K.ABS_TOL / K.REL_TOL and the same saturated constraint set."""
+    from simgrid_amd import multi as M
+
+    kw = dict(penalty_mix=1, bounded_permille=100, fatpipe_permille=50) if variant == "stress" else {}
+    ps, os_ = L.System(False), O.System(False)
+    pv = ps.gen_synthetic(100_000, 1_000_000, 8, seed=1, **kw)
+    ov = os_.gen_synthetic(100_000, 1_000_000, 8, seed=1, **kw)
+    f = M.export_flat(ps)
+    ps.solve()
+    os_.solve()
+    x = ps.values_of(pv)
+    y = os_.values_of(ov, len(pv))
+    assert ps.last_stats()["n_var"] > 900_000
+    tol = np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(y))
+    diff = np.abs(x - y)
+    assert np.all(diff <= tol), (float(diff.max()), int(np.count_nonzero(diff > tol)))
+    # dense variable i of the flat system is host variable f.var_ids[i]; the generator made pv in order
+    pos = np.searchsorted(pv, f.var_ids) if np.all(np.diff(pv) > 0) else None
+    assert pos is not None and np.array_equal(pv[pos], f.var_ids)
+    prec = L.get_precision()
+    np.testing.assert_array_equal(saturated_dense(f, x[pos], prec), saturated_dense(f, y[pos], prec))
+
+
 @pytest.mark.slow
 def test_synthetic_full_size_certificate():
     """C2 at full size (1e6 x 1e7 x 8): too big for the O(R*L) oracle, so check size-independent

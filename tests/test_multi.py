@@ -77,12 +77,12 @@ def test_pack_components():
 def test_components_and_single_rank_sharded_solve(kind):
     s, o, ovars = build_pair(kind)
     f = M.export_flat(s)
-    var_lab, cnst_lab, n = M.components(f)
+    var_lab, cnst_lab, n = M.components_host(f)
     assert n >= (8 if kind == 0 else 2)
     # every element joins a variable to a constraint of its own component
     rows = np.repeat(np.arange(len(f.penalty)), np.diff(f.var_ptr))
     assert np.all(var_lab[rows] == cnst_lab[f.cnst_idx])
-    x = M.solve_components(f, kind, M.LocalExchange(), oracle_solve_flat)
+    x = M.solve_components(f, kind, M.LocalExchange(), oracle_solve_flat, M.components_host)
     o.solve()
     want = np.array([ovars[int(i)].get_value() for i in f.var_ids])
     assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want)))
@@ -102,7 +102,7 @@ def _worker(rank, world, port, kind, out_dir):
         ex = M.DistExchange()
         s, _, _ = build_pair(kind)
         f = M.export_flat(s)
-        x = M.solve_components(f, kind, ex, oracle_solve_flat)
+        x = M.solve_components(f, kind, ex, oracle_solve_flat, M.components_host)
         date = M.next_event_date([0.5, 0.25][rank] if rank < 2 else -1.0, ex)
         none = M.next_event_date(-1.0, ex)
         np.save(os.path.join(out_dir, f"x{rank}.npy"), x)
