@@ -167,9 +167,10 @@ int lmmhip_round_profile(lmmhip_ctx* ctx, int64_t* alive_vars, int64_t* alive_el
 /* Per round of the last profiled maxmin solve: variables re-evaluated by the vote phase and their
  * elements.  Returns the number of rounds. */
 int lmmhip_vote_profile(lmmhip_ctx* ctx, int64_t* reeval_vars, int64_t* reeval_elems, int cap);
-/* Vote diagnostics of the last profiled maxmin solve run with LMMHIP_VOTE_DIAG set, 4 per round: rows whose
- * target's key changed, sensitive rows (skey 0), rows queued for a re-vote, constraints flagged changed. */
-int lmmhip_vote_diag_profile(lmmhip_ctx* ctx, int64_t* out4, int cap);
+/* Vote diagnostics of the last profiled maxmin solve run with LMMHIP_VOTE_DIAG set, 8 per round: rows whose
+ * target's key changed, sensitive rows (skey 0), rows queued for a re-vote, constraints flagged changed,
+ * distinct targets of the queued rows, the sum of those targets' CSC degrees, queued sensitive rows, 0. */
+int lmmhip_vote_diag_profile(lmmhip_ctx* ctx, int64_t* out8, int cap);
 
 /* Launch on `hip_stream` (a hipStream_t, e.g. a torch.cuda.Stream's cuda_stream) instead of the
  * context's own stream.  Lets a caller order its collectives and the solver's kernels on one stream

@@ -20,9 +20,11 @@ for v in "$@"; do
     if [ $rc -ne 0 ]; then echo "STOP $v $w rc=$rc"; tail -n 20 gpurun_out/ab_${i}_$w.log; exit $rc; fi
   done
   [ -n "$NOPROF" ] && { python3 scripts/ab_summary.py "$v" $i; continue; }
+  if [ -z "$NOC2PROF" ]; then
   env $envs timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --dropin-steps 0 \
     --profile-json gpurun_out/ab_${i}_c2prof.json > /dev/null 2> gpurun_out/ab_${i}_c2prof.log; rc=$?
   if [ $rc -ne 0 ]; then echo "STOP $v c2prof rc=$rc"; tail -n 20 gpurun_out/ab_${i}_c2prof.log; exit $rc; fi
+  fi
   env $envs timeout -k 10 200 python scripts/diag_r2.py c4 > gpurun_out/ab_${i}_diag.log 2>&1; rc=$?
   if [ $rc -ne 0 ]; then echo "STOP $v diag rc=$rc"; tail -n 20 gpurun_out/ab_${i}_diag.log; exit $rc; fi
   python3 scripts/ab_summary.py "$v" $i

@@ -20,6 +20,7 @@ run() {  # run <log> <limit s> <command...>
 wl_args() {  # bench arguments of one short run of a workload
   case $1 in
     c2) echo "--steps $2 --warmup 1 --no-cpu-baseline --dropin-steps 0";;
+    c2_stress) echo "--variant stress --steps $2 --warmup 1 --no-cpu-baseline --dropin-steps 0";;
     *) echo "--workload $1 --steps $2 --warmup 1 --no-cpu-baseline";;
   esac
 }

@@ -38,6 +38,8 @@ enum : int {
   // fair bottleneck: the reference's work summed over the rounds, three uint64 words:
   // elements of the listed constraints, listed variables, listed constraints (words 24..29)
   CTL_FBW = 24,
+  // multi-launch maxmin, voter index (mm_vote_idx): rows appended to the overflow list since the last rebuild
+  CTL_NOVF = 30,
   CTL_WORDS = 32
 };
 
@@ -140,7 +142,6 @@ struct Dev {
   int32_t* bready;  // [kMaxBlocks] ready count of each segment
   uint64_t* chgbits;  // [nC/64 + 2] bitmap: constraints changed in the last round (written by mm_update)
   int32_t* balive;  // [kMaxBlocks] constraints still alive after mm_update, per block
-  int32_t* touch[2];  // [nC] touched-constraint lists, per round parity
   int32_t* clist[2];  // [nC] alive-constraint lists (periodically compacted)
   // alive-row buffers: 0 = the original CSR (identity ids), 1/2 = compaction targets
   const int32_t* cvar[3];
@@ -160,6 +161,16 @@ struct Dev {
   int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag); sharded: all-reduce SUM
   double* xmin;              // [nC] one context: min of w*mu per FATPIPE constraint
   double* fbd;               // [nnz] one context: w*mu of every shared constraint's element, CSC order
+  // multi-launch maxmin, voter index (mm_vote_idx): the alive rows of the buffer in use grouped by
+  // the constraint they vote for, rebuilt every few rounds; rows that moved since sit in the overflow list.
+  uint32_t* vbeg;     // [nC+1] segment of each constraint in vidx / vsk
+  int32_t* vidx;      // [nV] row ids, segment by segment
+  uint16_t* vsk;      // [nV] the rows' floors (skey), kStaleFloor = the row moved to another constraint
+  int32_t* vpos;      // [nV] per row: its position in vidx, -1 = not indexed (moved: in the overflow list)
+  int32_t* ovl;       // [nV] overflow list (ctl CTL_NOVF entries)
+  uint32_t* mf;       // [nC] lower bound of the floors of the constraint's voters (0xFFFFFFFF = none)
+  uint32_t* vcnt;     // [nC] rebuild scratch: voters per constraint (zero between rebuilds)
+  uint64_t* flagbits;  // [nC/64 + 2] constraints whose voters the next vote must scan (written by mm_update)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };
@@ -172,6 +183,8 @@ __device__ __forceinline__ bool rbounded(int32_t cv) { return cv < 0; }
 constexpr int kStatRounds = 4096;  // rounds covered by the profiling counters
 constexpr int32_t kUnvoted = -1;   // row target: not evaluated yet
 constexpr int32_t kRetired = -2;   // row target: variable fixed or dropped (skip until compaction)
+constexpr uint16_t kStaleFloor = 0xFFFF;  // voter-index entry of a row that moved (a real floor of 0xFFFF is
+                                          // stored as 0xFFFE: no live key lies between the two)
 
 __device__ __forceinline__ double dinf() { return __builtin_huge_val(); }
 

@@ -69,8 +69,9 @@ __global__ void __launch_bounds__(kBlock) fb_pack_vst(Dev s) {
   }
 }
 
-// :67-74 — listed variables (w > 0: every flattened element) of each chunk of a listed constraint
-__global__ void __launch_bounds__(kBlock) fbk_count(Dev s) {
+// :67-74 — listed variables (w > 0: every flattened element) of each chunk of a listed constraint.  all = 1
+// (round 0: fair_bottleneck.cpp:29-41 lists every flattened variable): the chunk's length, nothing gathered.
+__global__ void __launch_bounds__(kBlock) fbk_count(Dev s, int all) {
   if (s.ctl[CTL_DONE])
     return;
   const int lane = threadIdx.x & (kWave - 1);
@@ -78,6 +79,11 @@ __global__ void __launch_bounds__(kBlock) fbk_count(Dev s) {
   for (int q = blockIdx.x * wpb + threadIdx.x / kWave; q < s.nch; q += gridDim.x * wpb) {
     const int c = s.ch_cnst[q];
     int nb = 0;
+    if (all) {
+      if (lane == 0)
+        s.pcnt[q] = int(chunk_end(s, q, c) - s.ch_beg[q]);
+      continue;
+    }
     if (s.ratio[c] == 0.0) {
       const uint32_t e = chunk_end(s, q, c);
       for (uint32_t j0 = s.ch_beg[q] + lane; j0 < e; j0 += 4 * kWave) {  // 4 gathers in flight per lane
@@ -273,7 +279,9 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
 // (vtmp) no longer moves, so its increment written in its last listed round still holds (every variable is
 // listed in round 0, a listed constraint was listed in every earlier round); vstb = the flags before
 // fb_var_inc.
-__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
+// Shared constraints shorter than `longmin` elements take their increments in fbk_update_seq itself (fb_chain_pull);
+// only the long ones, whose chains are the round's critical path, get them precomputed here.
+__global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int all, uint32_t longmin) {  // all: round 0, every variable listed
   if (s.ctl[CTL_DONE])
     return;
   const int lane = threadIdx.x & (kWave - 1);
@@ -282,6 +290,8 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
     const int c = s.ch_cnst[q];
     const bool fat = s.cflags[c] & 1;
     if (s.ratio[c] != 0.0)
+      continue;
+    if (!fat && s.cnst_ptr[c + 1] - s.cnst_ptr[c] < longmin)
       continue;
     if (!fat) {
       const uint32_t e = chunk_end(s, q, c);
@@ -292,10 +302,12 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s) {
           const uint32_t j = j0 + k * kWave;
           vv[k] = j < e ? s.csc_v[j] : -1;
         }
+        if (!all) {
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-          if (vv[k] >= 0 && !((s.vstb[vv[k] >> 5] >> (vv[k] & 31)) & 1))
-            vv[k] = -1;
+          for (int k = 0; k < 4; k++)
+            if (vv[k] >= 0 && !((s.vstb[vv[k] >> 5] >> (vv[k] & 31)) & 1))
+              vv[k] = -1;
+        }
         double dv[4];
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -362,6 +374,53 @@ __device__ __forceinline__ double fb_fat_update(const Dev& s, int64_t c, double 
 // at every step.
 constexpr int kSeqP = 8;  // 64-element blocks per batch
 
+// Lane 0: the n increments of one batch (d, in LDS; slots past n hold 0.0) chained into rem.
+__device__ __forceinline__ double fb_chain_batch(const double* d, int n, double rem, double prec, bool nonneg) {
+  if (nonneg) {
+    // kG increments per step, the next kG read from LDS while these are chained (slots past n hold 0.0:
+    // r - 0 == r); two register sets used in turn, so nothing is copied between steps
+    constexpr int kG = 32, kH = kG / 2;
+    const double2* dd = reinterpret_cast<const double2*>(d);
+    double2 ra[kH], rb[kH];
+#pragma unroll
+    for (int t = 0; t < kH; t++)
+      ra[t] = dd[t];
+    for (int k = 0; k < n; k += 2 * kG) {
+      if (k + kG < n) {
+#pragma unroll
+        for (int t = 0; t < kH; t++)
+          rb[t] = dd[(k + kG) / 2 + t];
+      }
+#pragma unroll
+      for (int t = 0; t < kH; t++) {
+        rem -= ra[t].x;
+        rem -= ra[t].y;
+      }
+      if (k + kG >= n)
+        break;
+      if (k + 2 * kG < n) {
+#pragma unroll
+        for (int t = 0; t < kH; t++)
+          ra[t] = dd[(k + 2 * kG) / 2 + t];
+      }
+#pragma unroll
+      for (int t = 0; t < kH; t++) {
+        rem -= rb[t].x;
+        rem -= rb[t].y;
+      }
+    }
+    if (rem < prec)
+      rem = 0.0;
+  } else {
+    for (int k = 0; k < n; k++) {
+      rem -= d[k];
+      if (rem < prec)
+        rem = 0.0;
+    }
+  }
+  return rem;
+}
+
 __device__ __forceinline__ double fb_chain(const double* __restrict__ fbd, uint32_t cb, uint32_t ce, double rem,
                                            double prec, double* d, int lane) {
   double nx[kSeqP];
@@ -385,59 +444,69 @@ __device__ __forceinline__ double fb_chain(const double* __restrict__ fbd, uint3
       nx[p] = j < ce ? fbd[j] : 0.0;
     }
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      const int n = int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave));
-      if (nonneg) {
-        // kG increments per step, the next kG read from LDS while these are chained (slots past n
-        // hold 0.0: r - 0 == r); two register sets used in turn, so nothing is copied between steps
-        constexpr int kG = 32, kH = kG / 2;
-        const double2* dd = reinterpret_cast<const double2*>(d);
-        double2 ra[kH], rb[kH];
+    if (lane == 0)
+      rem = fb_chain_batch(d, int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave)), rem,
+                           prec, nonneg);
+    __builtin_amdgcn_wave_barrier();
+  }
+  return rem;
+}
+
+// fb_chain with the increments computed on the fly, w * mu for EVERY element of the constraint (a delisted
+// variable's mu, vtmp, is the one of its last listed round: the same product fbk_acc would have kept in fbd):
+// the element loads run two batches ahead and the mu gathers one batch ahead of the chain.
+__device__ __forceinline__ double fb_chain_pull(const Dev& s, uint32_t cb, uint32_t ce, double rem, double prec,
+                                                double* d, int lane) {
+  int32_t ix[kSeqP];
+  double ww[kSeqP], vt[kSeqP];
 #pragma unroll
-        for (int t = 0; t < kH; t++)
-          ra[t] = dd[t];
-        for (int k = 0; k < n; k += 2 * kG) {
-          if (k + kG < n) {
+  for (int p = 0; p < kSeqP; p++) {  // batch 0: elements, then their mu
+    const uint32_t j = cb + p * kWave + lane;
+    ix[p] = j < ce ? s.csc_v[j] : -1;
+    ww[p] = j < ce ? s.csc_w[j] : 0.0;
+  }
 #pragma unroll
-            for (int t = 0; t < kH; t++)
-              rb[t] = dd[(k + kG) / 2 + t];
-          }
+  for (int p = 0; p < kSeqP; p++)
+    vt[p] = ix[p] >= 0 ? s.vtmp[ix[p]] : 0.0;
 #pragma unroll
-          for (int t = 0; t < kH; t++) {
-            rem -= ra[t].x;
-            rem -= ra[t].y;
-          }
-          if (k + kG >= n)
-            break;
-          if (k + 2 * kG < n) {
+  for (int p = 0; p < kSeqP; p++) {  // batch 1's elements
+    const uint32_t j = cb + kSeqP * kWave + p * kWave + lane;
+    ix[p] = j < ce ? s.csc_v[j] : -1;
+  }
+  for (uint32_t base = cb; base < ce; base += kSeqP * kWave) {  // wave-uniform
+    bool nonneg = true;
 #pragma unroll
-            for (int t = 0; t < kH; t++)
-              ra[t] = dd[(k + 2 * kG) / 2 + t];
-          }
-#pragma unroll
-          for (int t = 0; t < kH; t++) {
-            rem -= rb[t].x;
-            rem -= rb[t].y;
-          }
-        }
-        if (rem < prec)
-          rem = 0.0;
-      } else {
-        for (int k = 0; k < n; k++) {
-          rem -= d[k];
-          if (rem < prec)
-            rem = 0.0;
-        }
-      }
+    for (int p = 0; p < kSeqP; p++) {
+      const double x = ww[p] * vt[p];  // (0 * 0 past the end: r - 0 == r)
+      d[p * kWave + lane] = x;
+      nonneg &= x >= 0.0;
     }
+    nonneg = __all(nonneg);
+    const uint32_t nb = base + kSeqP * kWave, nb2 = nb + kSeqP * kWave;
+#pragma unroll
+    for (int p = 0; p < kSeqP; p++) {  // next batch: mu gathers (its elements arrived) and weights
+      const uint32_t j = nb + p * kWave + lane;
+      vt[p] = ix[p] >= 0 ? s.vtmp[ix[p]] : 0.0;
+      ww[p] = j < ce ? s.csc_w[j] : 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < kSeqP; p++) {  // the batch after: elements
+      const uint32_t j = nb2 + p * kWave + lane;
+      ix[p] = j < ce ? s.csc_v[j] : -1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0)
+      rem = fb_chain_batch(d, int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave)), rem,
+                           prec, nonneg);
     __builtin_amdgcn_wave_barrier();
   }
   return rem;
 }
 
 // :107-140 for ONE context: one wave per listed constraint, shared ones through fb_chain over fbd (written by
-// fbk_acc), FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0 erases the constraint (:129).
-__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
+// fbk_acc) when they hold `longmin` elements or more, fb_chain_pull otherwise; FATPIPE ones from the chunk
+// minima (fbk_accc); remaining <= 0 erases the constraint (:129).
+__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
@@ -456,7 +525,9 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec) {
       if (lane == 0)
         s.use[c] = u;
     } else {
-      rem = fb_chain(s.fbd, s.cnst_ptr[c], s.cnst_ptr[c + 1], rem, prec, d, lane);
+      const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
+      rem = ce - cb >= longmin ? fb_chain(s.fbd, cb, ce, rem, prec, d, lane)
+                               : fb_chain_pull(s, cb, ce, rem, prec, d, lane);
     }
     if (lane == 0) {
       s.rem[c] = rem;

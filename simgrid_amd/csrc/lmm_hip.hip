@@ -104,6 +104,7 @@ struct lmmhip_ctx {
   int64_t bt_cap = 0;
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
   int64_t fb_round = 0;
+  uint32_t fb_longmin = 0;  // solve_fair: shared constraints with >= this many elements use fbk_acc's increments
   double fb_prec = 0;
   bool fb_shard = false;
   FbOwner fbo{};                   // sharded solve: the owned constraints (lmmhip_fb_shard_owner)
@@ -142,6 +143,7 @@ struct lmmhip_ctx {
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
+  Scr pbig;                               // persistent engine: big ready constraints of a round (sat_big)
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
@@ -241,7 +243,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->pbig, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch})
@@ -333,6 +335,7 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   }
   rc |= dalloc(c, &d.chg, nC);
   rc |= dalloc(c, &d.chgbits, (nC + 127) / 128 * 2 + 2);
+  rc |= dalloc(c, &d.flagbits, (nC + 127) / 128 * 2 + 2);
   rc |= dalloc(c, &d.ready, nC + kMaxBlocks);
   rc |= dalloc(c, &d.bready, kMaxBlocks);
   rc |= dalloc(c, &d.ctouch, nC);
@@ -1146,6 +1149,7 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
       if (c->profiling && c->vote_diag) {  // measurement: bitmap load alone, filter alone (slot 7)
         LAUNCH(7, r + 1000000, (mm_vote_lane<kVBlock, true, 2>), c->n_cu, kVBlock, d, int(r));
         LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
+        LAUNCH(7, r, mm_vote_diagcount, grid_for((int64_t(d.nC) + 63) / 64, kBlock), kBlock, d, int(r));
       }
       LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, int(r));
     } else {
@@ -1319,7 +1323,15 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
     pt = c->ptime;
   }
   int sysf = env_int("LMMHIP_PERSIST_SYSFENCE", 0);
-  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf};
+  // ready constraints of more than bigch 64-element chunks are shared by the whole grid (sat_big); 0 = off
+  int bigch = env_int("LMMHIP_PBIG", 16);
+  int32_t* big = nullptr;
+  if (bigch > 0) {
+    if (int rc = scratch(c, c->pbig, 2 * int64_t(d.nC) + 2, &big))
+      return rc;
+  }
+  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf,
+                  &big, &bigch};
   // A plain launch on the context's stream: the occupancy query above guarantees one workgroup per CU, so the
   // n_cu workgroups are co-resident once the stream's earlier work has drained, and every barrier wait is
   // bounded (CTL_ERR) should they not be.  hipLaunchCooperativeKernel (LMMHIP_PERSIST_COOP=1) runs the same
@@ -1401,9 +1413,10 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
   const int gC = grid_for(d.nC, kBlock);
   const int gV = grid_for(d.nV, kBlock);
   switch (phase) {
-  case 0:
-    LAUNCH(2, r, fb_pack_vst, grid_for((int64_t(d.nV) + 31) / 32, kBlock), kBlock, d);
-    LAUNCH(2, r, fbk_count, gQ, kBlock, d);
+  case 0:  // round 0 lists every flattened variable (fair_bottleneck.cpp:29-41): counts without gathers
+    if (r > 0)
+      LAUNCH(2, r, fb_pack_vst, grid_for((int64_t(d.nV) + 31) / 32, kBlock), kBlock, d);
+    LAUNCH(2, r, fbk_count, gQ, kBlock, d, int(r == 0));
     LAUNCH(2, r, fbk_nb, gC, kBlock, d, par);
     break;
   case 1:
@@ -1413,7 +1426,7 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
       LAUNCH(3, r, fbo_put_mu, gV, kBlock, d, c->fbo);
       break;
     }
-    LAUNCH(4, r, fbk_acc, gQ, kBlock, d);
+    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(r == 0), c->fb_longmin);
     LAUNCH(4, r, fbk_accc, gC, kBlock, d);
     break;
   case 2:
@@ -1423,7 +1436,7 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
       break;
     }
     // one context: element by element in the CSC order, bit-identical to the reference
-    LAUNCH(5, r, fbk_update_seq, grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec);
+    LAUNCH(5, r, fbk_update_seq, grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec, c->fb_longmin);
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
     c->fb_round++;
     break;
@@ -1442,6 +1455,9 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
 
 static int solve_fair(lmmhip_ctx* c, double prec) {
   c->fb_shard = false;
+  // shared constraints of at least this many elements get their increments precomputed element-parallel
+  // (fbk_acc) for their critical-path chains; shorter ones compute them inside the chain (fb_chain_pull)
+  c->fb_longmin = uint32_t(std::max(0, env_int("LMMHIP_FB_LONG", 16384)));
   if (c->fbd_cap < c->d.nnz) {  // increments in CSC order (fbk_acc -> fbk_update_seq)
     if (int rc = dalloc(c, &c->d.fbd, c->d.nnz))
       return rc;
@@ -2079,7 +2095,7 @@ int lmmhip_vote_profile(lmmhip_ctx* c, int64_t* rows, int64_t* elems, int cap) {
   return R;
 }
 
-int lmmhip_vote_diag_profile(lmmhip_ctx* c, int64_t* out4, int cap) {
+int lmmhip_vote_diag_profile(lmmhip_ctx* c, int64_t* out8, int cap) {
   if (!c || !c->vstat)
     return fail(LMMHIP_E_STATE, "no profiled maxmin solve");
   const int R = int(std::min<int64_t>(c->stats.rounds, kStatRounds));
@@ -2087,8 +2103,8 @@ int lmmhip_vote_diag_profile(lmmhip_ctx* c, int64_t* out4, int cap) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpy(h.data(), c->vstat, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost));
   for (int r = 0; r < R && r < cap; r++)
-    for (int k = 0; k < 4; k++)
-      out4[4 * r + k] = h[2 * (size_t(r) * kMaxBlocks + kDiagSlot) + k];
+    for (int k = 0; k < 8; k++)
+      out8[8 * r + k] = h[2 * (size_t(r) * kMaxBlocks + kDiagSlot) + k];
   return R;
 }
 

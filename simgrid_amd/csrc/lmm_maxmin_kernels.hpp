@@ -565,7 +565,7 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   const uint16_t prev = uint16_t(round - 1);
   const unsigned long long below = (1ull << lane) - 1;
   int qn = 0, nq = 0;
-  int dg[3] = {0, 0, 0};  // kDiag 1: target-changed / sensitive / queued rows of this lane
+  int dg[4] = {0, 0, 0, 0};  // kDiag 1: target-changed / sensitive / queued / queued sensitive rows of this lane
   for (int64_t base = wlo; base < whi; base += int64_t(F) * kWave) {  // wave-uniform
     int tt[F];
     unsigned sk[F];
@@ -602,6 +602,10 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         dg[0] += ch[u];
         dg[1] += tt[u] >= 0 && sk[u] == 0;
         dg[2] += need;
+        if (need && tt[u] >= 0) {  // the targets whose voters need a re-vote (mm_vote_diagcount)
+          atomicOr(reinterpret_cast<unsigned long long*>(&s.flagbits[tt[u] >> 6]), 1ull << (tt[u] & 63));
+          dg[3] += sk[u] == 0;
+        }
       }
     }
 #pragma unroll 1
@@ -627,10 +631,10 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
     vote_row<R>(s, buf, round, qw[lane], st_rows, st_elems, key);
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < 4; k++) {
       const int t = grp_isum<kWave>(dg[k]);
       if (lane == 0 && t)
-        atomicAdd(&d[k], t);
+        atomicAdd(&d[k == 3 ? 6 : k], t);
     }
   }
   return nq + qn;
@@ -657,6 +661,30 @@ template <int B> __device__ __forceinline__ void load_bits(const Dev& s, uint64_
     for (int u = 0; u < kU; u++)
       if (i0 + u * B < n16)
         dst[i0 + u * B] = t[u];
+  }
+}
+
+// Vote diagnostics (measurement only): the constraints flagged by the filter pass (targets of queued rows,
+// flagbits) -> their count and the sum of their CSC degrees and voters' share, per round; clears the flags.
+__global__ void __launch_bounds__(kBlock) mm_vote_diagcount(Dev s, int round) {
+  int nf = 0, deg = 0;
+  for (int64_t w = int64_t(blockIdx.x) * kBlock + threadIdx.x; w < (s.nC + 63) / 64; w += int64_t(gridDim.x) * kBlock) {
+    unsigned long long m = s.flagbits[w];
+    s.flagbits[w] = 0;
+    while (m) {
+      const int b = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int64_t c = w * 64 + b;
+      nf++;
+      deg += int(s.cnst_ptr[c + 1] - s.cnst_ptr[c]);
+    }
+  }
+  nf = grp_isum<kWave>(nf);
+  deg = grp_isum<kWave>(deg);
+  if ((threadIdx.x & (kWave - 1)) == 0 && s.vstat && round < kStatRounds) {
+    int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
+    atomicAdd(&d[4], nf);
+    atomicAdd(&d[5], deg);
   }
 }
 
@@ -883,10 +911,68 @@ __device__ __forceinline__ void sat_flush(const Dev& s, int round, SatLds<NB, CA
   __syncthreads();
 }
 
+// Grid-wide sharing of big ready constraints (persistent engine): a ready constraint of more than `bigch`
+// chunks is posted to `list` (pairs: constraint, first global chunk) with ONE 64-bit atomic on `ctr` (count << 32
+// | chunks: entry order = chunk order); once every workgroup has posted (`posted`), every wave takes chunks
+// from `next` until they run out.  The words are reset by the caller between saturations.
+struct BigSat {
+  int32_t* list;
+  unsigned long long* ctr;
+  unsigned* next;
+  unsigned* posted;
+  int bigch;
+  int32_t* err;
+};
+
+__device__ __forceinline__ void sat_big(const Dev& s, int round, const BigSat& bs, int* pre) {
+  const int lane = threadIdx.x & (kWave - 1);
+  if (threadIdx.x == 0) {  // (the workgroup's posts precede this: sat_block's last barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(bs.posted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (lane == 0) {
+    const long long t0 = wall_clock64();
+    while (ld_rlx(bs.posted) < gridDim.x) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > 400000000ll) {  // 4 s: the protocol broke (grid not co-resident?)
+        st_rlx(bs.err, 1);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const unsigned long long tot = ld_rlx(bs.ctr);
+  const int nb = int(tot >> 32);
+  const unsigned total = unsigned(tot);
+  for (;;) {  // wave-uniform
+    unsigned g = 0;
+    if (lane == 0)
+      g = __hip_atomic_fetch_add(bs.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g = __shfl(g, 0, kWave);
+    if (g >= total)
+      break;
+    int lo = 0, hi = nb - 1;  // last entry whose first chunk is <= g
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if (unsigned(ld_rlx(&bs.list[2 * mid + 1])) <= g)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    const int32_t c = ld_rlx(&bs.list[2 * lo]);
+    const unsigned ch = g - unsigned(ld_rlx(&bs.list[2 * lo + 1]));
+    const double r = ld_rlx(&s.cst[c].ratio);
+    saturate_chunk(s, c, r, s.cnst_ptr[c] + ch * kWave, s.cnst_ptr[c + 1], round, lane, pre, s.cdup[c] != 0);
+    if (ch == 0 && lane == 0)
+      s.ctouch[c] = 2;
+  }
+}
+
 // Returns whether the workgroup found a ready constraint.
 template <int NB, int CAP>
 __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t* __restrict__ cl, int64_t n,
-                                          SatLds<NB, CAP>& L) {
+                                          SatLds<NB, CAP>& L, const BigSat* bs = nullptr) {
   static_assert(CAP >= NB, "one pass must fit");
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -899,8 +985,17 @@ __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t
     int32_t c = -1;
     if (i < n)
       c = cl ? cl[i] : int32_t(i);
-    const bool rdy = c >= 0 && s.key[c] != kDeadKey && s.nvote[c] == 0;
-    const int nch = rdy ? int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave) : 0;
+    bool rdy = c >= 0 && s.key[c] != kDeadKey && s.nvote[c] == 0;
+    int nch = rdy ? int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave) : 0;
+    if (bs && nch > bs->bigch) {  // posted to the grid-wide list (sat_big)
+      const unsigned long long o = atomicAdd(bs->ctr, (1ull << 32) | unsigned(nch));
+      const int i = int(o >> 32);
+      bs->list[2 * i] = c;
+      bs->list[2 * i + 1] = int32_t(uint32_t(o));
+      any = true;
+      rdy = false;
+      nch = 0;
+    }
     int ia = rdy, ib = nch;  // block exclusive scans of (ready, chunks)
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -939,6 +1034,11 @@ __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t
   }
   if (L.na)
     sat_flush<NB, CAP>(s, round, L);
+  if (bs) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's posts have reached the L2
+    __syncthreads();  // every wave's posts issued before the workgroup signals
+    sat_big(s, round, *bs, L.pre[threadIdx.x / kWave]);
+  }
   return any;
 }
 

@@ -15,6 +15,10 @@ hipError_t scan_i64(void* tmp, size_t& tmp_bytes, const int64_t* in, int64_t* ou
   return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, n, s);
 }
 
+hipError_t scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, n, s);
+}
+
 // Stable: equal keys keep their input order (the CSC of a constraint lists its elements in CSR order,
 // i.e. by ascending variable, as the host counting sort of lmmhip_upload does).
 hipError_t sort_pairs_i32(void* tmp, size_t& tmp_bytes, const int32_t* keys_in, int32_t* keys_out,

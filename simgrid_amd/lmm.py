@@ -555,14 +555,15 @@ class System:
         return rv[:r], re_[:r]
 
     def vote_diag_profile(self):
-        """LMMHIP_VOTE_DIAG runs: per round (target-changed rows, sensitive rows, queued rows, changed constraints)."""
+        """LMMHIP_VOTE_DIAG runs: per round (target-changed rows, sensitive rows, queued rows, changed constraints,
+        distinct targets of the queued rows, sum of their CSC degrees, queued sensitive rows, 0)."""
         c = self.device_ctx()
-        cap = 1 << 16
-        out = np.zeros(4 * cap, np.int64)
+        cap = 1 << 14
+        out = np.zeros(8 * cap, np.int64)
         r = lib().lmmhip_vote_diag_profile(c, out.ctypes.data_as(PI64), cap)
         if r < 0:
             raise LmmError(lib().lmmhip_last_error().decode())
-        return out[:4 * r].reshape(r, 4)
+        return out[:8 * r].reshape(r, 8)
 
     @property
     def modified(self):

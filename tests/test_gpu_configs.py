@@ -136,14 +136,26 @@ def test_c4_full_size_vs_oracle():
     assert infeasible == 0 and unbottlenecked == 0, (excess, infeasible, unbottlenecked)
 
 
-def test_c5_1e6_flows_vs_oracle():
+@pytest.fixture(scope="module")
+def c5_1e6_oracle():
     p = dict(model=L.L07, n_flows=1_000_000, seed=1, **C5_PLATFORM)
-    s, o = L.System(False, L.System.FAIR_BOTTLENECK), O.System(False, O.System.FAIR_BOTTLENECK)
-    _, vs = s.gen_platform_flows(L.platform_params(**p))
+    o = O.System(False, O.System.FAIR_BOTTLENECK)
     _, ov = o.gen_platform_flows(O.platform_params(**p))
-    s.solve()
     o.solve()
-    x, y = s.values_of(vs), o.values_of(ov, len(vs))
+    return p, o.values_of(ov, p["n_flows"])
+
+
+# LMMHIP_FB_LONG: shared constraints with at least this many elements chain increments precomputed by fbk_acc,
+# shorter ones compute them inside the chain (fb_chain_pull); the C5 1e6 system's longest holds ~1.6e4
+@pytest.mark.parametrize("longmin", ["default", "0", "4096", "1000000000"])
+def test_c5_1e6_flows_vs_oracle(c5_1e6_oracle, longmin, monkeypatch):
+    if longmin != "default":
+        monkeypatch.setenv("LMMHIP_FB_LONG", longmin)
+    p, y = c5_1e6_oracle
+    s = L.System(False, L.System.FAIR_BOTTLENECK)
+    _, vs = s.gen_platform_flows(L.platform_params(**p))
+    s.solve()
+    x = s.values_of(vs)
     bad, worst = _close(x, y)
     assert len(bad) == 0, (len(bad), worst)
     # one context, elements in the reference's list order: the same floating-point operations in the
