@@ -38,8 +38,8 @@ enum : int {
   // fair bottleneck: the reference's work summed over the rounds, three uint64 words:
   // elements of the listed constraints, listed variables, listed constraints (words 24..29)
   CTL_FBW = 24,
-  // multi-launch maxmin, voter index (mm_vote_idx): rows appended to the overflow list since the last rebuild
-  CTL_NOVF = 30,
+  // multi-launch maxmin, target-ordered rows: alive rows counted by the regroup (srt_prep -> srt_flip)
+  CTL_SORTN = 30,
   CTL_WORDS = 32
 };
 
@@ -149,6 +149,7 @@ struct Dev {
   const int32_t* ccol[3];
   int32_t* rtgt[3];  // per row: constraint the variable votes for; kUnvoted / kRetired
   uint16_t* skey[3];  // per row: min key over the row's OTHER constraints at its last vote (0 if bounded)
+  uint32_t* rend[3];  // target-ordered buffers 1 / 2: end of the row's CSR range (crow holds its start)
   int32_t* bsum;    // compaction scratch: per-block rows / elems (2 x blocks)
   // fair bottleneck: CSC chunks (lmm_fb_kernels.hpp) and the per-constraint exchange buffers
   int32_t nch;               // number of chunks
@@ -161,16 +162,13 @@ struct Dev {
   int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag); sharded: all-reduce SUM
   double* xmin;              // [nC] one context: min of w*mu per FATPIPE constraint
   double* fbd;               // [nnz] one context: w*mu of every shared constraint's element, CSC order
-  // multi-launch maxmin, voter index (mm_vote_idx): the alive rows of the buffer in use grouped by
-  // the constraint they vote for, rebuilt every few rounds; rows that moved since sit in the overflow list.
-  uint32_t* vbeg;     // [nC+1] segment of each constraint in vidx / vsk
-  int32_t* vidx;      // [nV] row ids, segment by segment
-  uint16_t* vsk;      // [nV] the rows' floors (skey), kStaleFloor = the row moved to another constraint
-  int32_t* vpos;      // [nV] per row: its position in vidx, -1 = not indexed (moved: in the overflow list)
-  int32_t* ovl;       // [nV] overflow list (ctl CTL_NOVF entries)
-  uint32_t* mf;       // [nC] lower bound of the floors of the constraint's voters (0xFFFFFFFF = none)
-  uint32_t* vcnt;     // [nC] rebuild scratch: voters per constraint (zero between rebuilds)
-  uint64_t* flagbits;  // [nC/64 + 2] constraints whose voters the next vote must scan (written by mm_update)
+  // multi-launch maxmin, target-ordered rows (mm_vote_tgt): regroup scratch — sort keys (the
+  // voted constraint / 16) and packed values (variable id, floor, low target bits), radix-sorted by hipCUB
+  uint32_t* sk_in;
+  uint32_t* sk_out;
+  unsigned long long* sv_in;
+  unsigned long long* sv_out;
+  uint64_t* flagbits;  // [nC/64 + 2] measurement only: targets of the rows the filter queued (kDiag)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };
@@ -183,8 +181,6 @@ __device__ __forceinline__ bool rbounded(int32_t cv) { return cv < 0; }
 constexpr int kStatRounds = 4096;  // rounds covered by the profiling counters
 constexpr int32_t kUnvoted = -1;   // row target: not evaluated yet
 constexpr int32_t kRetired = -2;   // row target: variable fixed or dropped (skip until compaction)
-constexpr uint16_t kStaleFloor = 0xFFFF;  // voter-index entry of a row that moved (a real floor of 0xFFFF is
-                                          // stored as 0xFFFE: no live key lies between the two)
 
 __device__ __forceinline__ double dinf() { return __builtin_huge_val(); }
 

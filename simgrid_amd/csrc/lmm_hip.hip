@@ -143,7 +143,7 @@ struct lmmhip_ctx {
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
-  Scr pbig;                               // persistent engine: big ready constraints of a round (sat_big)
+  Scr tg_kin, tg_kout, tg_vin, tg_vout, tg_tmp;  // multi-launch engine: regroup of target-ordered rows
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
@@ -243,7 +243,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->pbig, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch})
@@ -333,6 +333,9 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
     rc |= dalloc(c, &d.rtgt[b], nV);
     rc |= dalloc(c, &d.skey[b], nV);
   }
+  d.rend[0] = nullptr;
+  rc |= dalloc(c, &d.rend[1], nV);
+  rc |= dalloc(c, &d.rend[2], nV);
   rc |= dalloc(c, &d.chg, nC);
   rc |= dalloc(c, &d.chgbits, (nC + 127) / 128 * 2 + 2);
   rc |= dalloc(c, &d.flagbits, (nC + 127) / 128 * 2 + 2);
@@ -1200,6 +1203,28 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 32);
   const int cmp_pct = env_int("LMMHIP_COMPACT_PCT", 75);
   const int cl_every = env_int("LMMHIP_CLIST_EVERY", 8);
+  // Short rows, LMMHIP_TGT=1 (measured and off by default): target-ordered alive rows
+  // (mm_vote_tgt), regrouped after the first chunk and then every tgt_every rounds by a radix sort on
+  // (target + 1) / 16, instead of the bitmap-filter vote on order-preserving compactions
+  const bool tgt = (c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) != 0;
+  const int tgt_every = env_int("LMMHIP_TGT_EVERY", 16);
+  const uint32_t tg_dead = uint32_t((int64_t(d.nC) + 1) >> 4) + 1;
+  const int tg_bits = 32 - __builtin_clz(tg_dead);
+  void* tg_tmp = nullptr;
+  size_t tg_tb = 0;
+  if (tgt) {
+    int rc = scratch(c, c->tg_kin, d.nV, &d.sk_in);
+    rc = rc ? rc : scratch(c, c->tg_kout, d.nV, &d.sk_out);
+    rc = rc ? rc : scratch(c, c->tg_vin, d.nV, &d.sv_in);
+    rc = rc ? rc : scratch(c, c->tg_vout, d.nV, &d.sv_out);
+    if (rc)
+      return rc;
+    HIPCHK(sort_pairs_u32_u64(nullptr, tg_tb, d.sk_in, d.sk_out, d.sv_in, d.sv_out, d.nV, tg_bits, c->stream));
+    uint8_t* t = nullptr;
+    if (int rc2 = scratch(c, c->tg_tmp, int64_t(tg_tb), &t))
+      return rc2;
+    tg_tmp = t;
+  }
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
   // Host view of the sizes (upper bounds: rows and constraints only leave), refreshed at every poll; they
@@ -1218,7 +1243,12 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   for (;;) {
     const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
-      if (int rc = launch_vote(c, r, nrows))
+      if (tgt) {
+        const int gv = std::min(grid_for(nrows, kBlock * kFilt), kDiagSlot);  // (vstat: a slot per block)
+        if (c->profiling && c->vote_diag)  // measurement: the filter alone (slot 7)
+          LAUNCH(7, r, (mm_vote_tgt<kBlock, 1>), gv, kBlock, d, int(r));
+        LAUNCH(2, r, mm_vote_tgt<kBlock>, gv, kBlock, d, int(r));
+      } else if (int rc = launch_vote(c, r, nrows))
         return rc;
       LAUNCH(3, r, mm_ready, gL, kBlock, d);
       if (sat_k == 1)
@@ -1236,7 +1266,27 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       last_clist = r;
       cl = true;
     }
-    if (r - last_compact >= cmp_every && nrows > 4096) {  // order-preserving compaction of the alive rows
+    if (tgt && r - last_compact >= (last_compact == 0 ? 1 : tgt_every) && nrows > 4096) {  // regroup by target
+      const int g = grid_for(nrows, kBlock * 4);
+      LAUNCH(6, r, srt_prep, g, kBlock, d, nrows, tg_dead);
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (c->profiling) {
+        if (int rc = prof_event(c, &e0))
+          return rc;
+        HIPCHK(hipEventRecord(e0, c->stream));
+      }
+      HIPCHK(sort_pairs_u32_u64(tg_tmp, tg_tb, d.sk_in, d.sk_out, d.sv_in, d.sv_out, nrows, tg_bits, c->stream));
+      if (c->profiling) {
+        if (int rc = prof_event(c, &e1))
+          return rc;
+        HIPCHK(hipEventRecord(e1, c->stream));
+        c->launch_slot.push_back(6);
+        c->launch_round.push_back(int(r));
+      }
+      LAUNCH(6, r, srt_unpack, g, kBlock, d, nrows);
+      LAUNCH(6, r, srt_flip, 1, 1, d);
+      last_compact = r;
+    } else if (!tgt && r - last_compact >= cmp_every && nrows > 4096) {  // order-preserving compaction of the alive rows
       const int nblk = int((nrows + kCompactRows - 1) / kCompactRows);
       LAUNCH(6, r, cmp_count, nblk, kBlock, d);
       LAUNCH(6, r, cmp_scan, 1, 1024, d, nblk, cmp_pct);
@@ -1323,15 +1373,7 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
     pt = c->ptime;
   }
   int sysf = env_int("LMMHIP_PERSIST_SYSFENCE", 0);
-  // ready constraints of more than bigch 64-element chunks are shared by the whole grid (sat_big); 0 = off
-  int bigch = env_int("LMMHIP_PBIG", 16);
-  int32_t* big = nullptr;
-  if (bigch > 0) {
-    if (int rc = scratch(c, c->pbig, 2 * int64_t(d.nC) + 2, &big))
-      return rc;
-  }
-  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf,
-                  &big, &bigch};
+  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf};
   // A plain launch on the context's stream: the occupancy query above guarantees one workgroup per CU, so the
   // n_cu workgroups are co-resident once the stream's earlier work has drained, and every barrier wait is
   // bounded (CTL_ERR) should they not be.  hipLaunchCooperativeKernel (LMMHIP_PERSIST_COOP=1) runs the same

@@ -410,19 +410,22 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
 
 // Re-vote of one row, one lane: the first R elements in registers (their loads in flight together), longer
 // rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
-template <int R>
+// kCsr: the row's elements are read from the CSR (target-ordered rows, mm_vote_tgt: a row keeps its variable id
+// and CSR range); otherwise from the buffer's own row copy.
+template <int R, bool kCsr = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems, const uint16_t* __restrict__ key) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
   const uint32_t* __restrict__ crow = s.crow[buf];
-  const int32_t* __restrict__ ccol = s.ccol[buf];
+  const int32_t* __restrict__ ccol = kCsr ? s.csr_c : s.ccol[buf];
   int32_t* __restrict__ rtgt = s.rtgt[buf];
   uint16_t* __restrict__ skey = s.skey[buf];
   // (key: s.key, or its copy in LDS — persistent engine, small systems)
   const int t = rtgt[row];
   const int32_t cv = cvar[row];
   const int v = rvar(cv);
-  const uint32_t b = crow[row], e = crow[row + 1];
+  // (target-ordered buffers 1 / 2 keep each row's CSR range in crow / rend; buffer 0 is the CSR itself)
+  const uint32_t b = crow[row], e = kCsr && buf != 0 ? s.rend[buf][row] : crow[row + 1];
   const int32_t vst = s.vstate[v];
   const bool bnd = rbounded(cv);
   const double vb = bnd ? s.vbound[v] : -1.0;
@@ -730,6 +733,165 @@ template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B)
   }
 }
 
+// ---- multi-launch engine, short rows, TARGET-ORDERED alive rows (the default for mean row length <= 8) ----
+// The alive rows are regrouped every few rounds by the constraint they vote for (srt_prep + a hipCUB radix sort
+// + srt_unpack: a buffer then holds only the variable id, target and floor of each row; the elements are read from
+// the CSR).  The filter then reads the target keys of 64 neighbouring rows from a handful of lines (rows of one
+// constraint sit together) instead of 64 random 2-B gathers, and needs no changed-constraint bitmap: a row
+// re-votes when its target's key reached its floor (keys only grow, so an unchanged key is still below it), or
+// — sensitive rows (floor 0) — when its target was touched last round (chg stamp).  Rows that re-voted since the
+// last regroup keep their position (their gathers are random again until the next one).  The row order does not
+// change any result: a vote depends on its own row only, the vote counts are integer atomics.
+template <int R, int F, int kDiag>
+__device__ __forceinline__ int vote_waves_tgt(const Dev& s, int buf, int round, int64_t nrows, int* qw,
+                                              int* st_rows, int* st_elems) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / kWave);
+  const int32_t* __restrict__ rtgt = s.rtgt[buf];
+  const uint16_t* __restrict__ skey = s.skey[buf];
+  const uint16_t* __restrict__ key = s.key;
+  const uint16_t prev = uint16_t(round - 1);
+  const unsigned long long below = (1ull << lane) - 1;
+  int qn = 0, nq = 0;
+  // steps of F * 64 rows, strided over the waves of the grid: the rows of one constraint are neighbours, so
+  // contiguous per-wave shares would leave a constraint's whole re-vote burst to one wave
+  for (int64_t base = wave * (int64_t(F) * kWave); base < nrows; base += nwaves * (int64_t(F) * kWave)) {
+    int tt[F];
+    unsigned sk[F];
+#pragma unroll
+    for (int u = 0; u < F; u++) {
+      const int64_t row = base + u * kWave + lane;
+      tt[u] = row < nrows ? rtgt[row] : kRetired;
+      sk[u] = row < nrows ? unsigned(skey[row]) : 1u;
+    }
+    unsigned kt[F], cg[F];
+#pragma unroll
+    for (int u = 0; u < F; u++) {  // target key (floored rows) / change stamp (sensitive rows), together
+      kt[u] = tt[u] >= 0 && sk[u] != 0 ? unsigned(key[tt[u]]) : 0u;
+      cg[u] = tt[u] >= 0 && sk[u] == 0 ? unsigned(s.chg[tt[u]]) : 0x10000u;
+    }
+    unsigned needm = 0;
+#pragma unroll
+    for (int u = 0; u < F; u++) {
+      const bool need = tt[u] == kUnvoted || (tt[u] >= 0 && (sk[u] == 0 ? cg[u] == prev : kt[u] >= sk[u]));
+      needm |= unsigned(need) << u;
+    }
+#pragma unroll 1
+    for (int u = 0; u < F; u++) {
+      const bool need = (needm >> u) & 1;
+      const unsigned long long m = __ballot(need);
+      if (need)
+        qw[qn + __popcll(m & below)] = int(base + u * kWave + lane);
+      qn += __popcll(m);
+      if (qn >= kWave) {  // wave-uniform: resolve the newest 64
+        __builtin_amdgcn_wave_barrier();
+        qn -= kWave;
+        nq += kWave;
+        const int row = qw[qn + lane];
+        __builtin_amdgcn_wave_barrier();
+        if (kDiag == 0)
+          vote_row<R, true>(s, buf, round, row, st_rows, st_elems, key);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (kDiag == 0 && lane < qn)
+    vote_row<R, true>(s, buf, round, qw[lane], st_rows, st_elems, key);
+  return nq + qn;
+}
+
+// kDiag 1 (measurement only, LMMHIP_VOTE_DIAG): the filter alone, rows queued but not resolved.
+template <int B, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_tgt(Dev s, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int buf = s.ctl[CTL_BUF];
+  __shared__ int st_rows, st_elems;
+  __shared__ int q[(B / kWave) * kQW];  // per-wave queues of rows to re-vote
+  if (s.vstat) {
+    if (threadIdx.x == 0)
+      st_rows = st_elems = 0;
+    __syncthreads();
+  }
+  vote_waves_tgt<8, kFilt, kDiag>(s, buf, round, s.ctl[CTL_NROWS + buf], q + (threadIdx.x / kWave) * kQW, &st_rows,
+                                  &st_elems);
+  if (s.vstat && kDiag == 0) {
+    __syncthreads();
+    if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
+      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x)] = st_rows;
+      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x) + 1] = st_elems;
+    }
+  }
+}
+
+// Regroup, step 1: the rows of the buffer in use as (key, value) pairs — key = (target + 1) / 16 (16 constraints'
+// keys share a line), value = variable id | floor << 32 | the target's low bits << 48; dropped rows (retired, or
+// whose variable a saturation fixed: its target died) get `dead` and sort to the end.  nh = the host's upper bound
+// of the buffer's rows (the sort's length); the alive count goes to CTL_SORTN.
+__global__ void __launch_bounds__(kBlock) srt_prep(Dev s, int64_t nh, uint32_t dead) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int in = s.ctl[CTL_BUF];
+  const int64_t n = s.ctl[CTL_NROWS + in];
+  int cnt = 0;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nh; i += int64_t(gridDim.x) * kBlock) {
+    uint32_t k = dead;
+    unsigned long long val = 0;
+    if (i < n) {
+      const int t = s.rtgt[in][i];
+      const int32_t cv = s.cvar[in][i];
+      // a variable is fixed only with its target (the saturated constraint every alive element of it votes
+      // for) or at its bound (retired by its re-vote)
+      bool alive = t != kRetired;
+      if (t >= 0 && s.key[t] == kDeadKey)
+        alive = s.vstate[rvar(cv)] == 0;
+      if (alive) {
+        const uint32_t t1 = uint32_t(t + 1);
+        k = t1 >> 4;
+        val = (unsigned long long)uint32_t(cv) | ((unsigned long long)s.skey[in][i] << 32) |
+              ((unsigned long long)(t1 & 15u) << 48);
+        cnt++;
+      }
+    }
+    s.sk_in[i] = k;
+    s.sv_in[i] = val;
+  }
+  cnt = grp_isum<kWave>(cnt);
+  if ((threadIdx.x & (kWave - 1)) == 0 && cnt)
+    atomicAdd(&s.ctl[CTL_SORTN], cnt);
+}
+
+// Regroup, step 3 (after the sort): the sorted alive rows into the other buffer.
+__global__ void __launch_bounds__(kBlock) srt_unpack(Dev s, int64_t nh) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int in = s.ctl[CTL_BUF], out = in == 1 ? 2 : 1;
+  const int64_t n = s.ctl[CTL_SORTN] < nh ? s.ctl[CTL_SORTN] : nh;
+  int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
+  uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const uint32_t k = s.sk_out[i];
+    const unsigned long long val = s.sv_out[i];
+    const int v = rvar(int32_t(uint32_t(val)));
+    orow[i] = s.var_ptr[v];  // the row's CSR range (one gather per regroup instead of one per re-vote)
+    s.rend[out][i] = s.var_ptr[v + 1];
+    ovar[i] = int32_t(uint32_t(val));
+    s.skey[out][i] = uint16_t(val >> 32);
+    s.rtgt[out][i] = int32_t((k << 4) | uint32_t((val >> 48) & 15u)) - 1;
+  }
+}
+
+// Regroup, step 4 (one thread): switch to the regrouped buffer.
+__global__ void srt_flip(Dev s) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int in = s.ctl[CTL_BUF], out = in == 1 ? 2 : 1;
+  s.ctl[CTL_NROWS + out] = s.ctl[CTL_SORTN];
+  s.ctl[CTL_NELEM + out] = 0;  // (elements stay in the CSR)
+  s.ctl[CTL_SORTN] = 0;
+  s.ctl[CTL_BUF] = out;
+}
+
 // Round phase 2 — ready list: alive constraints every alive element votes for.  Block b scans one
 // contiguous chunk of the alive-constraint list and writes its ready constraints into its own segment
 // of `ready` (LDS counter, no global atomic); bready[b] = segment length.
@@ -911,68 +1073,10 @@ __device__ __forceinline__ void sat_flush(const Dev& s, int round, SatLds<NB, CA
   __syncthreads();
 }
 
-// Grid-wide sharing of big ready constraints (persistent engine): a ready constraint of more than `bigch`
-// chunks is posted to `list` (pairs: constraint, first global chunk) with ONE 64-bit atomic on `ctr` (count << 32
-// | chunks: entry order = chunk order); once every workgroup has posted (`posted`), every wave takes chunks
-// from `next` until they run out.  The words are reset by the caller between saturations.
-struct BigSat {
-  int32_t* list;
-  unsigned long long* ctr;
-  unsigned* next;
-  unsigned* posted;
-  int bigch;
-  int32_t* err;
-};
-
-__device__ __forceinline__ void sat_big(const Dev& s, int round, const BigSat& bs, int* pre) {
-  const int lane = threadIdx.x & (kWave - 1);
-  if (threadIdx.x == 0) {  // (the workgroup's posts precede this: sat_block's last barrier)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(bs.posted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (lane == 0) {
-    const long long t0 = wall_clock64();
-    while (ld_rlx(bs.posted) < gridDim.x) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > 400000000ll) {  // 4 s: the protocol broke (grid not co-resident?)
-        st_rlx(bs.err, 1);
-        break;
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const unsigned long long tot = ld_rlx(bs.ctr);
-  const int nb = int(tot >> 32);
-  const unsigned total = unsigned(tot);
-  for (;;) {  // wave-uniform
-    unsigned g = 0;
-    if (lane == 0)
-      g = __hip_atomic_fetch_add(bs.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g = __shfl(g, 0, kWave);
-    if (g >= total)
-      break;
-    int lo = 0, hi = nb - 1;  // last entry whose first chunk is <= g
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) / 2;
-      if (unsigned(ld_rlx(&bs.list[2 * mid + 1])) <= g)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    const int32_t c = ld_rlx(&bs.list[2 * lo]);
-    const unsigned ch = g - unsigned(ld_rlx(&bs.list[2 * lo + 1]));
-    const double r = ld_rlx(&s.cst[c].ratio);
-    saturate_chunk(s, c, r, s.cnst_ptr[c] + ch * kWave, s.cnst_ptr[c + 1], round, lane, pre, s.cdup[c] != 0);
-    if (ch == 0 && lane == 0)
-      s.ctouch[c] = 2;
-  }
-}
-
 // Returns whether the workgroup found a ready constraint.
 template <int NB, int CAP>
 __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t* __restrict__ cl, int64_t n,
-                                          SatLds<NB, CAP>& L, const BigSat* bs = nullptr) {
+                                          SatLds<NB, CAP>& L) {
   static_assert(CAP >= NB, "one pass must fit");
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -985,17 +1089,8 @@ __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t
     int32_t c = -1;
     if (i < n)
       c = cl ? cl[i] : int32_t(i);
-    bool rdy = c >= 0 && s.key[c] != kDeadKey && s.nvote[c] == 0;
-    int nch = rdy ? int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave) : 0;
-    if (bs && nch > bs->bigch) {  // posted to the grid-wide list (sat_big)
-      const unsigned long long o = atomicAdd(bs->ctr, (1ull << 32) | unsigned(nch));
-      const int i = int(o >> 32);
-      bs->list[2 * i] = c;
-      bs->list[2 * i + 1] = int32_t(uint32_t(o));
-      any = true;
-      rdy = false;
-      nch = 0;
-    }
+    const bool rdy = c >= 0 && s.key[c] != kDeadKey && s.nvote[c] == 0;
+    const int nch = rdy ? int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave) : 0;
     int ia = rdy, ib = nch;  // block exclusive scans of (ready, chunks)
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -1034,11 +1129,6 @@ __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t
   }
   if (L.na)
     sat_flush<NB, CAP>(s, round, L);
-  if (bs) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's posts have reached the L2
-    __syncthreads();  // every wave's posts issued before the workgroup signals
-    sat_big(s, round, *bs, L.pre[threadIdx.x / kWave]);
-  }
   return any;
 }
 

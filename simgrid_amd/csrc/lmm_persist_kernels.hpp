@@ -40,10 +40,7 @@ enum : int {
   BAR_FLAT = 416,   // launch rendezvous
   BAR_ALLOC = 432,  // u64 (2 words, 8-B aligned): compaction allocator (rows << 32 | elements)
   BAR_PALIVE = 448,  // [2 parities x 16]: constraints alive after a round's update, 8 partial words each
-  BAR_BIG = 480,     // u64: big ready constraints posted this round (count << 32 | their chunks), sat_block
-  BAR_BIGNEXT = 496,  // next big chunk to take (work sharing across the grid)
-  BAR_POSTED = 512,  // workgroups done posting this round
-  BAR_WORDS = 528
+  BAR_WORDS = 480
 };
 
 __device__ __forceinline__ unsigned xcc_id() {
@@ -194,14 +191,8 @@ __device__ void p_vote(const Dev& s, int buf, int round, int64_t nrows, PVoteLds
 }
 
 // S: ready test fused with saturation over every constraint (identity ids), sat_block (the ready
-// constraints' CSC chunks shared by the workgroup's 16 waves); ready constraints of more than `bigch` chunks
-// (a fat-tree core link) go to the grid-wide list `big` instead, whose chunks every wave of every workgroup
-// takes from one counter once its own ones are done.
-__device__ void p_saturate(const Dev& s, int round, PSatLds& L, const PBar& b, int32_t* big, int bigch) {
-  BigSat bs{big, reinterpret_cast<unsigned long long*>(b.w + BAR_BIG), b.w + BAR_BIGNEXT, b.w + BAR_POSTED, bigch,
-            b.err};
-  sat_block<kPB, 4 * kPB>(s, round, nullptr, s.nC, L, big ? &bs : nullptr);
-}
+// constraints' CSC chunks shared by the workgroup's 16 waves).
+__device__ void p_saturate(const Dev& s, int round, PSatLds& L) { sat_block<kPB, 4 * kPB>(s, round, nullptr, s.nC, L); }
 
 // C: compaction of the alive rows of buffer `in` into `out`, one contiguous chunk of rows per workgroup:
 // pass 1 counts the chunk's alive rows and elements, ONE 64-bit atomic per workgroup allocates both
@@ -300,8 +291,7 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
 
 template <bool kBits, int R>
 __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double prec, int max_rounds,
-                                                  int cmp_every, long long* pt, unsigned pt_cap, int sysf,
-                                                  int32_t* big, int bigch) {
+                                                  int cmp_every, long long* pt, unsigned pt_cap, int sysf) {
   __shared__ PLds<kBits> L;
   PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0, pt, pt_cap, sysf};
   if (pt && blockIdx.x == 0 && threadIdx.x == 0)
@@ -327,14 +317,9 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
         st_rlx(&palive[16 * ((r + 1) & 1) + i], 0);
       st_rlx(alloc, 0ull);
     }
-    p_saturate(s, r, L.sat, b, big, bigch);
+    p_saturate(s, r, L.sat);
     if (!grid_sync(b, ++gen))
       return;
-    if (lead) {  // the big-chunk words of the next saturation (last used before the barrier above)
-      st_rlx(reinterpret_cast<unsigned long long*>(barw + BAR_BIG), 0ull);
-      st_rlx(&barw[BAR_BIGNEXT], 0u);
-      st_rlx(&barw[BAR_POSTED], 0u);
-    }
     if (threadIdx.x == 0)
       L.cnt = 0;
     __syncthreads();

@@ -160,3 +160,16 @@ def test_fb_device_shards_over_gloo():
         dist.destroy_process_group()
     want = oracle_dense_values(o, ovars, f)
     assert x.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("stress", [False, True])
+def test_target_ordered_vote_bit_identical(stress, monkeypatch):
+    """The multi-launch engine's target-ordered rows (LMMHIP_TGT=1: mm_vote_tgt + regroups) and the default
+    bitmap-filter vote over order-preserving compactions give the same bytes: the row order
+    changes no vote.  1e5 x 1e6 x 8 (the C2/10 system: 25+ regroups)."""
+    out = []
+    for tgt in ("1", "0"):
+        monkeypatch.setenv("LMMHIP_TGT", tgt)
+        out.append(_values(_synthetic(100000, 1000000, 1, stress), L.System.ENGINE_ROUNDS))
+    assert out[0][1] == out[1][1]
+    assert out[0][0].tobytes() == out[1][0].tobytes(), float(np.max(np.abs(out[0][0] - out[1][0])))

@@ -13,7 +13,7 @@ import subprocess
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "simgrid_amd", "csrc")
 HOT = ("mm_persist", "mm_vote_lane", "mm_vote", "mm_ready", "mm_saturate", "mm_update", "mm_batch_lds",
-       "mm_init_cnsts", "cmp_write")
+       "mm_init_cnsts", "cmp_write", "fbk_", "fb_var_inc", "srt_")
 
 
 def resource_report():
@@ -28,7 +28,7 @@ def resource_report():
             cur = m.group(1)
             kernels[cur] = {}
             continue
-        m = re.search(r"remark: (VGPRs Spill|ScratchSize \[bytes/lane\]|VGPRs): (\d+)", line)
+        m = re.search(r"remark:\s+(VGPRs Spill|ScratchSize \[bytes/lane\]|VGPRs): (\d+)", line)
         if m and cur:
             kernels[cur][m.group(1)] = int(m.group(2))
     return kernels
@@ -38,5 +38,7 @@ def test_hot_kernels_do_not_spill():
     kernels = resource_report()
     hot = {k: v for k, v in kernels.items() if any(h in k for h in HOT)}
     assert any("mm_persist" in k for k in hot) and any("mm_saturate" in k for k in hot), sorted(kernels)
+    # the report was parsed (a format change must not make this test pass vacuously)
+    assert all("VGPRs" in v and "VGPRs Spill" in v for v in hot.values()), hot
     bad = {k: v for k, v in hot.items() if v.get("VGPRs Spill", 0) or v.get("ScratchSize [bytes/lane]", 0)}
     assert not bad, bad
