@@ -374,41 +374,13 @@ __device__ __forceinline__ double fb_fat_update(const Dev& s, int64_t c, double 
 // at every step.
 constexpr int kSeqP = 8;  // 64-element blocks per batch
 
-// Lane 0: the n increments of one batch (d, in LDS; slots past n hold 0.0) chained into rem.
+// Lane 0: the n increments of one batch (d, in LDS) chained into rem, one double_update per element — the
+// reference's loop; a batch of non-negative increments takes the clamp once at its end (same value, see above).
+// (The wave-parallel fb_chain_scan below takes non-negative batches; this loop is its fallback.)
 __device__ __forceinline__ double fb_chain_batch(const double* d, int n, double rem, double prec, bool nonneg) {
   if (nonneg) {
-    // kG increments per step, the next kG read from LDS while these are chained (slots past n hold 0.0:
-    // r - 0 == r); two register sets used in turn, so nothing is copied between steps
-    constexpr int kG = 32, kH = kG / 2;
-    const double2* dd = reinterpret_cast<const double2*>(d);
-    double2 ra[kH], rb[kH];
-#pragma unroll
-    for (int t = 0; t < kH; t++)
-      ra[t] = dd[t];
-    for (int k = 0; k < n; k += 2 * kG) {
-      if (k + kG < n) {
-#pragma unroll
-        for (int t = 0; t < kH; t++)
-          rb[t] = dd[(k + kG) / 2 + t];
-      }
-#pragma unroll
-      for (int t = 0; t < kH; t++) {
-        rem -= ra[t].x;
-        rem -= ra[t].y;
-      }
-      if (k + kG >= n)
-        break;
-      if (k + 2 * kG < n) {
-#pragma unroll
-        for (int t = 0; t < kH; t++)
-          ra[t] = dd[(k + 2 * kG) / 2 + t];
-      }
-#pragma unroll
-      for (int t = 0; t < kH; t++) {
-        rem -= rb[t].x;
-        rem -= rb[t].y;
-      }
-    }
+    for (int k = 0; k < n; k++)
+      rem -= d[k];
     if (rem < prec)
       rem = 0.0;
   } else {
@@ -421,33 +393,147 @@ __device__ __forceinline__ double fb_chain_batch(const double* d, int n, double 
   return rem;
 }
 
+// The same non-negative batch chained by the whole wave, exactly.  While the running value x stays in one
+// binade [2^e, 2^(e+1)) its grid is u = 2^(e-52) and x is a multiple of u, so fl(x - d) = x - u * rint(d / u)
+// unless d / u is a tie (xx.5: the result's parity would decide) or the result leaves the binade: the chain is
+// then x - u * (a prefix sum of integers), and the wave finds the first step that leaves the binade (prefix >= M
+// = (x - 2^e) / u: the result could round onto the coarser grid below) or is a tie with one int64 scan, takes
+// that step as the fp64 subtraction it is, and goes on from there.  Once x < prec the clamped chain is 0 (the
+// values only decrease).  Identical, bit for bit, to lane 0's sequential loop; after kScanExits such steps in a
+// batch (the value falls through binades element by element near the end of a saturating chain) the rest goes
+// back to that loop: *k = the first increment not yet applied.  Needs prec > 0 and every d >= 0.
+constexpr int kScanExits = 12;
+__device__ __forceinline__ double fb_chain_scan(const double* d, int n, double x, double prec, int lane, int* k_out) {
+  constexpr int kPer = kSeqP;  // increments per lane: lane l holds [l * kPer, (l + 1) * kPer)
+  double dv[kPer];
+  const double2* d2 = reinterpret_cast<const double2*>(d + lane * kPer);
+#pragma unroll
+  for (int t = 0; t < kPer / 2; t++) {
+    const double2 v = d2[t];
+    dv[2 * t] = v.x;
+    dv[2 * t + 1] = v.y;
+  }
+  int k = 0, exits = 0;
+  while (k < n) {  // wave-uniform (x, k identical on every lane)
+    if (!(x >= prec)) {  // every later value is below the precision too: the clamped chain is 0
+      k = n;
+      x = 0.0;
+      break;
+    }
+    if (x < 0x1p-1022 || exits >= kScanExits)  // subnormal grid / many binade steps: lane 0's loop
+      break;
+    const int e = __builtin_amdgcn_frexp_exp(x) - 1;  // x in [2^e, 2^(e+1))
+    const long long M = (long long)(__builtin_amdgcn_ldexp(x, 52 - e) - 0x1p52);  // (x - 2^e) / u, exact
+    long long run = 0, incl[kPer];
+    bool tie[kPer];
+#pragma unroll
+    for (int t = 0; t < kPer; t++) {
+      const int j = lane * kPer + t;
+      long long q = 0;
+      tie[t] = false;
+      if (j >= k && j < n) {
+        const double sc = __builtin_amdgcn_ldexp(dv[t], 52 - e);  // d / u, exact
+        if (!(sc < 0x1p52)) {
+          q = 1ll << 52;  // > M: leaves the binade
+        } else {
+          const double f = __builtin_floor(sc), fr = sc - f;
+          tie[t] = fr == 0.5;
+          q = (long long)f + (fr > 0.5 ? 1 : 0);
+        }
+      }
+      run += q;
+      incl[t] = run;
+    }
+    long long ex = run;  // exclusive wave scan of the lane totals
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const long long y = __shfl_up(ex, o, kWave);
+      if (lane >= o)
+        ex += y;
+    }
+    ex -= run;
+    int first = -1;
+    long long before = 0;
+#pragma unroll
+    for (int t = kPer - 1; t >= 0; t--) {  // this lane's first step that must be taken in fp64
+      const int j = lane * kPer + t;
+      if (j >= k && j < n && (tie[t] || ex + incl[t] >= M)) {
+        first = j;
+        before = ex + (t ? incl[t - 1] : 0);
+      }
+    }
+    const unsigned long long m = __ballot(first >= 0);
+    const double u = __builtin_amdgcn_ldexp(1.0, e - 52);
+    if (!m) {  // the whole rest stays in the binade
+      const long long tot = __shfl(ex + run, kWave - 1, kWave);
+      x -= double(tot) * u;  // exact: a multiple of u in [2^e + u, 2^(e+1))
+      k = n;
+      break;
+    }
+    const int src = __ffsll((long long)m) - 1;
+    const int js = __shfl(first, src, kWave);
+    const long long pb = __shfl(before, src, kWave);
+    x -= double(pb) * u;  // exact (pb < M)
+    x -= d[js];           // the step itself, as the sequential loop takes it
+    k = js + 1;
+    exits++;
+  }
+  if (k >= n && x < prec)  // the batch's end clamp
+    x = 0.0;
+  *k_out = k;
+  return x;
+}
+
+// One batch of the chain (d: this wave's LDS slots; the result is on every lane).
+__device__ __forceinline__ double fb_chain_step(const double* d, int n, double rem, double prec, bool nonneg,
+                                                int lane) {
+  int k = 0;
+  if (nonneg && prec > 0.0)
+    rem = fb_chain_scan(d, n, rem, prec, lane, &k);
+  // (after a partial scan: one clamp per step — the same value for non-negative increments, and it reads exactly
+  // the n - k slots left, where the batched loop reads whole groups from an aligned start)
+  if (k < n && lane == 0)
+    rem = fb_chain_batch(d + k, n - k, rem, prec, nonneg && k == 0);
+  rem = __shfl(rem, 0, kWave);
+  __builtin_amdgcn_wave_barrier();
+  return rem;
+}
+
+// The increments stream in kChainD batches ahead of the chain (kChainD x kSeqP doubles per lane in flight): with
+// the batch itself chained wave-parallel (fb_chain_scan), the memory latency per batch is what is left to hide.
+constexpr int kChainD = 4;
 __device__ __forceinline__ double fb_chain(const double* __restrict__ fbd, uint32_t cb, uint32_t ce, double rem,
                                            double prec, double* d, int lane) {
-  double nx[kSeqP];
+  constexpr uint32_t kB = kSeqP * kWave;
+  double nx[kChainD][kSeqP];
 #pragma unroll
-  for (int p = 0; p < kSeqP; p++) {
-    const uint32_t j = cb + p * kWave + lane;
-    nx[p] = j < ce ? fbd[j] : 0.0;
-  }
-  for (uint32_t base = cb; base < ce; base += kSeqP * kWave) {  // wave-uniform
-    bool nonneg = true;
+  for (int t = 0; t < kChainD; t++)
 #pragma unroll
     for (int p = 0; p < kSeqP; p++) {
-      d[p * kWave + lane] = nx[p];
-      nonneg &= nx[p] >= 0.0;
+      const uint32_t j = cb + t * kB + p * kWave + lane;
+      nx[t][p] = j < ce ? fbd[j] : 0.0;
     }
-    nonneg = __all(nonneg);
-    const uint32_t nb = base + kSeqP * kWave;
+  for (uint32_t base = cb; base < ce; base += kChainD * kB) {  // wave-uniform
 #pragma unroll
-    for (int p = 0; p < kSeqP; p++) {  // the next batch's loads, in flight during the chain
-      const uint32_t j = nb + p * kWave + lane;
-      nx[p] = j < ce ? fbd[j] : 0.0;
+    for (int t = 0; t < kChainD; t++) {
+      const uint32_t b0 = base + t * kB;
+      if (b0 >= ce)  // wave-uniform
+        break;
+      bool nonneg = true;
+#pragma unroll
+      for (int p = 0; p < kSeqP; p++) {
+        d[p * kWave + lane] = nx[t][p];
+        nonneg &= nx[t][p] >= 0.0;
+      }
+      nonneg = __all(nonneg);
+#pragma unroll
+      for (int p = 0; p < kSeqP; p++) {  // the batch kChainD ahead
+        const uint32_t j = b0 + kChainD * kB + p * kWave + lane;
+        nx[t][p] = j < ce ? fbd[j] : 0.0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      rem = fb_chain_step(d, int(ce - b0 < kB ? ce - b0 : kB), rem, prec, nonneg, lane);
     }
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0)
-      rem = fb_chain_batch(d, int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave)), rem,
-                           prec, nonneg);
-    __builtin_amdgcn_wave_barrier();
   }
   return rem;
 }
@@ -495,10 +581,8 @@ __device__ __forceinline__ double fb_chain_pull(const Dev& s, uint32_t cb, uint3
       ix[p] = j < ce ? s.csc_v[j] : -1;
     }
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0)
-      rem = fb_chain_batch(d, int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave)), rem,
-                           prec, nonneg);
-    __builtin_amdgcn_wave_barrier();
+    rem = fb_chain_step(d, int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave)), rem, prec,
+                        nonneg, lane);
   }
   return rem;
 }

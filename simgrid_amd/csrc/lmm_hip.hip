@@ -1498,7 +1498,9 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
 static int solve_fair(lmmhip_ctx* c, double prec) {
   c->fb_shard = false;
   // shared constraints of at least this many elements get their increments precomputed element-parallel
-  // (fbk_acc) for their critical-path chains; shorter ones compute them inside the chain (fb_chain_pull)
+  // (fbk_acc) and streamed into their chains (fb_chain); shorter ones compute them inside the chain
+  // (fb_chain_pull).  Pulling in round 0 and streaming fbk_acc's listed-variable rewrites afterwards measured
+  // 3 % slower on C5 (9.68 vs 9.42 ms, same box): the increments' gathers move, they do not go away.
   c->fb_longmin = uint32_t(std::max(0, env_int("LMMHIP_FB_LONG", 16384)));
   if (c->fbd_cap < c->d.nnz) {  // increments in CSC order (fbk_acc -> fbk_update_seq)
     if (int rc = dalloc(c, &c->d.fbd, c->d.nnz))
