@@ -10,7 +10,6 @@
 
 #include "../include/lmm/lmm_system.h"
 #include "../simgrid_amd/csrc/lmm_generators.hpp"
-#include "../simgrid_amd/csrc/lmm_platforms.hpp"
 #include "lmm_oracle.hpp"
 
 using namespace lmm_oracle;
@@ -191,33 +190,37 @@ long long oracle_gen_synthetic(void* s, long long nb_cnst, long long nb_var, int
   return nb_var;
 }
 
-// Cluster platform + flows, same generator as the product's lmm_gen_platform_flows.
-int oracle_platform_size(const lmm_platform_params* p, long long* n_links, long long* n_hosts) {
-  try {
-    std::unique_ptr<lmm_plat::Platform> plat(lmm_plat::make_platform(lmm_plat::params_from(*p)));
-    *n_links = (long long)plat->links.size();
-    *n_hosts = plat->n_hosts;
-    return 0;
-  } catch (const std::exception&) {
-    return -1;
-  }
-}
-long long oracle_gen_platform_flows(void* s, const lmm_platform_params* p, void** cnst_out, void** var_out) {
-  try {
-    const lmm_plat::Params prm = lmm_plat::params_from(*p);
-    std::unique_ptr<lmm_plat::Platform> plat(lmm_plat::make_platform(prm));
-    Builder b{S(s)};
-    std::vector<Constraint*> cs;
-    std::vector<Variable*> vs;
-    lmm_plat::flows(b, *plat, prm, &cs, var_out ? &vs : nullptr);
+// Cluster platform + flows: the system oracle/platforms.py restates from the reference's zones
+// and models, replayed as its API calls — constraint_new (+ unshare for FATPIPE) per constraint, then per flow
+// variable_new(penalty, bound, number of constraints) and its elements in call order, expand_add where eadd is
+// set, expand otherwise.  No generator logic here: it is independent of the product's lmm_platforms.hpp.
+long long oracle_build_flows(void* s, long long nc, const double* cbound, const unsigned char* cfat, long long nv,
+                             const double* vpen, const double* vbound, const int* vn, const long long* eptr,
+                             const int* ecnst, const double* ew, const unsigned char* eadd, void** cnst_out,
+                             void** var_out) {
+  Builder b{S(s)};
+  std::vector<Constraint*> cs(static_cast<size_t>(nc));
+  for (long long i = 0; i < nc; i++) {
+    cs[size_t(i)] = b.constraint_new(cbound[i]);
+    if (cfat[i])
+      b.unshare(cs[size_t(i)]);
     if (cnst_out)
-      std::memcpy(cnst_out, cs.data(), cs.size() * sizeof(void*));
-    if (var_out)
-      std::memcpy(var_out, vs.data(), vs.size() * sizeof(void*));
-    return prm.n_flows;
-  } catch (const std::exception&) {
-    return -1;
+      cnst_out[i] = cs[size_t(i)];
   }
+  for (long long f = 0; f < nv; f++) {
+    Variable* v = b.variable_new(vpen[f], vbound[f], vn[f]);
+    for (long long e = eptr[f]; e < eptr[f + 1]; e++) {
+      if (ecnst[e] < 0 || ecnst[e] >= nc)
+        return -1;
+      if (eadd[e])
+        b.expand_add(cs[size_t(ecnst[e])], v, ew[e]);
+      else
+        b.expand(cs[size_t(ecnst[e])], v, ew[e]);
+    }
+    if (var_out)
+      var_out[f] = v;
+  }
+  return nv;
 }
 
 }  // extern "C"

@@ -22,19 +22,29 @@ SHARED, SPLITDUPLEX, FATPIPE = 0, 1, 2
 CM02, LV08, L07 = 0, 1, 2
 
 
-class PlatformParams(ct.Structure):
-    """lmm_platform_params (include/lmm/lmm_system.h)."""
-    _fields_ = [("topology", I), ("topo_parameters", ct.c_char_p), ("bw", D), ("lat", D), ("policy", I),
-                ("loopback_bw", D), ("loopback_lat", D), ("limiter_bw", D), ("speed", D), ("model", I),
-                ("crosstraffic", I), ("n_flows", LL), ("seed", ct.c_ulonglong), ("size_min", D), ("size_max", D),
-                ("tcp_gamma", D)]
-
-
 def platform_params(topology=FAT_TREE, topo_parameters="", bw=1.25e8, lat=5e-5, policy=SPLITDUPLEX, loopback_bw=0.0,
                     loopback_lat=0.0, limiter_bw=0.0, speed=1e9, model=LV08, crosstraffic=True, n_flows=1000,
                     seed=1, size_min=1e6, size_max=1e9, tcp_gamma=4194304.0):
-    return PlatformParams(topology, topo_parameters.encode(), bw, lat, policy, loopback_bw, loopback_lat, limiter_bw,
-                          speed, model, int(crosstraffic), n_flows, seed, size_min, size_max, tcp_gamma)
+    """The parameters of a generated platform (the fields of lmm_platform_params, include/lmm/lmm_system.h),
+    for oracle/platforms.py."""
+    if policy not in (SHARED, SPLITDUPLEX, FATPIPE):
+        raise ValueError(f"unknown sharing policy {policy}")
+    if n_flows < 0:
+        raise ValueError("negative flow count")
+    return dict(topology=topology, topo_parameters=topo_parameters, bw=bw, lat=lat, policy=policy,
+                loopback_bw=loopback_bw, loopback_lat=loopback_lat, limiter_bw=limiter_bw, speed=speed, model=model,
+                crosstraffic=bool(crosstraffic), n_flows=int(n_flows), seed=int(seed), size_min=size_min,
+                size_max=size_max, tcp_gamma=tcp_gamma)
+
+
+def params_dict(p):
+    return dict(p)
+
+
+def platform_size(p):
+    """(links, hosts) of platform p (oracle/platforms.py)."""
+    from oracle import platforms as PL
+    return PL.platform_size(p)
 
 
 _SIGS = {
@@ -81,8 +91,9 @@ _SIGS = {
     "oracle_update_constraint_bound": (None, [P, P, D]),
     "oracle_gen_maxmin_bench": (I, [P, I, I, ct.POINTER(P), ct.POINTER(P), ct.POINTER(I), ct.POINTER(I)]),
     "oracle_gen_synthetic": (LL, [P, LL, LL, I, ct.c_ulonglong, I, I, I, I, ct.POINTER(P)]),
-    "oracle_platform_size": (I, [ct.POINTER(PlatformParams), ct.POINTER(LL), ct.POINTER(LL)]),
-    "oracle_gen_platform_flows": (LL, [P, ct.POINTER(PlatformParams), ct.POINTER(P), ct.POINTER(P)]),
+    "oracle_build_flows": (LL, [P, LL, ct.POINTER(D), ct.POINTER(ct.c_ubyte), LL, ct.POINTER(D), ct.POINTER(D),
+                                ct.POINTER(ct.c_int), ct.POINTER(LL), ct.POINTER(ct.c_int), ct.POINTER(D),
+                                ct.POINTER(ct.c_ubyte), ct.POINTER(P), ct.POINTER(P)]),
 }
 
 
@@ -287,14 +298,24 @@ class System:
         return vs
 
     def gen_platform_flows(self, p):
-        """Links (+ L07 CPUs) and p.n_flows flows: (constraint list, variable handle array)."""
-        nl, nh = LL(), LL()
-        if lib().oracle_platform_size(ct.byref(p), ct.byref(nl), ct.byref(nh)) != 0:
-            raise ValueError("bad platform parameters")
-        nc = nl.value + (nh.value if p.model == L07 else 0)
-        cs, vs = (P * nc)(), (P * p.n_flows)()
-        if lib().oracle_gen_platform_flows(self.h, ct.byref(p), cs, vs) < 0:
-            raise ValueError("bad platform parameters")
+        """Links (+ L07 CPUs) and p.n_flows flows built by oracle/platforms.py, the oracle's own restatement of
+        the reference's zones and flow models: (constraint list, variable handle array)."""
+        import numpy as np
+
+        from oracle import platforms as PL
+        ops = PL.flow_ops(params_dict(p))
+        nc, nv = len(ops["cbound"]), len(ops["vpen"])
+        cs, vs = (P * nc)(), (P * nv)()
+
+        def ptr(a, t):
+            return np.ascontiguousarray(a).ctypes.data_as(ct.POINTER(t))
+        keep = [np.ascontiguousarray(ops[k]) for k in ("cbound", "cfat", "vpen", "vbound", "vn", "eptr", "ecnst",
+                                                        "ew", "eadd")]
+        rc = lib().oracle_build_flows(self.h, nc, ptr(keep[0], D), ptr(keep[1], ct.c_ubyte), nv, ptr(keep[2], D),
+                                      ptr(keep[3], D), ptr(keep[4], ct.c_int), ptr(keep[5], LL),
+                                      ptr(keep[6], ct.c_int), ptr(keep[7], D), ptr(keep[8], ct.c_ubyte), cs, vs)
+        if rc < 0:
+            raise ValueError("bad flow element")
         return [Constraint(self, cs[i]) for i in range(nc)], vs
 
     def values_of(self, handles, n):

@@ -3,9 +3,11 @@
 The reference's tesh files print no fat-tree / dragonfly route, so routing parity with the reference is
 unpinned: routes are checked here against an independent Python restatement of the hop structure
 FatTreeZone.cpp:62-129 / DragonflyZone.cpp:238-336 produce (route lengths per host pair, latencies,
-LV08 penalties and TCP-gamma bounds), and the product and the oracle are checked to build identical
-systems from the same generator call.  Their solves are compared on the GPU
-(tests/test_gpu_platforms.py).
+LV08 penalties and TCP-gamma bounds), and the product's generator (simgrid_amd/csrc/lmm_platforms.hpp) is
+checked to build exactly the system the oracle's own restatement of the zones and flow models builds
+(oracle/platforms.py, replayed through the oracle's System API; it shares no code with the product).  The
+GPU-vs-oracle solves on these systems (tests/test_gpu_platforms.py, test_gpu_configs.py C4 / C5) therefore
+check the product's generator too.
 """
 import math
 from collections import defaultdict
@@ -158,8 +160,16 @@ def test_crosstraffic_off():
 
 @pytest.mark.parametrize("plat,model,kind", [
     (FAT_TREE, L.LV08, 0), (FAT_TREE, L.CM02, 0), (FAT_TREE, L.L07, 1),
-    (DRAGONFLY, L.LV08, 0), (DRAGONFLY, L.L07, 1),
+    (DRAGONFLY, L.LV08, 0), (DRAGONFLY, L.L07, 1), (DRAGONFLY, L.CM02, 0),
     (dict(topology=L.DRAGONFLY, topo_parameters="2,1;2,2;3,1;2", policy=L.SHARED), L.LV08, 0),
+    (dict(topology=L.DRAGONFLY, topo_parameters="3,4;4,3;5,1;2", policy=L.FATPIPE), L.L07, 1),
+    # three levels, switch limiters on the routes, no back route
+    (dict(topology=L.FAT_TREE, topo_parameters="3;4,4,4;1,4,2;1,1,2", limiter_bw=1e8), L.LV08, 0),
+    (dict(topology=L.FAT_TREE, topo_parameters="3;4,4,4;1,4,2;1,1,2", limiter_bw=1e8, crosstraffic=False),
+     L.CM02, 0),
+    # the C4 / C5 platforms of bench.py (fewer flows)
+    (dict(topology=L.FAT_TREE, topo_parameters="3;16,16,16;1,16,16;1,1,1", loopback_bw=1e9), L.LV08, 0),
+    (dict(topology=L.DRAGONFLY, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8), L.L07, 1),
 ])
 def test_product_and_oracle_build_the_same_system(plat, model, kind):
     ps, os_ = L.System(False, kind), O.System(False, kind)
@@ -171,3 +181,15 @@ def test_product_and_oracle_build_the_same_system(plat, model, kind):
                    {i: O.Variable(os_, ov[i]) for i in range(len(pv))})
     for i in range(len(pv)):
         assert L.Variable(ps, int(pv[i])).get_bound() == O.Variable(os_, ov[i]).get_bound()
+        assert L.Variable(ps, int(pv[i])).get_penalty() == O.Variable(os_, ov[i]).get_penalty()
+
+
+@pytest.mark.parametrize("kw", [
+    dict(topology=L.FAT_TREE, topo_parameters="2;4;1,2;1,2"),
+    dict(topology=L.DRAGONFLY, topo_parameters="3;4,3;5,1;2"),
+    dict(topology=7, topo_parameters="2;4,4;1,2;1,2"),
+    dict(topology=L.FAT_TREE, topo_parameters="2;4,4;1,2;1,2", loopback_bw=1e8, limiter_bw=1e8),
+])
+def test_oracle_restatement_rejects_bad_parameters(kw):
+    with pytest.raises(ValueError):
+        O.System(False).gen_platform_flows(O.platform_params(**kw))
