@@ -1514,22 +1514,35 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   // The reference's rounds are not bounded by the system size (FATPIPE remaining can shrink
   // geometrically: millions of rounds on 60-variable systems); give up past this budget.
   const int64_t max_rounds = 64 * (int64_t(c->d.nV) + int64_t(c->d.nC)) + 4096;
-  int chunk = 4;
+  // One round queued ahead of the termination poll: after round r the control words go to a pinned slot
+  // (mm_ctl_out), round r + 1 is queued, then the host waits for round r's words.  A FairBottleneck round is
+  // long (C5: 0.2-3 ms), so the GPU never waits on the host and at most one empty round (its launches return
+  // at once) runs after the last one; chunks of 4, 8, ... rounds left up to 7 empty rounds (63 launches,
+  // ~0.2 ms on C5) plus a host round trip between chunks.
+  int slot = 0;
+  bool pending = false;
+  int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
+  int32_t* hcd[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; k++)
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
   for (;;) {
-    for (int k = 0; k < chunk; k++)
-      for (int ph = 0; ph < 3; ph++)
-        if (int rc = fb_phase(c, ph))
-          return rc;
-    if (int rc = poll_ctl(c))
-      return rc;
-    if (c->h_ctl[CTL_DONE])
-      break;
+    for (int ph = 0; ph < 3; ph++)
+      if (int rc = fb_phase(c, ph))
+        return rc;
+    const Dev& d = c->d;
+    LAUNCH(6, c->fb_round, mm_ctl_out, 1, kWave, d, hcd[slot]);
+    HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
+    if (pending) {
+      HIPCHK(hipEventSynchronize(c->ev_poll[slot ^ 1]));
+      if (hc[slot ^ 1][CTL_DONE])
+        break;
+    }
+    pending = true;
+    slot ^= 1;
     if (c->fb_round > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "fair-bottleneck round guard tripped");
-    if (chunk < 64)
-      chunk *= 2;
   }
-  return 0;
+  return poll_ctl(c);  // (the queued round has run: final words for the stats)
 }
 
 int lmmhip_ctx_set_stream(lmmhip_ctx* c, void* stream) {
