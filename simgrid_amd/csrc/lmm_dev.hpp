@@ -110,6 +110,10 @@ struct Dev {
   const int32_t* csc_v;      // [nnz]
   const double* csc_w;       // [nnz]
   double* csc_u;             // [nnz] w / penalty of each CSC element (recomputed when penalties change)
+  // [nnz] per CSC element, its variable's penalty and CSR row (begin | end << 32): a saturation reads them with
+  // the element, coalesced, instead of gathering them per claimed variable after the claim (mm_elem_usage)
+  double* csc_p;
+  unsigned long long* csc_row;
   const double* pen;         // [nV]
   const double* vbound;      // [nV]
   const double* cbound;      // [nC]

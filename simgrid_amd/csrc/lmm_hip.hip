@@ -305,6 +305,8 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   rc |= dalloc(c, &csc_v, nnz);
   rc |= dalloc(c, &csc_w, nnz);
   rc |= dalloc(c, &d.csc_u, nnz);
+  rc |= dalloc(c, &d.csc_p, nnz);
+  rc |= dalloc(c, &d.csc_row, nnz);
   rc |= dalloc(c, &pen, nV);
   rc |= dalloc(c, &vb, nV);
   rc |= dalloc(c, &cb, nC);
@@ -432,7 +434,7 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
   if (nC > 0)  // constraints with a duplicate (variable, constraint) pair (structure only)
     HIPCHK(hipMemsetAsync(d.cdup, 0, size_t(nC), c->stream));
   if (nnz > 0) {  // per-element usage w / penalty, kept in step with pen (lmmhip_update_vars)
-    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, c->stream, d);
+    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, c->stream, d, 1);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(mm_dup_check, dim3(grid_for(nV, kBlock)), dim3(kBlock), 0, c->stream, d);
     HIPCHK(hipGetLastError());
@@ -576,7 +578,7 @@ int lmmhip_update_vars(lmmhip_ctx* c, const double* penalty, const double* var_b
   if (penalty && c->d.nV)
     HIPCHK(hipMemcpyAsync((void*)c->d.pen, penalty, sizeof(double) * c->d.nV, hipMemcpyHostToDevice, c->stream));
   if (penalty && c->d.nnz) {
-    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(c->d.nnz, kBlock)), dim3(kBlock), 0, c->stream, c->d);
+    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(c->d.nnz, kBlock)), dim3(kBlock), 0, c->stream, c->d, 0);
     HIPCHK(hipGetLastError());
   }
   if (var_bound && c->d.nV)
@@ -797,7 +799,7 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
       RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, nullptr, const_cast<double*>(d.cbound),
                 const_cast<uint8_t*>(d.cflags));
       if ((flags & kResPenalty) && d.nnz > 0)
-        RS_LAUNCH(mm_elem_usage, d.nnz, d);
+        RS_LAUNCH(mm_elem_usage, d.nnz, d, 0);
       HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       c->res_refreshes++;

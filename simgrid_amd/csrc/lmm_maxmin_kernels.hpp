@@ -27,9 +27,17 @@ namespace lmmdev {
 
 // Per-element usage w / penalty of every CSC element (maxmin.cpp:531-533's summand), computed at upload
 // and whenever the penalties change, so the per-solve init streams it instead of gathering pen[v].
-__global__ void __launch_bounds__(kBlock) mm_elem_usage(Dev s) {
-  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz; j += int64_t(gridDim.x) * kBlock)
-    s.csc_u[j] = s.csc_w[j] / s.pen[s.csc_v[j]];
+// Per CSC element: usage w / penalty and the penalty (with every penalty change), and — rows = 1, with every
+// structure change — its variable's CSR row.
+__global__ void __launch_bounds__(kBlock) mm_elem_usage(Dev s, int rows) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz; j += int64_t(gridDim.x) * kBlock) {
+    const int32_t v = s.csc_v[j];
+    const double p = s.pen[v];
+    s.csc_u[j] = s.csc_w[j] / p;
+    s.csc_p[j] = p;
+    if (rows)
+      s.csc_row[j] = (unsigned long long)s.var_ptr[v] | ((unsigned long long)s.var_ptr[v + 1] << 32);
+  }
 }
 
 // cdup (zeroed before): constraints holding two elements of one variable; every constraint of a row longer
@@ -943,9 +951,13 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
   double lp = 1.0, lx = 0.0;
   uint32_t rb = 0, re = 0;
   if (j < ce) {
-    // (penalty and row are read for claimed variables only: issuing them with the state costs C2 more
-    // random reads than the round trip it saves)
+    // the variable's penalty and CSR row come with the element (coalesced, csc_p / csc_row): no gather after
+    // the claim (round 3; gathering them there cost C2 one more dependent random read per fixed variable)
     lv = s.csc_v[j];
+    lp = s.csc_p[j];
+    const unsigned long long row = s.csc_row[j];
+    rb = uint32_t(row);
+    re = uint32_t(row >> 32);
     if (s.vstate[lv] != 0)
       lv = -1;
     else if (!dup)
@@ -955,12 +967,11 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
   }
   int len = 0;
   if (lv >= 0) {
-    lp = s.pen[lv];
-    rb = s.var_ptr[lv];
-    re = s.var_ptr[lv + 1];
     lx = r / lp;
     s.x[lv] = lx;
     len = int(re - rb);
+  } else {
+    rb = re = 0;
   }
   int incl = len;  // inclusive wave scan of the row lengths
 #pragma unroll
