@@ -166,6 +166,7 @@ struct Dev {
   int32_t* xnb;              // [nC+1] listed count per constraint (+ any-listed flag); sharded: all-reduce SUM
   double* xmin;              // [nC] one context: min of w*mu per FATPIPE constraint
   double* fbd;               // [nnz] one context: w*mu of every shared constraint's element, CSC order
+  int32_t* fb_long;          // [nC+1] one context: count, then the long shared constraints (fb_long_list)
   // multi-launch maxmin, target-ordered rows (mm_vote_tgt): regroup scratch — sort keys (the
   // voted constraint / 16) and packed values (variable id, floor, low target bits), radix-sorted by hipCUB
   uint32_t* sk_in;

@@ -587,31 +587,222 @@ __device__ __forceinline__ double fb_chain_pull(const Dev& s, uint32_t cb, uint3
   return rem;
 }
 
-// :107-140 for ONE context: one wave per listed constraint, shared ones through fb_chain over fbd (written by
-// fbk_acc) when they hold `longmin` elements or more, fb_chain_pull otherwise; FATPIPE ones from the chunk
-// minima (fbk_accc); remaining <= 0 erases the constraint (:129).
+// Long shared constraints (>= longmin elements, C5's global dragonfly links with up to 1.6e5): their chains
+// are the round's critical path, so each gets a whole workgroup (`fb_long_chain`) instead of one wave:
+// fb_chain_scan's argument over steps of kBlock x 8 = 2048 increments, the int64 prefix a block-wide scan.
+// The list (fb_long[0] = count, then the constraint ids) is built once per solve by fb_long_list.
+__global__ void __launch_bounds__(kBlock) fb_long_list(Dev s, uint32_t longmin) {
+  for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < s.nC; c += int64_t(gridDim.x) * kBlock)
+    if (!(s.cflags[c] & 1) && s.cnst_ptr[c + 1] - s.cnst_ptr[c] >= longmin)
+      s.fb_long[1 + atomicAdd(&s.fb_long[0], 1)] = int32_t(c);
+}
+
+constexpr int kLongBlocks = 128;  // workgroups of fbk_update_seq that take the long constraints
+
+// Block-wide (kBlock threads) exclusive scan of an int64 per thread; *tot = the block total.
+__device__ __forceinline__ long long fb_block_scan64(long long v, long long* ws, long long* tot) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  long long incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const long long y = __shfl_up(incl, o, kWave);
+    if (lane >= o)
+      incl += y;
+  }
+  if (lane == kWave - 1)
+    ws[w] = incl;
+  __syncthreads();
+  long long off = 0, t = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / kWave; i++) {
+    off += i < w ? ws[i] : 0;
+    t += ws[i];
+  }
+  __syncthreads();
+  *tot = t;
+  return off + incl - v;
+}
+
+// Block-wide minimum of an int per thread.
+__device__ __forceinline__ int fb_block_min(int v, int* wi) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1)
+    v = min(v, __shfl_xor(v, o, kWave));
+  if (lane == 0)
+    wi[w] = v;
+  __syncthreads();
+  int m = wi[0];
+#pragma unroll
+  for (int i = 1; i < kBlock / kWave; i++)
+    m = min(m, wi[i]);
+  __syncthreads();
+  return m;
+}
+
+// The chain of long shared constraint c by the whole workgroup (sh: kBlock * kSeqP doubles of LDS).  Bit for
+// bit the reference's loop, as fb_chain: non-negative steps are chained by the binade scan (exits and ties as
+// fp64 steps, the end clamp once per step), anything else by thread 0 one double_update at a time.
+__device__ void fb_long_chain(const Dev& s, int32_t c, double prec, double* sh) {
+  __shared__ long long ws[kBlock / kWave];
+  __shared__ int wi[kBlock / kWave];
+  __shared__ double bx[2];
+  constexpr int P = kSeqP;
+  constexpr uint32_t kS = uint32_t(kBlock) * P;
+  const int tid = threadIdx.x;
+  const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
+  double x = s.rem[c];
+  double nx[P];
+#pragma unroll
+  for (int t = 0; t < P; t++) {  // coalesced: element t * kBlock + tid of the step
+    const uint32_t j = cb + t * kBlock + tid;
+    nx[t] = j < ce ? s.fbd[j] : 0.0;
+  }
+  for (uint32_t base = cb; base < ce; base += kS) {  // block-uniform
+    const int n = int(ce - base < kS ? ce - base : kS);
+    bool nonneg = true;
+#pragma unroll
+    for (int t = 0; t < P; t++) {
+      sh[t * kBlock + tid] = nx[t];
+      nonneg &= nx[t] >= 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < P; t++) {  // the next step's increments, in flight during this one
+      const uint32_t j = base + kS + t * kBlock + tid;
+      nx[t] = j < ce ? s.fbd[j] : 0.0;
+    }
+    nonneg = __syncthreads_and(nonneg);  // (also: sh written)
+    double dv[P];
+#pragma unroll
+    for (int t = 0; t < P; t++)
+      dv[t] = sh[tid * P + t];  // this thread's P consecutive increments
+    int k = 0;
+    if (nonneg && prec > 0.0) {
+      int exits = 0;
+      while (k < n) {  // block-uniform
+        if (!(x >= prec)) {
+          k = n;
+          x = 0.0;
+          break;
+        }
+        if (x < 0x1p-1022 || exits >= kScanExits)
+          break;
+        const int e = __builtin_amdgcn_frexp_exp(x) - 1;
+        const long long M = (long long)(__builtin_amdgcn_ldexp(x, 52 - e) - 0x1p52);
+        long long run = 0, incl[P];
+        bool tie[P];
+#pragma unroll
+        for (int t = 0; t < P; t++) {
+          const int j = tid * P + t;
+          long long q = 0;
+          tie[t] = false;
+          if (j >= k && j < n) {
+            const double sc = __builtin_amdgcn_ldexp(dv[t], 52 - e);
+            if (!(sc < 0x1p52)) {
+              q = 1ll << 52;
+            } else {
+              const double f = __builtin_floor(sc), fr = sc - f;
+              tie[t] = fr == 0.5;
+              q = (long long)f + (fr > 0.5 ? 1 : 0);
+            }
+          }
+          run += q;
+          incl[t] = run;
+        }
+        long long tot;
+        const long long ex = fb_block_scan64(run, ws, &tot);
+        int first = INT_MAX;
+#pragma unroll
+        for (int t = P - 1; t >= 0; t--) {
+          const int j = tid * P + t;
+          if (j >= k && j < n && (tie[t] || ex + incl[t] >= M))
+            first = j;
+        }
+        const int js = fb_block_min(first, wi);
+        const double u = __builtin_amdgcn_ldexp(1.0, e - 52);
+        if (js == INT_MAX) {
+          x -= double(tot) * u;  // exact
+          k = n;
+          break;
+        }
+        if (first == js) {  // the owner of the step publishes the prefix before it
+          const int t = js - tid * P;
+          long long pb = ex;
+#pragma unroll
+          for (int i = 0; i < P; i++)
+            if (i < t)
+              pb = ex + incl[i];
+          bx[0] = double(pb);
+        }
+        __syncthreads();
+        x -= bx[0] * u;  // exact (the prefix is below M < 2^52)
+        x -= sh[js];     // the step itself
+        __syncthreads();  // (bx reused)
+        k = js + 1;
+        exits++;
+      }
+      if (k >= n && x < prec)
+        x = 0.0;
+    }
+    if (k < n) {  // thread 0, one double_update at a time (as fb_chain_batch)
+      if (tid == 0)
+        bx[1] = fb_chain_batch(sh + k, n - k, x, prec, nonneg && k == 0);
+      __syncthreads();
+      x = bx[1];
+    }
+    __syncthreads();  // sh is rewritten by the next step
+  }
+  if (tid == 0) {
+    s.erased[c] = 0;
+    s.rem[c] = x;
+    if (x <= 0.0) {
+      s.ratio[c] = dinf();
+      s.erased[c] = 1;
+    }
+  }
+}
+
+// :107-140 for ONE context.  Workgroups [0, kLongBlocks) take the long shared constraints of fb_long, one whole
+// workgroup each (fb_long_chain, from fbk_acc's increments in fbd); the others one wave per listed constraint:
+// shorter shared ones through fb_chain_pull, FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0
+// erases the constraint (:129).
 __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
+  if (blockIdx.x < kLongBlocks) {
+    const int nl = s.fb_long[0];
+    for (int i = blockIdx.x; i < nl; i += kLongBlocks) {  // block-uniform
+      const int32_t c = s.fb_long[1 + i];
+      if (s.ratio[c] != 0.0) {
+        if (threadIdx.x == 0)
+          s.erased[c] = 0;
+        continue;
+      }
+      fb_long_chain(s, c, prec, &dl[0][0]);
+    }
+    return;
+  }
   const int lane = threadIdx.x & (kWave - 1);
   double* d = dl[threadIdx.x / kWave];
-  for (int64_t c = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; c < s.nC;
-       c += int64_t(gridDim.x) * (kBlock / kWave)) {  // wave-uniform
+  for (int64_t c = (int64_t(blockIdx.x - kLongBlocks) * kBlock + threadIdx.x) / kWave; c < s.nC;
+       c += int64_t(gridDim.x - kLongBlocks) * (kBlock / kWave)) {  // wave-uniform
+    const bool fat = s.cflags[c] & 1;
+    const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
+    if (!fat && ce - cb >= longmin)  // a long constraint: its workgroup writes everything
+      continue;
     if (lane == 0)
       s.erased[c] = 0;
     if (s.ratio[c] != 0.0)
       continue;
     double rem = s.rem[c];
-    if (s.cflags[c] & 1) {
+    if (fat) {
       double u;
       rem = fb_fat_update(s, c, rem, s.xmin[c], prec, &u);
       if (lane == 0)
         s.use[c] = u;
     } else {
-      const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
-      rem = ce - cb >= longmin ? fb_chain(s.fbd, cb, ce, rem, prec, d, lane)
-                               : fb_chain_pull(s, cb, ce, rem, prec, d, lane);
+      rem = fb_chain_pull(s, cb, ce, rem, prec, d, lane);
     }
     if (lane == 0) {
       s.rem[c] = rem;

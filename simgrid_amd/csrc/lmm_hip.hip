@@ -144,6 +144,7 @@ struct lmmhip_ctx {
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
   Scr tg_kin, tg_kout, tg_vin, tg_vout, tg_tmp;  // multi-launch engine: regroup of target-ordered rows
+  Scr fb_longl;                                   // solve_fair: the long shared constraints (fb_long_list)
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
@@ -243,7 +244,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch})
@@ -1480,7 +1481,8 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
       break;
     }
     // one context: element by element in the CSC order, bit-identical to the reference
-    LAUNCH(5, r, fbk_update_seq, grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec, c->fb_longmin);
+    LAUNCH(5, r, fbk_update_seq, kLongBlocks + grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec,
+           c->fb_longmin);
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
     c->fb_round++;
     break;
@@ -1509,6 +1511,12 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
       return rc;
     c->fbd_cap = c->d.nnz;
   }
+  if (int rc = scratch(c, c->fb_longl, int64_t(c->d.nC) + 1, &c->d.fb_long))  // the long shared constraints
+    return rc;
+  HIPCHK(hipMemsetAsync(c->d.fb_long, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(fb_long_list, dim3(grid_for(c->d.nC, kBlock)), dim3(kBlock), 0, c->stream, c->d,
+                     c->fb_longmin);
+  HIPCHK(hipGetLastError());
   c->d.xnb = c->xnb_own;
   c->d.xmin = c->xmin_own;
   if (int rc = fb_begin(c, prec))
