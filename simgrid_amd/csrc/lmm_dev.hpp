@@ -167,6 +167,11 @@ struct Dev {
   double* xmin;              // [nC] one context: min of w*mu per FATPIPE constraint
   double* fbd;               // [nnz] one context: w*mu of every shared constraint's element, CSC order
   int32_t* fb_long;          // [nC+1] one context: count, then the long shared constraints (fb_long_list)
+  // one context, locality order of the increments' gathers (fb_perm): the variables sorted by their rows' first
+  // and last constraint (a flow's source- and destination-side links), mu kept in that order too
+  int32_t* vperm;            // [nV] position of each variable in the locality order
+  int32_t* csc_vp;           // [nnz] csc_v through vperm
+  double* mu_p;              // [nV] mu (vtmp) in the locality order
   // multi-launch maxmin, target-ordered rows (mm_vote_tgt): regroup scratch — sort keys (the
   // voted constraint / 16) and packed values (variable id, floor, low target bits), radix-sorted by hipCUB
   uint32_t* sk_in;

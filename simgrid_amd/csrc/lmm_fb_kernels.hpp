@@ -27,6 +27,8 @@ __global__ void __launch_bounds__(kBlock) fb_init(Dev s) {
     if (i < s.nV) {  // fair_bottleneck.cpp:29-41 (only listed variables are flattened)
       s.x[i] = 0.0;
       s.vtmp[i] = 0.0;
+      if (s.mu_p)
+        s.mu_p[i] = 0.0;
       s.vst[i] = 1;
       s.fixr[i] = -1;
     }
@@ -170,6 +172,8 @@ __device__ __forceinline__ int var_inc_finish(const Dev& s, int64_t v, double in
   if (vb > 0)
     inc = fmin(inc, vb - x);
   s.vtmp[v] = inc;
+  if (s.mu_p)
+    s.mu_p[s.vperm[v]] = inc;  // (one scattered store per listed variable: the chains then gather with locality)
   x += inc;
   s.x[v] = x;
   s.fixr[v] = round;  // last round in which v was listed
@@ -272,6 +276,33 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
   fb_work_add(s, 1, nvl);
 }
 
+// mu of CSC element j (variable v): from the locality-ordered copy when there is one (fb_perm).
+__device__ __forceinline__ double fb_mu(const Dev& s, uint32_t j, int32_t v) {
+  return s.mu_p ? s.mu_p[s.csc_vp[j]] : s.vtmp[v];
+}
+
+// Locality order of the mu gathers (one context, once per upload): a flow's elements sit on its route's links,
+// so sorting the variables by their row's first and last constraint (source-side and destination-side links)
+// puts the flows a link carries in few runs; the chains, which must visit a link's elements in the reference's
+// order, then gather mu from a few regions instead of one line per element.  Values never move: only the
+// copy of mu the chains read (mu_p) and the element -> position map (csc_vp) use the order.
+__global__ void __launch_bounds__(kBlock) fbp_keys(Dev s, unsigned long long* key, int32_t* val) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
+    const uint32_t b = s.var_ptr[v], e = s.var_ptr[v + 1];
+    key[v] = b < e ? (unsigned long long)uint32_t(s.csr_c[b]) * uint64_t(s.nC) + uint32_t(s.csr_c[e - 1])
+                   : ~0ull;
+    val[v] = int32_t(v);
+  }
+}
+__global__ void __launch_bounds__(kBlock) fbp_inv(Dev s, const int32_t* order) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < s.nV; i += int64_t(gridDim.x) * kBlock)
+    s.vperm[order[i]] = int32_t(i);
+}
+__global__ void __launch_bounds__(kBlock) fbp_csc(Dev s) {
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz; j += int64_t(gridDim.x) * kBlock)
+    s.csc_vp[j] = s.vperm[s.csc_v[j]];
+}
+
 // :107-127 — per chunk of a listed constraint.  FATPIPE: min of w*mu over ALL its elements (the stale mu of
 // variables that already left the list included) -> pacc.  Shared: the increments w * mu in CSC order into
 // fbd (element-parallel, all gathers of the round spread over the chip), which fbk_update_seq then chains
@@ -311,7 +342,7 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int all, uint32_t longm
         double dv[4];
 #pragma unroll
         for (int k = 0; k < 4; k++)
-          dv[k] = vv[k] >= 0 ? s.csc_w[j0 + k * kWave] * s.vtmp[vv[k]] : 0.0;
+          dv[k] = vv[k] >= 0 ? s.csc_w[j0 + k * kWave] * fb_mu(s, j0 + k * kWave, vv[k]) : 0.0;
 #pragma unroll
         for (int k = 0; k < 4; k++)
           if (vv[k] >= 0)
@@ -321,7 +352,7 @@ __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int all, uint32_t longm
     }
     double acc = dinf();
     for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave)
-      acc = fmin(acc, s.csc_w[j] * s.vtmp[s.csc_v[j]]);
+      acc = fmin(acc, s.csc_w[j] * fb_mu(s, j, s.csc_v[j]));
     acc = wave_min(acc);
     if (lane == 0)
       s.pacc[q] = acc;
@@ -545,19 +576,21 @@ __device__ __forceinline__ double fb_chain_pull(const Dev& s, uint32_t cb, uint3
                                                 double* d, int lane) {
   int32_t ix[kSeqP];
   double ww[kSeqP], vt[kSeqP];
+  const int32_t* __restrict__ cv = s.mu_p ? s.csc_vp : s.csc_v;  // (mu gathered in the locality order)
+  const double* __restrict__ mu = s.mu_p ? s.mu_p : s.vtmp;
 #pragma unroll
   for (int p = 0; p < kSeqP; p++) {  // batch 0: elements, then their mu
     const uint32_t j = cb + p * kWave + lane;
-    ix[p] = j < ce ? s.csc_v[j] : -1;
+    ix[p] = j < ce ? cv[j] : -1;
     ww[p] = j < ce ? s.csc_w[j] : 0.0;
   }
 #pragma unroll
   for (int p = 0; p < kSeqP; p++)
-    vt[p] = ix[p] >= 0 ? s.vtmp[ix[p]] : 0.0;
+    vt[p] = ix[p] >= 0 ? mu[ix[p]] : 0.0;
 #pragma unroll
   for (int p = 0; p < kSeqP; p++) {  // batch 1's elements
     const uint32_t j = cb + kSeqP * kWave + p * kWave + lane;
-    ix[p] = j < ce ? s.csc_v[j] : -1;
+    ix[p] = j < ce ? cv[j] : -1;
   }
   for (uint32_t base = cb; base < ce; base += kSeqP * kWave) {  // wave-uniform
     bool nonneg = true;
@@ -572,13 +605,13 @@ __device__ __forceinline__ double fb_chain_pull(const Dev& s, uint32_t cb, uint3
 #pragma unroll
     for (int p = 0; p < kSeqP; p++) {  // next batch: mu gathers (its elements arrived) and weights
       const uint32_t j = nb + p * kWave + lane;
-      vt[p] = ix[p] >= 0 ? s.vtmp[ix[p]] : 0.0;
+      vt[p] = ix[p] >= 0 ? mu[ix[p]] : 0.0;
       ww[p] = j < ce ? s.csc_w[j] : 0.0;
     }
 #pragma unroll
     for (int p = 0; p < kSeqP; p++) {  // the batch after: elements
       const uint32_t j = nb2 + p * kWave + lane;
-      ix[p] = j < ce ? s.csc_v[j] : -1;
+      ix[p] = j < ce ? cv[j] : -1;
     }
     __builtin_amdgcn_wave_barrier();
     rem = fb_chain_step(d, int(ce - base < uint32_t(kSeqP * kWave) ? ce - base : uint32_t(kSeqP * kWave)), rem, prec,

@@ -145,6 +145,8 @@ struct lmmhip_ctx {
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
   Scr tg_kin, tg_kout, tg_vin, tg_vout, tg_tmp;  // multi-launch engine: regroup of target-ordered rows
   Scr fb_longl;                                   // solve_fair: the long shared constraints (fb_long_list)
+  Scr fbp_k0, fbp_k1, fbp_v0, fbp_v1, fbp_tmp, fbp_perm, fbp_cscvp, fbp_mu;  // solve_fair: locality order (fb_perm)
+  bool fb_perm_ok = false;                        // the order matches the uploaded system
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
 };
@@ -244,7 +246,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch})
@@ -428,6 +430,7 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
 // Solver launch parameters from the system's shape + per-element usage; the system is then solvable.
 static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
   Dev& d = c->d;
+  c->fb_perm_ok = false;
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
   const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
@@ -1499,6 +1502,48 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
   return 0;
 }
 
+// The locality order of the one-context FairBottleneck's mu gathers (lmm_fb_kernels.hpp fbp_*): once per
+// uploaded system, outside the solve.  LMMHIP_FB_PERM=0 gathers mu by variable id instead (measurement knob).
+static int fb_perm(lmmhip_ctx* c) {
+  Dev& d = c->d;
+  if (!env_int("LMMHIP_FB_PERM", 1) || d.nV == 0) {
+    d.mu_p = nullptr;
+    return 0;
+  }
+  int32_t *v0, *v1;
+  unsigned long long *k0, *k1;
+  int rc = scratch(c, c->fbp_k0, d.nV, &k0);
+  rc = rc ? rc : scratch(c, c->fbp_k1, d.nV, &k1);
+  rc = rc ? rc : scratch(c, c->fbp_v0, d.nV, &v0);
+  rc = rc ? rc : scratch(c, c->fbp_v1, d.nV, &v1);
+  rc = rc ? rc : scratch(c, c->fbp_perm, d.nV, &d.vperm);
+  rc = rc ? rc : scratch(c, c->fbp_cscvp, std::max<int64_t>(d.nnz, 1), &d.csc_vp);
+  rc = rc ? rc : scratch(c, c->fbp_mu, d.nV, &d.mu_p);
+  if (rc)
+    return rc;
+  if (!c->fb_perm_ok) {
+    const unsigned long long span = (unsigned long long)d.nC * (unsigned long long)d.nC + 1;
+    const int bits = std::min(64, 64 - __builtin_clzll(span));
+    hipLaunchKernelGGL(fbp_keys, dim3(grid_for(d.nV, kBlock)), dim3(kBlock), 0, c->stream, d, k0, v0);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0;
+    HIPCHK(sort_pairs_u64_i32(nullptr, tb, k0, k1, v0, v1, d.nV, 64, c->stream));
+    uint8_t* t = nullptr;
+    if ((rc = scratch(c, c->fbp_tmp, int64_t(tb), &t)))
+      return rc;
+    // (keys of empty rows are all ones: sorted with the 64-bit width when the span needs it)
+    HIPCHK(sort_pairs_u64_i32(t, tb, k0, k1, v0, v1, d.nV, bits < 64 ? 64 : bits, c->stream));
+    hipLaunchKernelGGL(fbp_inv, dim3(grid_for(d.nV, kBlock)), dim3(kBlock), 0, c->stream, d, v1);
+    HIPCHK(hipGetLastError());
+    if (d.nnz > 0) {
+      hipLaunchKernelGGL(fbp_csc, dim3(grid_for(d.nnz, kBlock)), dim3(kBlock), 0, c->stream, d);
+      HIPCHK(hipGetLastError());
+    }
+    c->fb_perm_ok = true;
+  }
+  return 0;
+}
+
 static int solve_fair(lmmhip_ctx* c, double prec) {
   c->fb_shard = false;
   // shared constraints of at least this many elements get their increments precomputed element-parallel
@@ -1519,6 +1564,8 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   HIPCHK(hipGetLastError());
   c->d.xnb = c->xnb_own;
   c->d.xmin = c->xmin_own;
+  if (int rc = fb_perm(c))
+    return rc;
   if (int rc = fb_begin(c, prec))
     return rc;
   // The reference's rounds are not bounded by the system size (FATPIPE remaining can shrink
@@ -1767,6 +1814,7 @@ int lmmhip_fb_shard_begin(lmmhip_ctx* c, double precision, int32_t* xnb, double*
   c->fbo.xrem = xrem;
   c->fbo.mu_off = mu_off;
   c->fb_shard = true;
+  c->d.mu_p = nullptr;  // (the shard kernels gather mu by variable id; fb_perm is the one-context path's)
   c->last_kind = LMMHIP_KIND_FAIR_BOTTLENECK;
   return fb_begin(c, precision);
 }

@@ -33,4 +33,11 @@ hipError_t sort_pairs_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* keys
   return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0, end_bit, s);
 }
 
+// Locality order of the FairBottleneck mu gathers (fb_perm): 64-bit keys, variable ids.
+hipError_t sort_pairs_u64_i32(void* tmp, size_t& tmp_bytes, const unsigned long long* keys_in,
+                              unsigned long long* keys_out, const int32_t* vals_in, int32_t* vals_out, int64_t n,
+                              int end_bit, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0, end_bit, s);
+}
+
 }  // namespace lmmdev
