@@ -961,7 +961,7 @@ __global__ void __launch_bounds__(kBlock) fbo_apply(Dev s, FbOwner o) {
 }
 
 // :132-139 — the listed variables of an erased constraint leave the list
-__global__ void __launch_bounds__(kBlock) fbk_unlist(Dev s) {
+__global__ void __launch_bounds__(kBlock) fbk_unlist(Dev s, int bits) {
   if (s.ctl[CTL_DONE])
     return;
   const int lane = threadIdx.x & (kWave - 1);
@@ -970,8 +970,14 @@ __global__ void __launch_bounds__(kBlock) fbk_unlist(Dev s) {
     const int c = s.ch_cnst[q];
     if (!s.erased[c])
       continue;
-    for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave)
-      s.vst[s.csc_v[j]] = 0;
+    // bits (rounds > 0): skip the variables the round-start flags (vstb, resident in L2) already show delisted —
+    // a variable leaves one time but sits on several erased constraints, and a random byte store costs a
+    // partial-line write where the flag test is an L2 hit
+    for (uint32_t j = s.ch_beg[q] + lane, e = chunk_end(s, q, c); j < e; j += kWave) {
+      const int32_t v = s.csc_v[j];
+      if (!bits || ((s.vstb[v >> 5] >> (v & 31)) & 1))
+        s.vst[v] = 0;
+    }
   }
 }
 

@@ -1486,14 +1486,14 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
     // one context: element by element in the CSC order, bit-identical to the reference
     LAUNCH(5, r, fbk_update_seq, kLongBlocks + grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec,
            c->fb_longmin);
-    LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
+    LAUNCH(5, r, fbk_unlist, gQ, kBlock, d, int(r > 0));  // (vstb is packed in rounds > 0)
     c->fb_round++;
     break;
   case 3:
     if (!c->fb_shard)
       return fail(LMMHIP_E_ARG, "phase 3 exists only in a sharded solve");
     LAUNCH(5, r, fbo_apply, gC, kBlock, d, c->fbo);
-    LAUNCH(5, r, fbk_unlist, gQ, kBlock, d);
+    LAUNCH(5, r, fbk_unlist, gQ, kBlock, d, int(r > 0));  // (vstb is packed in rounds > 0)
     c->fb_round++;
     break;
   default:
