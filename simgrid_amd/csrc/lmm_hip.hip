@@ -148,7 +148,7 @@ struct lmmhip_ctx {
   Scr fbp_k0, fbp_k1, fbp_v0, fbp_v1, fbp_tmp, fbp_perm, fbp_cscvp, fbp_mu;  // solve_fair: locality order (fb_perm)
   bool fb_perm_ok = false;                        // the order matches the uploaded system
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
-      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch;
+      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch, rs_rowpen;
 };
 
 static void free_owner(lmmhip_ctx* c) {
@@ -249,7 +249,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
-                             &c->rs_nck, &c->rs_cch})
+                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen})
     if (b->p)
       (void)hipFree(b->p);
   for (lmmhip_ctx::Scr& b : c->rs_stage)
@@ -428,7 +428,7 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
 }
 
 // Solver launch parameters from the system's shape + per-element usage; the system is then solvable.
-static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
+static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, bool elem_done = false) {
   Dev& d = c->d;
   c->fb_perm_ok = false;
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
@@ -438,8 +438,10 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz) {
   if (nC > 0)  // constraints with a duplicate (variable, constraint) pair (structure only)
     HIPCHK(hipMemsetAsync(d.cdup, 0, size_t(nC), c->stream));
   if (nnz > 0) {  // per-element usage w / penalty, kept in step with pen (lmmhip_update_vars)
-    hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, c->stream, d, 1);
-    HIPCHK(hipGetLastError());
+    if (!elem_done) {
+      hipLaunchKernelGGL(mm_elem_usage, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, c->stream, d, 1);
+      HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(mm_dup_check, dim3(grid_for(nV, kBlock)), dim3(kBlock), 0, c->stream, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -883,13 +885,15 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   c->res_flat_kind = fair ? LMMHIP_KIND_FAIR_BOTTLENECK : LMMHIP_KIND_MAXMIN;
   c->res_flat_nv = nvs;
   int32_t *rowid, *kidx, *skey, *sval;
+  RowPen* rowpen;
   rc = scratch(c, c->rs_rowid, nnz, &rowid) | scratch(c, c->rs_kidx, nnz, &kidx) |
-       scratch(c, c->rs_skey, nnz, &skey) | scratch(c, c->rs_sval, nnz, &sval);
+       scratch(c, c->rs_skey, nnz, &skey) | scratch(c, c->rs_sval, nnz, &sval) |
+       scratch(c, c->rs_rowpen, std::max<int64_t>(nV, 1), &rowpen);
   if (rc)
     return rc;
   RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, fair ? lzero : nullptr, fb.cb, fb.cf);
   RS_LAUNCH(rs_write, nvs, nvs, r, pos, lany, dcl, vm, dv, ro, fb.vp, fb.csr_c, fb.csr_w, fb.pen, fb.vb, fb.cvar0,
-            rowid, kidx);
+            rowid, kidx, rowpen);
   const uint32_t nnz32 = uint32_t(nnz);
   HIPCHK(hipMemcpyAsync(fb.vp + nV, &nnz32, sizeof(nnz32), hipMemcpyHostToDevice, c->stream));
   if (fair)
@@ -910,12 +914,13 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     if ((rc = scratch(c, c->rs_tmp, int64_t(tb), &t)))
       return rc;
     HIPCHK(sort_pairs_i32(t, tb, fb.csr_c, skey, kidx, sval, nnz, bits, c->stream));
-    RS_LAUNCH(rs_csc, nnz, nnz, sval, rowid, fb.csr_w, fb.csc_v, fb.csc_w);
+    RS_LAUNCH(rs_csc, nnz, nnz, sval, rowid, fb.csr_w, rowpen, fb.csc_v, fb.csc_w, c->d.csc_u, c->d.csc_p,
+              c->d.csc_row);
     if (!fair)
       RS_LAUNCH(rs_cptr_sorted, nnz, nnz, nC, skey, fb.cp);
   }
   HIPCHK(hipStreamSynchronize(c->stream));  // before the host's list buffer is released
-  if ((rc = finish_flat(c, nV, nC, nnz)))
+  if ((rc = finish_flat(c, nV, nC, nnz, true)))  // (rs_csc wrote the per-element usage, penalty and row)
     return rc;
   c->res_last_list.assign(cnst_list, cnst_list + nl);
   c->res_last_prec = precision;

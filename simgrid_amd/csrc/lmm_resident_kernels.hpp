@@ -307,12 +307,19 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// Per dense row: its CSR range and penalty in one 16-B record, so that rs_csc reads them with ONE gather per
+// element (the per-element usage, penalty and row of the CSC come out of the transpose itself).
+struct alignas(16) RowPen {
+  uint32_t rb, re;
+  double pen;
+};
+
 // CSR rows, per-variable arrays and the dense -> slot map.
 __global__ void __launch_bounds__(kBlock)
     rs_write(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
              const int64_t* __restrict__ dcl, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
              const int64_t* __restrict__ ro, uint32_t* var_ptr, int32_t* csr_c, double* csr_w, double* pen,
-             double* vbound, int32_t* cvar0, int32_t* rowid, int32_t* kidx) {
+             double* vbound, int32_t* cvar0, int32_t* rowid, int32_t* kidx, RowPen* rowpen) {
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
     if (!vm[v])
       continue;
@@ -349,6 +356,7 @@ __global__ void __launch_bounds__(kBlock)
           k++;
         }
     }
+    rowpen[i] = RowPen{uint32_t(ro[v]), uint32_t(k), r.v_pen[v]};
   }
 }
 
@@ -364,13 +372,22 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// The CSC in CSR order (the sort's values sk), plus what mm_elem_usage would gather per element afterwards:
+// usage w / penalty, the penalty and the variable's CSR row (the same division: identical bits).
 __global__ void __launch_bounds__(kBlock)
     rs_csc(int64_t nnz, const int32_t* __restrict__ sk, const int32_t* __restrict__ rowid,
-           const double* __restrict__ csr_w, int32_t* csc_v, double* csc_w) {
+           const double* __restrict__ csr_w, const RowPen* __restrict__ rowpen, int32_t* csc_v, double* csc_w,
+           double* csc_u, double* csc_p, unsigned long long* csc_row) {
   for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < nnz; j += int64_t(gridDim.x) * kBlock) {
     const int32_t k = sk[j];
-    csc_v[j] = rowid[k];
-    csc_w[j] = csr_w[k];
+    const int32_t v = rowid[k];
+    const double w = csr_w[k];
+    const RowPen rp = rowpen[v];
+    csc_v[j] = v;
+    csc_w[j] = w;
+    csc_u[j] = w / rp.pen;
+    csc_p[j] = rp.pen;
+    csc_row[j] = (unsigned long long)rp.rb | ((unsigned long long)rp.re << 32);
   }
 }
 
