@@ -73,26 +73,34 @@ __global__ void __launch_bounds__(kBlock) mm_dup_check(Dev s) {
 // Init, one wave per constraint: maxmin.cpp:520-555.  remaining = bound; skipped when
 // bound <= bound*prec; usage = sum (SHARED) or max (FATPIPE) of w/p over the active elements.
 // Waves `wave`, `wave + nwaves`, ... of the grid; returns (on lane 0) the constraints made alive.
+// One group of kInitG lanes per constraint (kWave / kInitG constraints per wave at a time: a wave used to take its
+// ~120 constraints of C2 one after the other, each a dependent chain of loads — 377 us per solve).
+constexpr int kInitG = 16;
 __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64_t wave, int64_t nwaves) {
-  const int lane = threadIdx.x & (kWave - 1);
+  const int lane = threadIdx.x & (kWave - 1), gl = lane & (kInitG - 1);
+  constexpr int kGpw = kWave / kInitG;
   int alive_cnt = 0;
-  for (int64_t c = wave; c < s.nC; c += nwaves) {
+  for (int64_t c = wave * kGpw + lane / kInitG; c < s.nC; c += nwaves * kGpw) {  // group-uniform
     const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
     const bool fat = s.cflags[c] & 1;
     double acc = 0.0;
-    // four loads in flight per lane, accumulated in the same order as a one-at-a-time loop (a missing
-    // term adds 0.0 / max's 0.0 to a non-negative acc: bit-identical)
-    for (uint32_t j0 = b + lane; j0 < e; j0 += 4 * kWave) {
+    // four loads in flight per lane, accumulated in a fixed order (a missing term adds 0.0 / max's 0.0 to a
+    // non-negative acc), so every engine computes the same bits
+    for (uint32_t j0 = b + gl; j0 < e; j0 += 4 * kInitG) {
       double u[4];
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        u[k] = j0 + k * kWave < e ? s.csc_u[j0 + k * kWave] : 0.0;
+        u[k] = j0 + k * kInitG < e ? s.csc_u[j0 + k * kInitG] : 0.0;
 #pragma unroll
       for (int k = 0; k < 4; k++)
         acc = fat ? fmax(acc, u[k]) : acc + u[k];
     }
-    acc = fat ? wave_max(acc) : wave_sum(acc);
-    if (lane == 0) {
+#pragma unroll
+    for (int o = kInitG / 2; o > 0; o >>= 1) {
+      const double y = __shfl_xor(acc, o, kInitG);
+      acc = fat ? fmax(acc, y) : acc + y;
+    }
+    if (gl == 0) {
       const double bound = s.cbound[c];
       const bool part = bound > bound * prec;
       const double usage = part ? acc : 0.0;
@@ -121,7 +129,7 @@ __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64
 
 __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int alive_cnt = init_cnsts_waves(s, prec, wave, int64_t(gridDim.x) * (kBlock / kWave));
+  const int alive_cnt = grp_isum<kWave>(init_cnsts_waves(s, prec, wave, int64_t(gridDim.x) * (kBlock / kWave)));
   if ((threadIdx.x & (kWave - 1)) == 0 && alive_cnt)
     atomicAdd(&s.ctl[CTL_ALIVE_C], alive_cnt);
 }
