@@ -1454,14 +1454,26 @@ __global__ void __launch_bounds__(kBlock) cmp_count(Dev s) {
   __shared__ int sh[2 * kBlock];
   const int64_t nrows = s.ctl[CTL_NROWS + in];
   const int64_t r0 = int64_t(blockIdx.x) * kCompactRows + int64_t(threadIdx.x) * kRowsPerThread;
+  // the thread's rows' loads issued together (ids, then states and row bounds), not one row's chain after another
+  int32_t cv[kRowsPerThread];
+#pragma unroll
+  for (int k = 0; k < kRowsPerThread; k++)
+    cv[k] = r0 + k < nrows ? s.cvar[in][r0 + k] : -1;
+  bool al[kRowsPerThread];
+  uint32_t rb[kRowsPerThread + 1];
+#pragma unroll
+  for (int k = 0; k < kRowsPerThread; k++)
+    al[k] = r0 + k < nrows && s.vstate[rvar(cv[k])] == 0;
+#pragma unroll
+  for (int k = 0; k <= kRowsPerThread; k++)
+    rb[k] = r0 + k <= nrows ? s.crow[in][r0 + k] : 0u;
   int nr = 0, ne = 0;
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t row = r0 + k;
-    if (row < nrows && row_alive(s, in, row)) {
+#pragma unroll
+  for (int k = 0; k < kRowsPerThread; k++)
+    if (al[k]) {
       nr++;
-      ne += int(s.crow[in][row + 1] - s.crow[in][row]);
+      ne += int(rb[k + 1] - rb[k]);
     }
-  }
   int a = nr, b = ne;
   block_scan2(a, b, sh);
   if (threadIdx.x == kBlock - 1) {
