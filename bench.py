@@ -131,6 +131,8 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2 = the BASELINE metric's config (default); c3/c4/c5 = the other SURVEY.md §8(d) configs")
     ap.add_argument("--flows", type=int, default=None, help="c4/c5: number of flows (default 1e5 / 1e7)")
+    ap.add_argument("--c3-weak", action="store_true",
+                    help="c3: 4096 systems per rank (weak scaling; default: 4096 in total, strong scaling)")
     ap.add_argument("--variant", default="plain", choices=["plain", "stress"],
                     help="c2: stress = 5%% FATPIPE constraints, 10%% bounded variables, penalties {1,2,4}")
     ap.add_argument("--dropin-steps", type=int, default=3,
@@ -460,16 +462,18 @@ def run_config(args):
     shards = None
     batch = None
     if args.workload == "c3":
-        n_sys = 4096
-        bounds = M.balanced_blocks(np.ones(n_sys), world)
+        # strong scaling: the 4096 seeds split over the ranks; weak (--c3-weak): 4096 per rank, rank r taking
+        # seeds 4096 r .. 4096 (r + 1) - 1 of the same generator (SURVEY.md §8(e) reports both)
+        n_sys = 4096 * world if args.c3_weak else 4096
+        bounds = [r * 4096 for r in range(world + 1)] if args.c3_weak else M.balanced_blocks(np.ones(n_sys), world)
         systems = []
         for i in range(bounds[rank], bounds[rank + 1]):
             systems.append(lmm.System(False))
             systems[-1].gen_maxmin_bench(1, i)
         batch = M.DeviceBatch(systems)  # block-diagonal upload: one workgroup per system, system in LDS
         del systems
-        work_vars, scaling = 100 * n_sys, "strong"
-        desc = dict(workload="C3: 4096 independent maxmin_bench medium systems (100 cnst x 100 vars), "
+        work_vars, scaling = 100 * n_sys, "weak" if args.c3_weak else "strong"
+        desc = dict(workload=f"C3: {n_sys} independent maxmin_bench medium systems (100 cnst x 100 vars), "
                              "one block-diagonal batch per rank (lmmhip_set_batch: one workgroup per system, "
                              "the system in LDS)", systems=n_sys,
                     parallelism=f"systems in nnz-balanced blocks x{world}")
