@@ -10,6 +10,7 @@ constraint-bound updates.  Prints one JSON line per path with the per-phase wall
 usage: python scripts/resident_steps.py [--cnst N] [--vars N] [--steps K] [--pen P] [--cb B]
 """
 import argparse
+import ctypes as ct
 import json
 import os
 import sys
@@ -39,9 +40,12 @@ def run(resident, a):
         s.solve()
         wall = (time.perf_counter() - t) * 1e3
         st = s.last_stats()
+        nref = ct.c_int64(-1)
+        if resident:
+            L._check_hip(L.lib().lmmhip_res_refreshes(s.device_ctx(), ct.byref(nref)))
         rows.append(dict(step=step, wall_ms=wall, flatten_ms=st["flatten_ms"], upload_ms=st["upload_ms"],
                          device_ms=st["device_ms"], fetch_ms=st["fetch_ms"], delta_records=st["delta_records"],
-                         n_var=st["n_var"]))
+                         n_var=st["n_var"], refreshes=nref.value))
         print(json.dumps(dict(path="resident" if resident else "host", **rows[-1])), file=sys.stderr, flush=True)
     x = s.values_of(vs)
     steady = rows[1:]

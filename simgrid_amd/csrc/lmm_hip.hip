@@ -148,7 +148,7 @@ struct lmmhip_ctx {
   Scr fbp_k0, fbp_k1, fbp_v0, fbp_v1, fbp_tmp, fbp_perm, fbp_cscvp, fbp_mu;  // solve_fair: locality order (fb_perm)
   bool fb_perm_ok = false;                        // the order matches the uploaded system
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
-      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch, rs_rowpen;
+      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch, rs_rowpen, rs_posd, rs_cls, rs_lanyc;
 };
 
 static void free_owner(lmmhip_ctx* c) {
@@ -249,7 +249,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
-                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen})
+                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc})
     if (b->p)
       (void)hipFree(b->p);
   for (lmmhip_ctx::Scr& b : c->rs_stage)
@@ -404,9 +404,10 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
   const bool fits = have && nV <= c->fcap[0] && nC <= c->fcap[1] && nnz <= c->fcap[2] && nch <= c->fcap[3];
   if (!fits) {
     int64_t a[4] = {nV, nC, nnz, nch};
-    if (have)
-      for (int i = 0; i < 4; i++)
-        a[i] = std::max(a[i], c->fcap[i] + c->fcap[i] / 4);
+    // headroom: a simulation's next system is usually a little larger (flows arriving, a link's bound
+    // leaving 0); growing the flat buffers costs ~10 ms of frees and allocations at C2's size
+    for (int i = 0; i < 4; i++)
+      a[i] = have ? std::max(a[i], c->fcap[i] + c->fcap[i] / 4) : a[i] + a[i] / 16;
     if (a[2] > INT32_MAX)
       a[2] = std::max(nnz, int64_t(INT32_MAX));
     if (int rc = alloc_flat_exact(c, a[0], a[1], a[2], a[3], &c->fb_last))
@@ -616,7 +617,7 @@ template <class T> static int scratch(lmmhip_ctx* c, lmmhip_ctx::Scr& b, int64_t
     HIPCHK(hipStreamSynchronize(c->stream));  // the old buffer may still be read by queued work
     if (b.p)
       HIPCHK(hipFree(b.p));
-    const size_t bytes = std::max(need, b.bytes + b.bytes / 2);
+    const size_t bytes = b.bytes ? std::max(need, b.bytes + b.bytes / 2) : need + need / 16;  // (alloc_flat)
     b.p = nullptr;
     b.bytes = 0;
     HIPCHK(hipMalloc(&b.p, bytes));
@@ -726,8 +727,9 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
     c->res_capC = cap;
   }
   if (!c->res_dirty) {
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 2 * sizeof(int32_t)));  // flags, fair error
-    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 2 * sizeof(int32_t), c->stream));
+    // flags, fair error, "mixed" variable (rs_mark), spare
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 4 * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 4 * sizeof(int32_t), c->stream));
   }
   if (ne || n_var_total > c->res_nV || n_cnst_total > c->res_nC)
     c->res_struct_host = true;
@@ -817,8 +819,8 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
       return 0;
     }
   }
-  int32_t *pos, *list;
-  uint8_t *lpart, *vrst, *lzero;
+  int32_t *pos, *list, *posd;
+  uint8_t *lpart, *vrst, *lzero, *cls = nullptr, *lanyc = nullptr;
   int64_t *lany, *dcl, *cdeg, *cptr, *vm, *dv, *rl, *ro;
   int rc = scratch(c, c->rs_pos, c->res_nC, &pos) | scratch(c, c->rs_list, nl, &list) |
            scratch(c, c->rs_lzero, nl, &lzero) |
@@ -826,7 +828,10 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
            scratch(c, c->rs_dcl, nl + 1, &dcl) | scratch(c, c->rs_cdeg, nl + 1, &cdeg) |
            scratch(c, c->rs_cptr, nl + 1, &cptr) | scratch(c, c->rs_vrst, nvs, &vrst) |
            scratch(c, c->rs_vm, nvs + 1, &vm) | scratch(c, c->rs_dv, nvs + 1, &dv) |
-           scratch(c, c->rs_rl, nvs + 1, &rl) | scratch(c, c->rs_ro, nvs + 1, &ro);
+           scratch(c, c->rs_rl, nvs + 1, &rl) | scratch(c, c->rs_ro, nvs + 1, &ro) |
+           scratch(c, c->rs_posd, std::max<int64_t>(c->res_nC, 1), &posd);
+  if (!fair)
+    rc |= scratch(c, c->rs_cls, c->res_nC, &cls) | scratch(c, c->rs_lanyc, c->res_nC, &lanyc);
   if (rc)
     return rc;
   if (nl)
@@ -835,22 +840,33 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     HIPCHK(hipMemsetAsync(pos, 0xFF, size_t(c->res_nC) * sizeof(int32_t), c->stream));
   HIPCHK(hipMemsetAsync(cdeg, 0, size_t(nl + 1) * sizeof(int64_t), c->stream));
   if (!c->res_dirty) {
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 2 * sizeof(int32_t)));
-    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 2 * sizeof(int32_t), c->stream));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 4 * sizeof(int32_t)));
+    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 4 * sizeof(int32_t), c->stream));
   }
-  RS_LAUNCH(rs_pos, nl, nl, list, r, precision, int(fair), pos, lpart, lany, lzero);
+  if (!fair && c->res_nC) {
+    HIPCHK(hipMemsetAsync(cls, 0, size_t(c->res_nC), c->stream));
+    HIPCHK(hipMemsetAsync(lanyc, 0, size_t(c->res_nC), c->stream));
+  }
+  RS_LAUNCH(rs_pos, nl, nl, list, r, precision, int(fair), pos, lpart, lany, lzero, cls);
   if (fair) {
     HIPCHK(hipMemsetAsync(c->res_dirty + 1, 0, sizeof(int32_t), c->stream));
     RS_LAUNCH(rs_mark_fair, nvs, nvs, r, pos, lany, lzero, vrst, vm, c->res_dirty + 1);
   } else {
-    RS_LAUNCH(rs_mark, nvs, nvs, r, pos, lpart, lany, vrst, vm);
+    HIPCHK(hipMemsetAsync(c->res_dirty + 2, 0, sizeof(int32_t), c->stream));
+    RS_LAUNCH(rs_mark, nvs, nvs, r, cls, lanyc, vrst, vm, rl, c->res_dirty + 2);
+    RS_LAUNCH(rs_lany_list, nl, nl, list, lanyc, lany);
   }
   if ((rc = dev_scan(c, lany, dcl, nl + 1)))
     return rc;
+  // posd[c] = dense id of constraint c, or -1: one gather per element in rs_rowlen / rs_write instead of the
+  // dependent pos -> lany -> dcl chain
+  if (c->res_nC)
+    HIPCHK(hipMemsetAsync(posd, 0xFF, size_t(c->res_nC) * sizeof(int32_t), c->stream));
+  RS_LAUNCH(rs_posd, nl, nl, list, lany, dcl, posd);
   if (fair)
     RS_LAUNCH(rs_rowlen_fair, nvs, nvs, r, pos, lany, dcl, vm, rl, cdeg);
-  else  // (max-min: CSC offsets from the sorted ids below, no degree atomics)
-    RS_LAUNCH(rs_rowlen, nvs, nvs, r, pos, lany, dcl, vm, rl, static_cast<int64_t*>(nullptr));
+  else  // (max-min: rs_mark counted the rows unless a member has a disabled element; CSC offsets from the sort)
+    RS_LAUNCH(rs_rowlen, nvs, nvs, r, posd, vm, rl, c->res_dirty + 2);
   if ((rc = dev_scan(c, vm, dv, nvs + 1)) || (rc = dev_scan(c, rl, ro, nvs + 1)) ||
       (fair && (rc = dev_scan(c, cdeg, cptr, nl + 1))))
     return rc;
@@ -884,16 +900,17 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   c->res_flat = true;
   c->res_flat_kind = fair ? LMMHIP_KIND_FAIR_BOTTLENECK : LMMHIP_KIND_MAXMIN;
   c->res_flat_nv = nvs;
-  int32_t *rowid, *kidx, *skey, *sval;
+  int32_t *kidx, *skey, *sval;
+  WRow* wrow;
   RowPen* rowpen;
-  rc = scratch(c, c->rs_rowid, nnz, &rowid) | scratch(c, c->rs_kidx, nnz, &kidx) |
+  rc = scratch(c, c->rs_rowid, nnz, &wrow) | scratch(c, c->rs_kidx, nnz, &kidx) |
        scratch(c, c->rs_skey, nnz, &skey) | scratch(c, c->rs_sval, nnz, &sval) |
        scratch(c, c->rs_rowpen, std::max<int64_t>(nV, 1), &rowpen);
   if (rc)
     return rc;
   RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, fair ? lzero : nullptr, fb.cb, fb.cf);
-  RS_LAUNCH(rs_write, nvs, nvs, r, pos, lany, dcl, vm, dv, ro, fb.vp, fb.csr_c, fb.csr_w, fb.pen, fb.vb, fb.cvar0,
-            rowid, kidx, rowpen);
+  RS_LAUNCH(rs_write, nvs, nvs, r, posd, vm, dv, ro, fb.vp, fb.csr_c, fb.csr_w, fb.pen, fb.vb, fb.cvar0,
+            wrow, kidx, rowpen);
   const uint32_t nnz32 = uint32_t(nnz);
   HIPCHK(hipMemcpyAsync(fb.vp + nV, &nnz32, sizeof(nnz32), hipMemcpyHostToDevice, c->stream));
   if (fair)
@@ -914,7 +931,7 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     if ((rc = scratch(c, c->rs_tmp, int64_t(tb), &t)))
       return rc;
     HIPCHK(sort_pairs_i32(t, tb, fb.csr_c, skey, kidx, sval, nnz, bits, c->stream));
-    RS_LAUNCH(rs_csc, nnz, nnz, sval, rowid, fb.csr_w, rowpen, fb.csc_v, fb.csc_w, c->d.csc_u, c->d.csc_p,
+    RS_LAUNCH(rs_csc, nnz, nnz, sval, wrow, rowpen, fb.csc_v, fb.csc_w, c->d.csc_u, c->d.csc_p,
               c->d.csc_row);
     if (!fair)
       RS_LAUNCH(rs_cptr_sorted, nnz, nnz, nC, skey, fb.cp);

@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(kBlock)
 // (cleared here) then marks the ones with an enabled zero-weight element (cflags bit1).
 __global__ void __launch_bounds__(kBlock)
     rs_pos(int64_t nl, const int32_t* __restrict__ list, ResDev r, double prec, int fair, int32_t* pos,
-           uint8_t* lpart, int64_t* lany, uint8_t* lzero) {
+           uint8_t* lpart, int64_t* lany, uint8_t* lzero, uint8_t* cls) {
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i <= nl; i += int64_t(gridDim.x) * kBlock) {
     lany[i] = 0;
     if (i == nl)
@@ -108,67 +108,97 @@ __global__ void __launch_bounds__(kBlock)
     pos[c] = int32_t(i);
     const double b = r.c_bound[c];
     lpart[i] = fair ? 1 : b > b * prec;
+    if (cls)  // max-min: class of constraint c by id (0 = not listed, 1 = listed, 2 = listed and part)
+      cls[c] = uint8_t(1 + lpart[i]);
   }
 }
 
 // Per variable slot: value reset (enabled element on a listed constraint, maxmin.cpp:509-514) and
 // membership (such an element with w > 0 on a part constraint, :527-538); marks the constraints that
-// have one (lany, plain stores of 1: the race is benign).
+// have one (lanyc by constraint id, plain stores of 1: the race is benign; rs_lany_list puts them in list
+// order).  One gather per element, of the 1-byte class cls[c] written by rs_pos.  The row length is the
+// number of those elements unless a member also has a disabled element of weight > 0
+// (System::flatten_maxmin takes every element of a member whose constraint is marked, enabled or not):
+// *mixed then asks rs_rowlen for the full count.
 __global__ void __launch_bounds__(kBlock)
-    rs_mark(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const uint8_t* __restrict__ lpart,
-            int64_t* lany, uint8_t* vrst, int64_t* vm) {
+    rs_mark(int64_t nv, ResDev r, const uint8_t* __restrict__ cls, uint8_t* lanyc, uint8_t* vrst, int64_t* vm,
+            int64_t* rl, int32_t* mixed) {
+  bool mix = false;
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
     if (v == nv) {
-      vm[v] = 0;  // scan sentinel
+      vm[v] = 0;  // scan sentinels
+      rl[v] = 0;
       break;
     }
     uint8_t rst = 0;
-    int64_t mk = 0;
+    int64_t cnt = 0;
+    bool dis = false;
     const int64_t b = r.v_ebase[v];
     const int n = r.v_n[v];
     for (int i0 = 0; i0 < n; i0 += kRsU) {  // kRsU elements' loads in flight together
       int32_t p[kRsU];
-      uint8_t fl[kRsU];
+      uint8_t fl[kRsU], k[kRsU];
+      double w[kRsU];
 #pragma unroll
       for (int u = 0; u < kRsU; u++) {
         p[u] = i0 + u < n ? r.e_cnst[b + i0 + u] : -1;
         fl[u] = i0 + u < n ? r.e_fl[b + i0 + u] : 0;
+        w[u] = i0 + u < n ? r.e_w[b + i0 + u] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < kRsU; u++)
-        if (!(fl[u] & kResElemEnabled))
+        if (!(fl[u] & kResElemEnabled)) {
+          dis |= p[u] >= 0 && w[u] > 0;
           p[u] = -1;
+        }
 #pragma unroll
       for (int u = 0; u < kRsU; u++)
-        p[u] = p[u] >= 0 ? pos[p[u]] : -1;
+        k[u] = p[u] >= 0 ? cls[p[u]] : 0;
 #pragma unroll
       for (int u = 0; u < kRsU; u++) {
-        if (p[u] < 0)
+        if (!k[u])
           continue;
         rst = 1;
-        if (r.e_w[b + i0 + u] > 0 && lpart[p[u]]) {
-          mk = 1;
-          lany[p[u]] = 1;
+        if (w[u] > 0 && k[u] == 2) {
+          cnt++;
+          lanyc[p[u]] = 1;
         }
       }
     }
     vrst[v] = rst;
-    vm[v] = mk;
+    vm[v] = cnt > 0;
+    rl[v] = cnt;
+    mix |= cnt > 0 && dis;
   }
+  if (mix)
+    atomicOr(mixed, 1);
 }
 
-// Row lengths of the member variables (elements with w > 0 on a part constraint, in slot order, no
-// enabled-list test: System::flatten_maxmin) and the per-constraint degrees (dense ids = dcl).
-// cdeg == nullptr: row lengths only (max-min: the CSC offsets come from the sorted constraint ids,
-// rs_cptr_sorted, instead of one atomic per element — 8e7 of them at C2).
+// lany[i] = lanyc[list[i]] (max-min: rs_mark marks by constraint id).
 __global__ void __launch_bounds__(kBlock)
-    rs_rowlen(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
-              const int64_t* __restrict__ dcl, const int64_t* __restrict__ vm, int64_t* rl, int64_t* cdeg) {
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
-    if (v == nv) {
-      rl[v] = 0;
-      break;
-    }
+    rs_lany_list(int64_t nl, const int32_t* __restrict__ list, const uint8_t* __restrict__ lanyc, int64_t* lany) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nl; i += int64_t(gridDim.x) * kBlock)
+    lany[i] = lanyc[list[i]];
+}
+
+// posd[c] = dense id of listed constraint c when it is marked (lany), else left at -1.
+__global__ void __launch_bounds__(kBlock)
+    rs_posd(int64_t nl, const int32_t* __restrict__ list, const int64_t* __restrict__ lany,
+            const int64_t* __restrict__ dcl, int32_t* posd) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nl; i += int64_t(gridDim.x) * kBlock)
+    if (lany[i])
+      posd[list[i]] = int32_t(dcl[i]);
+}
+
+// Max-min row lengths when a member has a disabled element (*mixed, from rs_mark; otherwise nothing to do):
+// elements with w > 0 on a marked constraint, in slot order, no enabled-list test (System::flatten_maxmin).
+// The CSC offsets come from the sorted constraint ids (rs_cptr_sorted), not from degree atomics.
+__global__ void __launch_bounds__(kBlock)
+    rs_rowlen(int64_t nv, ResDev r, const int32_t* __restrict__ posd, const int64_t* __restrict__ vm, int64_t* rl,
+              const int32_t* __restrict__ mixed) {
+  if (!*mixed)
+    return;
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
     int64_t cnt = 0;
     if (vm[v]) {
       const int64_t b = r.v_ebase[v];
@@ -180,14 +210,11 @@ __global__ void __launch_bounds__(kBlock)
           p[u] = i0 + u < n ? r.e_cnst[b + i0 + u] : -1;
 #pragma unroll
         for (int u = 0; u < kRsU; u++)
-          p[u] = p[u] >= 0 ? pos[p[u]] : -1;
+          p[u] = p[u] >= 0 ? posd[p[u]] : -1;
 #pragma unroll
         for (int u = 0; u < kRsU; u++)
-          if (p[u] >= 0 && lany[p[u]] && r.e_w[b + i0 + u] > 0) {
+          if (p[u] >= 0 && r.e_w[b + i0 + u] > 0)
             cnt++;
-            if (cdeg)
-              atomicAdd(reinterpret_cast<unsigned long long*>(cdeg + dcl[p[u]]), 1ull);
-          }
       }
     }
     rl[v] = cnt;
@@ -314,12 +341,18 @@ struct alignas(16) RowPen {
   double pen;
 };
 
+// Per CSR element: its weight and dense row in one 16-B record, so that rs_csc gathers both with one load.
+struct alignas(16) WRow {
+  double w;
+  int32_t v, pad;
+};
+
 // CSR rows, per-variable arrays and the dense -> slot map.
 __global__ void __launch_bounds__(kBlock)
-    rs_write(int64_t nv, ResDev r, const int32_t* __restrict__ pos, const int64_t* __restrict__ lany,
-             const int64_t* __restrict__ dcl, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
-             const int64_t* __restrict__ ro, uint32_t* var_ptr, int32_t* csr_c, double* csr_w, double* pen,
-             double* vbound, int32_t* cvar0, int32_t* rowid, int32_t* kidx, RowPen* rowpen) {
+    rs_write(int64_t nv, ResDev r, const int32_t* __restrict__ posd, const int64_t* __restrict__ vm,
+             const int64_t* __restrict__ dv, const int64_t* __restrict__ ro, uint32_t* var_ptr, int32_t* csr_c,
+             double* csr_w, double* pen, double* vbound, int32_t* cvar0, WRow* wrow, int32_t* kidx,
+             RowPen* rowpen) {
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
     if (!vm[v])
       continue;
@@ -341,17 +374,13 @@ __global__ void __launch_bounds__(kBlock)
       }
 #pragma unroll
       for (int u = 0; u < kRsU; u++)
-        p[u] = p[u] >= 0 ? pos[p[u]] : -1;
-      int64_t dc[kRsU];
+        p[u] = p[u] >= 0 && w[u] > 0 ? posd[p[u]] : -1;
 #pragma unroll
       for (int u = 0; u < kRsU; u++)
-        dc[u] = p[u] >= 0 && w[u] > 0 && lany[p[u]] ? dcl[p[u]] : -1;
-#pragma unroll
-      for (int u = 0; u < kRsU; u++)
-        if (dc[u] >= 0) {
-          csr_c[k] = int32_t(dc[u]);
+        if (p[u] >= 0) {
+          csr_c[k] = p[u];
           csr_w[k] = w[u];
-          rowid[k] = int32_t(i);
+          wrow[k] = WRow{w[u], int32_t(i), 0};
           kidx[k] = int32_t(k);
           k++;
         }
@@ -375,13 +404,13 @@ __global__ void __launch_bounds__(kBlock)
 // The CSC in CSR order (the sort's values sk), plus what mm_elem_usage would gather per element afterwards:
 // usage w / penalty, the penalty and the variable's CSR row (the same division: identical bits).
 __global__ void __launch_bounds__(kBlock)
-    rs_csc(int64_t nnz, const int32_t* __restrict__ sk, const int32_t* __restrict__ rowid,
-           const double* __restrict__ csr_w, const RowPen* __restrict__ rowpen, int32_t* csc_v, double* csc_w,
-           double* csc_u, double* csc_p, unsigned long long* csc_row) {
+    rs_csc(int64_t nnz, const int32_t* __restrict__ sk, const WRow* __restrict__ wrow,
+           const RowPen* __restrict__ rowpen, int32_t* csc_v, double* csc_w, double* csc_u, double* csc_p,
+           unsigned long long* csc_row) {
   for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < nnz; j += int64_t(gridDim.x) * kBlock) {
-    const int32_t k = sk[j];
-    const int32_t v = rowid[k];
-    const double w = csr_w[k];
+    const WRow e = wrow[sk[j]];
+    const int32_t v = e.v;
+    const double w = e.w;
     const RowPen rp = rowpen[v];
     csc_v[j] = v;
     csc_w[j] = w;
