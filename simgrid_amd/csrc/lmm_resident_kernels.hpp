@@ -407,16 +407,33 @@ __global__ void __launch_bounds__(kBlock)
     rs_csc(int64_t nnz, const int32_t* __restrict__ sk, const WRow* __restrict__ wrow,
            const RowPen* __restrict__ rowpen, int32_t* csc_v, double* csc_w, double* csc_u, double* csc_p,
            unsigned long long* csc_row) {
-  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < nnz; j += int64_t(gridDim.x) * kBlock) {
-    const WRow e = wrow[sk[j]];
-    const int32_t v = e.v;
-    const double w = e.w;
-    const RowPen rp = rowpen[v];
-    csc_v[j] = v;
-    csc_w[j] = w;
-    csc_u[j] = w / rp.pen;
-    csc_p[j] = rp.pen;
-    csc_row[j] = (unsigned long long)rp.rb | ((unsigned long long)rp.re << 32);
+  // kCscU elements per thread per step, their two dependent gathers (record, then row) in flight together
+  constexpr int kCscU = 4;
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t j0 = int64_t(blockIdx.x) * kBlock + threadIdx.x; j0 < nnz; j0 += kCscU * stride) {
+    int32_t k[kCscU];
+    WRow e[kCscU];
+    RowPen rp[kCscU];
+#pragma unroll
+    for (int u = 0; u < kCscU; u++)
+      k[u] = j0 + u * stride < nnz ? sk[j0 + u * stride] : -1;
+#pragma unroll
+    for (int u = 0; u < kCscU; u++)
+      e[u] = k[u] >= 0 ? wrow[k[u]] : WRow{0.0, -1, 0};
+#pragma unroll
+    for (int u = 0; u < kCscU; u++)
+      rp[u] = e[u].v >= 0 ? rowpen[e[u].v] : RowPen{0, 0, 1.0};
+#pragma unroll
+    for (int u = 0; u < kCscU; u++) {
+      const int64_t j = j0 + u * stride;
+      if (j >= nnz)
+        break;
+      csc_v[j] = e[u].v;
+      csc_w[j] = e[u].w;
+      csc_u[j] = e[u].w / rp[u].pen;
+      csc_p[j] = rp[u].pen;
+      csc_row[j] = (unsigned long long)rp[u].rb | ((unsigned long long)rp[u].re << 32);
+    }
   }
 }
 
@@ -426,12 +443,17 @@ __global__ void __launch_bounds__(kBlock) rs_ptr32(int64_t n, const int64_t* __r
 }
 
 // Per variable slot after the solve: the solved value of a member, 0 for the others (only slots with
-// vrst set are written back by the host).
+// vrst set are written back by the host).  out / rst_out are the context's mapped pinned host buffers: the
+// values cross the host link as the kernel's own coalesced stores, with no staging copy (rst_out may be null).
 __global__ void __launch_bounds__(kBlock)
     rs_values(int64_t nv, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
-              const uint8_t* __restrict__ vrst, const double* __restrict__ x, double* out) {
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock)
-    out[v] = vm[v] ? x[dv[v]] : vrst[v] == 3 ? 1.0 : 0.0;
+              const uint8_t* __restrict__ vrst, const double* __restrict__ x, double* out, uint8_t* rst_out) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
+    const uint8_t r = vrst[v];
+    out[v] = vm[v] ? x[dv[v]] : r == 3 ? 1.0 : 0.0;
+    if (rst_out)
+      rst_out[v] = r;
+  }
 }
 
 }  // namespace lmmdev
