@@ -443,8 +443,7 @@ __global__ void __launch_bounds__(kBlock) rs_ptr32(int64_t n, const int64_t* __r
 }
 
 // Per variable slot after the solve: the solved value of a member, 0 for the others (only slots with
-// vrst set are written back by the host).  out / rst_out are the context's mapped pinned host buffers: the
-// values cross the host link as the kernel's own coalesced stores, with no staging copy (rst_out may be null).
+// vrst set are written back by the host); rst_out (optional) receives a copy of the reset flags.
 __global__ void __launch_bounds__(kBlock)
     rs_values(int64_t nv, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
               const uint8_t* __restrict__ vrst, const double* __restrict__ x, double* out, uint8_t* rst_out) {
