@@ -190,7 +190,15 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
 #define LMMHIP_ENGINE_PERSISTENT 0
 #define LMMHIP_ENGINE_ROUNDS 1
 #define LMMHIP_ENGINE_AUTO 2
+/*   LMMHIP_ENGINE_FRONTIER — one launch per phase per round like ROUNDS, but each round only touches what
+ *     changed: votes are registered at their target constraint, so the update pass queues exactly the votes
+ *     a touched constraint may have invalidated (no pass over the alive rows; lmm_frontier_kernels.hpp). */
+#define LMMHIP_ENGINE_FRONTIER 3
 int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
+/* Persistent solves of this context that were re-run by the multi-launch engine because a grid-barrier wait
+ * timed out (the persistent grid was not co-resident: another process or library held CUs for seconds).
+ * Persistent launches of one process are serialised per device, so two Systems never starve each other. */
+int lmmhip_engine_fallbacks(lmmhip_ctx* ctx, int64_t* n);
 /* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the
  * wall-clock time (100 MHz) of the last workgroup's arrival and of workgroup 0's exit.  With t != NULL,
  * copies the last solve's records: t[2i] = last arrival at barrier i, t[2i+1] = exit (barrier 0 = the

@@ -1,5 +1,4 @@
-"""Round-2 diagnostics on the GPU box: (1) C5 FairBottleneck values at 1e6 flows (System path and the
-shard path) saved for offline comparison; (2) persistent-engine barrier timestamps on C2 / C4."""
+"""Round-2 diagnostics on the GPU box: persistent-engine barrier timestamps on C2 / C4."""
 import json
 import sys
 import time
@@ -11,45 +10,9 @@ from simgrid_amd import lmm as L  # noqa: E402
 from simgrid_amd import multi as M  # noqa: E402
 
 what = sys.argv[1]
-if what == "c5":
-    P = dict(topology=L.DRAGONFLY, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8, model=L.L07,
-             n_flows=int(sys.argv[2]), seed=1)
-    s = L.System(False, 1)
-    s.gen_platform_flows(L.platform_params(**P), want_vars=False)
-    f = M.export_flat(s)
-    s.solve()
-    np.save("gpurun_out/c5_dev.npy", s.device_values())
-    np.save("gpurun_out/c5_ids.npy", f.var_ids)
-    print("rounds", s.last_stats()["rounds"], flush=True)
-    sh = M.DeviceFbShard(f)
-    M.fb_solve_sharded([sh], M.LocalExchange(), len(f.penalty), len(f.cbound))
-    np.save("gpurun_out/c5_shard.npy", sh.values())
-    sh.close()
-elif what == "c5rounds":  # per-round exchange buffers of the shard protocol
-    import torch
-    P = dict(topology=L.DRAGONFLY, topo_parameters="8,4;16,3;8,2;4", loopback_bw=1e9, limiter_bw=2e8, model=L.L07,
-             n_flows=int(sys.argv[2]), seed=1)
-    s = L.System(False, 1)
-    s.gen_platform_flows(L.platform_params(**P), want_vars=False)
-    f = M.export_flat(s)
-    sh = M.DeviceFbShard(f)
-    out = {}
-    with torch.cuda.stream(sh.stream):
-        for r in range(8):
-            sh.step(0)
-            out[f"xnb{r}"] = sh.xnb.cpu().numpy()
-            sh.step(1)
-            out[f"xsum{r}"] = sh.xsum.cpu().numpy()
-            out[f"xmin{r}"] = sh.xmin.cpu().numpy()
-            sh.step(2)
-            out[f"x{r}"] = sh.values()
-            done, rounds = sh.poll()
-            print(r, done, rounds, flush=True)
-            if done:
-                break
-    np.savez("gpurun_out/c5_rounds.npz", **out)
-    sh.close()
-else:
+if what not in ("c2", "c4"):
+    sys.exit("usage: diag_r2.py c2|c4  (the C5 shard diagnostics moved to tests/test_gpu_multi.py)")
+if True:
     s = L.System(False)
     if what == "c2":
         s.gen_synthetic(1_000_000, 10_000_000, 8, seed=1, want_vars=False)

@@ -179,6 +179,15 @@ struct Dev {
   unsigned long long* sv_in;
   unsigned long long* sv_out;
   uint64_t* flagbits;  // [nC/64 + 2] measurement only: targets of the rows the filter queued (kDiag)
+  // frontier engine (lmm_frontier_kernels.hpp): votes registered at their target constraint
+  const int2* csr_cs;        // [nnz] per CSR element: its constraint and its CSC position (one 8-B pair)
+  double2* pvb;              // [nV] per variable: (bound, penalty) of this solve, one 16-B record
+  uint32_t* key32;           // [nC] 32-bit key of the ratio (ratio_key32), kDead32 when out of the light table
+  uint32_t* vslot;           // [nnz] per CSC element: floor of the vote registered there, kNoVoter if none
+  uint32_t* minfl;           // [nC] lower bound of the floors registered at the constraint (kNoVoter: none)
+  unsigned long long* fq_a;  // [nnz] re-vote queue, one segment per fr_update workgroup: variable | target << 32
+  unsigned long long* fq_b;  // [nnz]   and the variable's CSR row (begin | end << 32)
+  int32_t* fq_n;             // [nC / kFB + 1] queued variables per segment
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };
@@ -204,6 +213,12 @@ __device__ __forceinline__ uint16_t ratio_key(double r) {
   float f = __double2float_rd(r);
   return uint16_t(__float_as_uint(f) >> (23 - LMM_KEY_MANT));
 }
+
+// 32-bit monotone key (frontier engine): the ratio rounded down to f32, its bits.  Ties between different
+// ratios are 2^16 times rarer than with ratio_key, so a vote's floor is crossed only when its target's ratio
+// really reaches another constraint's (within 2^-24).
+constexpr uint32_t kDead32 = 0xFFFFFFFFu;  // > the bits of every non-negative f32, +inf included
+__device__ __forceinline__ uint32_t ratio_key32(double r) { return __float_as_uint(__double2float_rd(r)); }
 
 template <int W> __device__ __forceinline__ double grp_min(double v) {
 #pragma unroll

@@ -1,0 +1,544 @@
+// lmm_frontier_kernels.hpp — System::lmm_solve, "frontier" engine (gfx950; included by lmm_hip.hip).
+//
+// The same local-minimum progressive filling as lmm_maxmin_kernels.hpp (every alive variable
+// votes for the smallest-id constraint of minimal ratio among its constraints; a constraint every alive
+// element votes for is a local minimum and saturates), with every round's work proportional to what CHANGED
+// instead of to what is still alive.  The multi-launch engine streams every alive row each round to find the
+// votes that may move (9e6 rows and ~3.6e6 random key gathers per C2 round); here each vote is registered
+// where it can be invalidated — at its target constraint:
+//
+//   vslot[j]  (u32, per CSC element j of constraint c): the vote floor of j's variable when that variable
+//             votes for c through one of its elements on c, kNoVoter otherwise.  The floor (row_floor32) is
+//             the min 32-bit key (ratio_key32) over the variable's other constraints (and of its bound level):
+//             while c's key stays strictly below it the vote stands, because keys never decrease; 0 =
+//             "sensitive", the vote depends on c's exact ratio (a tie within 2^-24).
+//   minfl[c]  (u32): a lower bound of the floors registered at c (kNoVoter: none).
+//
+// So a vote can only move when its target was touched in the last update and the target's new key reached
+// the floor: the update pass, which owns every touched constraint anyway, reads the slots of exactly the
+// touched constraints whose new key reached minfl and queues those voters.  Round r (3 launches):
+//
+//   fr_vote    re-vote the queued variables (one lane each, the row in registers): new target and floor,
+//              slot + minfl at the new target, vote counts moved; bound fixes (maxmin.cpp:587-589) and
+//              variables whose every constraint left the light table as in mm_vote.  Round 0 (fr_vote_all)
+//              votes every variable.
+//   fr_sat     ready test (alive, nvote == 0) fused with the saturation of the ready constraints (their CSC
+//              chunks shared by the workgroup's waves, saturate_chunk: maxmin.cpp:578-606); constraints of
+//              more than kFrBigCh chunks go to a list that fr_sat_big spreads over the whole grid.
+//   fr_update  constraint update (maxmin.cpp:603-658, as mm_update) + the slot scan of the touched
+//              constraints whose key reached minfl -> the workgroup's segment of the re-vote queue.
+//
+// The decisions are exactly those of the other engines (same votes before every saturation, same ready
+// sets, integer / fixed-point atomics only): results are bit-identical to them (tests/test_gpu_engines.py).
+// Work per C2 round: the touched constraints' records and slots, the re-voted rows, the saturated
+// constraints' elements — no pass over the alive rows, no compaction.
+#pragma once
+#include "lmm_maxmin_kernels.hpp"
+
+namespace lmmdev {
+
+constexpr int kFB = 256;                 // threads per workgroup = constraints per workgroup (update, saturation)
+constexpr uint32_t kNoVoter = 0xFFFFFFFFu;  // vslot: no vote registered at this element; minfl: none at all
+constexpr int kFrBigCh = 16;             // constraints of more CSC chunks than this saturate in fr_sat_big
+constexpr int kFrBigWaves = 16;          // waves per big constraint in fr_sat_big
+
+// CSR element -> (constraint, CSC position) pairs (csr_cs), once per uploaded structure: one wave per
+// constraint, each CSC element finds its CSR element in its variable's row (csc_row); the k-th element of a
+// variable on a constraint maps to the k-th (duplicates: cdup).  Also the largest CSC degree (into *maxdeg).
+__global__ void __launch_bounds__(kBlock) fr_c2s(Dev s, int2* cs, int32_t* maxdeg) {
+  const int lane = threadIdx.x & (kWave - 1);
+  int md = 0;
+  for (int64_t c = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; c < s.nC;
+       c += int64_t(gridDim.x) * (kBlock / kWave)) {
+    const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
+    md = max(md, int(e - b));
+    const bool dup = s.cdup[c] != 0;
+    for (uint32_t j = b + lane; j < e; j += kWave) {
+      const int32_t v = s.csc_v[j];
+      const unsigned long long row = s.csc_row[j];
+      int occ = 0;
+      if (dup)
+        for (uint32_t i = b; i < j; i++)
+          occ += s.csc_v[i] == v;
+      for (uint32_t k = uint32_t(row); k < uint32_t(row >> 32); k++)
+        if (s.csr_c[k] == int32_t(c) && occ-- == 0) {
+          cs[k] = make_int2(int32_t(c), int32_t(j));
+          break;
+        }
+    }
+  }
+  md = -grp_imin<kWave>(-md);
+  if (lane == 0 && md)
+    atomicMax(maxdeg, md);
+}
+
+// Per-solve variable state (mm_init_vars) + the (bound, penalty) record the re-votes read in one line.
+__global__ void __launch_bounds__(kBlock) fr_init_vars(Dev s) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
+    s.x[v] = 0.0;
+    s.vstate[v] = 0;
+    s.rtgt[0][v] = kUnvoted;
+    s.pvb[v] = make_double2(s.vbound[v], s.pen[v]);
+  }
+}
+
+// Diagnostic counters (profiling mode only, vstat's kDiagSlot words of each round): 0 touched constraints,
+// 1 scanned constraints, 2 scanned slots, 3 queued votes, 4 moved votes, 5 ready constraints, 6 re-votes,
+// 7 bound fixes.
+__device__ __forceinline__ void fr_diag(const Dev& s, int round, int k, bool pred) {
+  if (!s.vstat || round >= kStatRounds)
+    return;
+  const unsigned long long m = __ballot(pred);
+  if (m && (threadIdx.x & (kWave - 1)) == __ffsll((long long)m) - 1)
+    atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + k, __popcll(m));
+}
+__device__ __forceinline__ void fr_diag_n(const Dev& s, int round, int k, int n) {
+  if (!s.vstat || round >= kStatRounds)
+    return;
+  n = grp_isum<kWave>(n);
+  if ((threadIdx.x & (kWave - 1)) == 0 && n)
+    atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + k, n);
+}
+
+// Re-vote of variable v (one lane): t = its current target (kUnvoted in round 0), [b, e) its CSR row.  The
+// first R elements stay in registers with their loads in flight together; longer rows loop over the rest.
+// The arithmetic and the decisions are vote_row's (lmm_maxmin_kernels.hpp).
+// Outcome of fr_revote (diagnostics): the vote stayed, moved, was fixed at its bound, or dropped.
+enum : int { FR_STAY = 0, FR_MOVE = 1, FR_BOUND = 2, FR_DROP = 3 };
+
+// The floor of a vote for a constraint of key mk (row_floor with 32-bit keys): min key over the row's other
+// constraints and, bounded, the key of the level bound * penalty; 0 = sensitive (a key-level tie).
+__device__ __forceinline__ uint32_t row_floor32(uint32_t sk, uint32_t mk, double vb, double p) {
+  uint32_t fl = sk;
+  if (vb > 0)
+    fl = min(fl, ratio_key32(vb * p));
+  return fl <= mk ? 0u : fl;
+}
+
+template <int R>
+__device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b, uint32_t e, int round) {
+  const uint32_t* __restrict__ key = s.key32;
+  // (a queued variable is alive: votes are registered only by alive variables, and the slot of a variable
+  // fixed since — at its bound, by fr_revote — was cleared when it was queued)
+  const double2 bp = s.pvb[v];
+  const double vb = bp.x, p = bp.y;
+  int32_t cc[R];
+  uint32_t sl[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    const int2 x = b + i < e ? s.csr_cs[b + i] : make_int2(-1, 0);
+    cc[i] = x.x;
+    sl[i] = uint32_t(x.y);
+  }
+  uint32_t kk[R];
+#pragma unroll
+  for (int i = 0; i < R; i++)
+    kk[i] = cc[i] >= 0 ? key[cc[i]] : kDead32;
+  uint32_t mk = kDead32;
+#pragma unroll
+  for (int i = 0; i < R; i++)
+    mk = min(mk, kk[i]);
+#pragma unroll 4
+  for (uint32_t j = b + R; j < e; j++)
+    mk = min(mk, key[s.csr_cs[j].x]);
+  if (mk == kDead32) {  // every constraint of v left the light table: v stays at 0
+    s.vstate[v] = round + 1;
+    return FR_DROP;
+  }
+  int nmin = 0, mult_old = 0, newt = INT_MAX;
+  uint32_t kt = kDead32;
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    nmin += kk[i] == mk;
+    if (cc[i] == t) {
+      mult_old++;
+      kt = kk[i];
+    }
+    if (kk[i] == mk)
+      newt = min(newt, cc[i]);
+  }
+#pragma unroll 4
+  for (uint32_t j = b + R; j < e; j++) {
+    const int32_t c = s.csr_cs[j].x;
+    const uint32_t k = key[c];
+    nmin += k == mk;
+    if (c == t) {
+      mult_old++;
+      kt = k;
+    }
+    if (k == mk)
+      newt = min(newt, c);
+  }
+  double minr = dinf();
+  if (nmin > 1 || vb > 0) {  // exact ratios at the minimal key: lexicographic min of (ratio, id)
+    newt = INT_MAX;
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      if (kk[i] == mk) {
+        const double r = s.cst[cc[i]].ratio;
+        if (r < minr || (r == minr && cc[i] < newt)) {
+          minr = r;
+          newt = cc[i];
+        }
+      }
+    for (uint32_t j = b + R; j < e; j++) {
+      const int32_t c = s.csr_cs[j].x;
+      if (key[c] == mk) {
+        const double r = s.cst[c].ratio;
+        if (r < minr || (r == minr && c < newt)) {
+          minr = r;
+          newt = c;
+        }
+      }
+    }
+  }
+  if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
+    s.vstate[v] = round + 1;
+    s.x[v] = vb;
+    if (t >= 0 && kt != kDead32)
+      atomicAdd(&s.nvote[t], mult_old);
+    for (uint32_t j = b; j < e; j++)
+      push_decrement(s, j, vb, p);
+    return FR_BOUND;
+  }
+  uint32_t sk = kDead32;  // min key over the other constraints of the row
+  int mult_new = 0;
+  uint32_t slot = 0xFFFFFFFFu;  // CSC position of one of v's elements on newt (the smallest)
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    if (cc[i] != newt) {
+      sk = min(sk, kk[i]);
+    } else {
+      mult_new++;
+      slot = min(slot, sl[i]);
+    }
+  }
+  for (uint32_t j = b + R; j < e; j++) {
+    const int2 x = s.csr_cs[j];
+    if (x.x != newt) {
+      sk = min(sk, key[x.x]);
+    } else {
+      mult_new++;
+      slot = min(slot, uint32_t(x.y));
+    }
+  }
+  // (a floor of kDead32 — no other alive constraint, unbounded — is stored as kDead32 - 1: the vote then
+  // moves only when newt itself dies, exactly as before)
+  const uint32_t fl = min(row_floor32(sk, mk, vb, p), kNoVoter - 1u);
+  s.vslot[slot] = fl;
+  if (fl < s.minfl[newt])
+    atomicMin(&s.minfl[newt], fl);
+  if (newt == t)
+    return FR_STAY;
+  if (t >= 0 && kt != kDead32)
+    atomicAdd(&s.nvote[t], mult_old);
+  atomicSub(&s.nvote[newt], mult_new);
+  s.rtgt[0][v] = newt;
+  return FR_MOVE;
+}
+
+// Round 0: every variable votes.
+__global__ void __launch_bounds__(kBlock) fr_vote_all(Dev s) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock)
+    fr_revote<8>(s, int(v), kUnvoted, s.var_ptr[v], s.var_ptr[v + 1], 0);
+}
+
+// Rounds >= 1: the variables fr_update queued in workgroup b's segment (the CSC range of its constraints).
+// Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
+__global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      s.ctl[CTL_DONE] = 1;
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_PALIVE0 + (round & 1)] = 0;  // this round's fr_update raises it
+  const int n = s.fq_n[blockIdx.x];
+  if (n == 0)
+    return;
+  const uint32_t seg = s.cnst_ptr[int64_t(blockIdx.x) * kFB];
+  for (int i = threadIdx.x; i < n; i += kFB) {
+    const unsigned long long a = s.fq_a[seg + i], rw = s.fq_b[seg + i];
+    const int o = fr_revote<8>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw), uint32_t(rw >> 32), round);
+    if (s.vstat) {
+      fr_diag(s, round, 6, true);
+      fr_diag(s, round, 4, o == FR_MOVE);
+      fr_diag(s, round, 7, o == FR_BOUND);
+    }
+  }
+}
+
+// Ready test + saturation: workgroup b tests its kFB constraints; the ready ones are collected in LDS with
+// the prefix of their 64-element CSC chunks and the workgroup's waves take the chunks round-robin
+// (sat_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
+__global__ void __launch_bounds__(kFB) fr_sat(Dev s, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ SatLds<kFB, kFB> L;
+  constexpr int NBW = kFB / kWave;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int64_t c = int64_t(blockIdx.x) * kFB + threadIdx.x;
+  bool rdy = false;
+  int nch = 0;
+  if (c < s.nC && s.key32[c] != kDead32 && s.nvote[c] == 0) {
+    rdy = true;
+    nch = int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave);
+    if (s.vstat)
+      atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 5, 1);
+    if (nch > kFrBigCh) {  // rare (fat-tree core links): spread over the grid by fr_sat_big
+      s.ready[atomicAdd(&s.ctl[CTL_NREADY], 1)] = int32_t(c);
+      rdy = false;
+      nch = 0;
+    }
+  }
+  int ia = rdy, ib = nch;  // wave inclusive scans of (ready, chunks)
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int xa = __shfl_up(ia, o, kWave), xb = __shfl_up(ib, o, kWave);
+    if (lane >= o) {
+      ia += xa;
+      ib += xb;
+    }
+  }
+  if (lane == kWave - 1) {
+    L.wa[w] = ia;
+    L.wb[w] = ib;
+  }
+  __syncthreads();
+  int oa = 0, ob = 0, ta = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < NBW; k++) {
+    oa += k < w ? L.wa[k] : 0;
+    ob += k < w ? L.wb[k] : 0;
+    ta += L.wa[k];
+    tb += L.wb[k];
+  }
+  if (rdy) {
+    L.rc[oa + ia - 1] = int32_t(c);
+    L.rr[oa + ia - 1] = ob + ib - nch;
+  }
+  if (threadIdx.x == 0) {
+    L.na = ta;
+    L.nb = tb;
+    if (ta)
+      s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
+  }
+  __syncthreads();
+  if (ta)  // workgroup-uniform
+    sat_flush<kFB, kFB>(s, round, L);
+}
+
+// The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
+// constraint over the whole grid, wave k taking chunks k, k + kFrBigWaves, ...
+__global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round) {
+  if (s.ctl[CTL_DONE])
+    return;
+  const int nb = s.ctl[CTL_NREADY];
+  if (nb == 0)
+    return;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_LASTR] = round;
+  __shared__ int wpre[kBlock / kWave][kWave];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+  for (int64_t g = wave; g < int64_t(nb) * kFrBigWaves; g += nwaves) {
+    const int32_t c = s.ready[g / kFrBigWaves];
+    const int k = int(g % kFrBigWaves);
+    const double r = ld_rlx(&s.cst[c].ratio);
+    const uint32_t ce = s.cnst_ptr[c + 1];
+    const bool dup = s.cdup[c] != 0;
+    for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += kFrBigWaves * kWave)
+      saturate_chunk(s, c, r, base, ce, round, lane, wpre[w], dup);
+    if (k == 0 && lane == 0)
+      s.ctouch[c] = 2;
+  }
+}
+
+// Constraint update (maxmin.cpp:603-658; the arithmetic of update_groups) + slot scan.  Workgroup b owns
+// constraints [b * kFB, (b + 1) * kFB), one per thread.  A touched constraint whose new key reached its minfl
+// (or that left the light table) has its slots read — all such constraints of a wave flattened over the wave,
+// kFrScanU x 64 slots in flight — and the voters whose floor the key reached are queued for fr_vote in the
+// workgroup's segment (fq_a: variable | old target << 32, fq_b: CSR row), their slots cleared; minfl becomes
+// the min floor of the voters that stay.
+constexpr int kFrScanU = 4;
+
+__global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ int qn;
+  __shared__ int pre[kFB / kWave][kWave];
+  __shared__ uint32_t mf[kFB];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (threadIdx.x == 0)
+    qn = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    s.ctl[CTL_ROUNDS] += 1;
+    s.ctl[CTL_NREADY] = 0;  // fr_sat_big's list of the next round
+  }
+  const int64_t gbase = int64_t(blockIdx.x) * kFB + int64_t(w) * kWave;
+  const int64_t c = gbase + lane;
+  const bool in = c < s.nC;
+  const uint32_t okey = in ? s.key32[c] : kDead32;
+  const unsigned tf = in ? unsigned(s.ctouch[c]) : 0u;  // 1 = received decrements, 2 = saturated this round
+  const bool live0 = okey != kDead32;
+  const bool sat = live0 && tf == 2;
+  const bool live = live0 && !sat;
+  const bool tch = live && tf == 1;
+  unsigned long long qx = 0, qy = 0, qz = 0;
+  double rem = 0.0, use = 0.0, bnd = 0.0;
+  int32_t ce = 0, nv = 0;
+  uint32_t mfl = kNoVoter;
+  uint32_t cb = 0, cend = 0;
+  if (tch) {
+    const CstRec* rec = s.cst + c;
+    qx = rec->drem;
+    qy = rec->duse;
+    qz = rec->dcnt;
+    rem = rec->rem;
+    use = rec->use;
+    bnd = rec->bound;
+    ce = s.cexp[c];
+    nv = s.nvote[c];
+    mfl = s.minfl[c];
+    cb = s.cnst_ptr[c];
+    cend = s.cnst_ptr[c + 1];
+  }
+  const bool fat = tch && (ce & kCexpFat);
+  // FATPIPE: recompute only when a removed element reached the usage (fat_bits in duse)
+  const bool fre = fat && !(__longlong_as_double((long long)qy) < use);
+  double fuse = use;
+  unsigned long long fm = __ballot(fre);
+  while (fm) {  // wave-uniform: FATPIPE usage over the still-unfixed elements (maxmin.cpp:625-658)
+    const int l = __ffsll((long long)fm) - 1;
+    fm &= fm - 1;
+    const int64_t cl = gbase + l;
+    const uint32_t b = s.cnst_ptr[cl], e = s.cnst_ptr[cl + 1];
+    double m = 0.0;
+    for (uint32_t j = b + lane; j < e; j += kWave)
+      if (!(s.x[s.csc_v[j]] > 0))
+        m = fmax(m, s.csc_u[j]);
+    m = wave_max(m);
+    if (lane == l)
+      fuse = m;
+  }
+  uint32_t nk = okey;
+  bool alive = false;
+  if (sat) {
+    s.key32[c] = kDead32;
+    s.cexp[c] = kCexpDead;
+    s.ctouch[c] = 0;
+    s.cst[c].ratio = dinf();
+    nk = kDead32;
+  } else if (live) {
+    if (!tch) {
+      alive = true;
+    } else {
+      CstRec* rec = s.cst + c;
+      s.ctouch[c] = 0;
+      rec->drem = rec->duse = rec->dcnt = 0;
+      s.nvote[c] = nv - int(qz);
+      double r0 = rem, u0;
+      if (!fat) {
+        u0 = use - dec_val(qy, cexp_use(ce));
+        r0 -= dec_val(qx, cexp_rem(ce));
+        if (r0 < bnd * prec)
+          r0 = 0.0;
+        if (u0 < prec)
+          u0 = 0.0;
+      } else {
+        u0 = fuse;
+      }
+      rec->rem = r0;
+      rec->use = u0;
+      if (!(u0 > prec) || !(r0 > bnd * prec)) {
+        rec->ratio = dinf();
+        s.key32[c] = kDead32;
+        s.cexp[c] = kCexpDead;
+        nk = kDead32;
+      } else {
+        const double r = r0 / u0;
+        rec->ratio = r;
+        nk = ratio_key32(r);
+        s.key32[c] = nk;
+        alive = true;
+      }
+    }
+  }
+  // ---- slot scan of the touched constraints whose key reached a registered floor ----
+  const bool scan = tch && mfl != kNoVoter && nk >= mfl;
+  const int len = scan ? int(cend - cb) : 0;
+  if (s.vstat) {
+    fr_diag(s, round, 0, tch);
+    fr_diag(s, round, 1, scan);
+    fr_diag_n(s, round, 2, len);
+  }
+  int incl = len;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int x = __shfl_up(incl, o, kWave);
+    if (lane >= o)
+      incl += x;
+  }
+  const int total = __shfl(incl, kWave - 1, kWave);
+  pre[w][lane] = incl - len;
+  mf[threadIdx.x] = kNoVoter;
+  __syncthreads();  // (qn, pre, mf)
+  const uint32_t seg = s.cnst_ptr[int64_t(blockIdx.x) * kFB];
+  for (int f0 = 0; f0 < total; f0 += kFrScanU * kWave) {  // wave-uniform
+    int ol[kFrScanU];
+    uint32_t jj[kFrScanU];
+    uint32_t fl[kFrScanU];
+#pragma unroll
+    for (int u = 0; u < kFrScanU; u++) {
+      const int f = f0 + u * kWave + lane;
+      int o = 0;  // owner lane: last lane with pre <= f
+#pragma unroll
+      for (int step = kWave / 2; step > 0; step >>= 1)
+        if (pre[w][o + step] <= f)
+          o += step;
+      ol[u] = o;
+      jj[u] = uint32_t(__shfl(int(cb), o, kWave)) + uint32_t(f - pre[w][o]);
+      fl[u] = f < total ? s.vslot[jj[u]] : kNoVoter;
+    }
+#pragma unroll
+    for (int u = 0; u < kFrScanU; u++) {
+      const uint32_t okk = uint32_t(__shfl(int(nk), ol[u], kWave));
+      const bool q = fl[u] != kNoVoter && fl[u] <= okk;
+      if (fl[u] != kNoVoter && !q)
+        atomicMin(&mf[w * kWave + ol[u]], fl[u]);
+      const unsigned long long m = __ballot(q);
+      if (s.vstat && m && lane == 0)
+        atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 3, __popcll(m));
+      int base = 0;
+      if (m) {
+        if (lane == 0)
+          base = atomicAdd(&qn, __popcll(m));
+        base = __shfl(base, 0, kWave);
+      }
+      if (q) {
+        const uint32_t j = jj[u];
+        const int pos = base + __popcll(m & ((1ull << lane) - 1));
+        s.fq_a[seg + pos] = (unsigned long long)uint32_t(s.csc_v[j]) |
+                            ((unsigned long long)uint32_t(gbase + ol[u]) << 32);
+        s.fq_b[seg + pos] = s.csc_row[j];
+        s.vslot[j] = kNoVoter;
+      }
+    }
+  }
+  __syncthreads();  // (mf, qn)
+  if (scan)
+    s.minfl[c] = mf[threadIdx.x];
+  const bool any_alive = __syncthreads_or(alive);
+  if (threadIdx.x == 0) {
+    s.fq_n[blockIdx.x] = qn;
+    if (any_alive)
+      s.ctl[CTL_PALIVE0 + (round & 1)] = 1;
+  }
+  if (__syncthreads_or(tch || sat) && threadIdx.x == 0)
+    s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
+}
+
+}  // namespace lmmdev

@@ -11,6 +11,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -20,6 +22,7 @@
 #include "lmm_step_kernels.hpp"
 #include "lmm_maxmin_kernels.hpp"
 #include "lmm_persist_kernels.hpp"
+#include "lmm_frontier_kernels.hpp"
 #include "lmm_batch_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
 #include "lmm_cc_kernels.hpp"
@@ -94,6 +97,7 @@ struct lmmhip_ctx {
   bool persist_prof = false;    // record barrier timestamps in the persistent launch
   long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
   int persist_grid = 0;  // workgroups of the persistent launch (one per CU, checked at first use)
+  int64_t persist_fallbacks = 0;  // persistent solves re-run by the multi-launch engine (barrier timeout)
   bool ev1_done = false;  // the solve recorded ev1 itself (right behind its last kernel)
   // block-diagonal batch (lmmhip_set_batch): system offsets on the device, largest system
   int64_t bt_n = 0;
@@ -147,6 +151,11 @@ struct lmmhip_ctx {
   Scr fb_longl;                                   // solve_fair: the long shared constraints (fb_long_list)
   Scr fbp_k0, fbp_k1, fbp_v0, fbp_v1, fbp_tmp, fbp_perm, fbp_cscvp, fbp_mu;  // solve_fair: locality order (fb_perm)
   bool fb_perm_ok = false;                        // the order matches the uploaded system
+  // frontier engine (lmm_frontier_kernels.hpp): CSR -> CSC map of the uploaded structure, vote slots, floors,
+  // re-vote queue; the map and the largest CSC degree are rebuilt after every structural change
+  Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
+  bool fr_map_ok = false;
+  int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
       rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch, rs_rowpen, rs_posd, rs_cls, rs_lanyc;
 };
@@ -246,7 +255,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc})
@@ -432,6 +441,7 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
 static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, bool elem_done = false) {
   Dev& d = c->d;
   c->fb_perm_ok = false;
+  c->fr_map_ok = false;
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
   const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
@@ -1065,6 +1075,7 @@ int lmmhip_set_profiling(lmmhip_ctx* c, int on) {
 
 static int solve_maxmin(lmmhip_ctx* c, double prec);
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec);
+static int solve_maxmin_frontier(lmmhip_ctx* c, double prec);
 static int solve_fair(lmmhip_ctx* c, double prec);
 static int engine_of(const lmmhip_ctx* c);
 static bool batch_fits(const lmmhip_ctx* c);
@@ -1102,6 +1113,7 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   int rc = kind == LMMHIP_KIND_FAIR_BOTTLENECK ? solve_fair(c, precision)
            : batch_fits(c)                             ? solve_maxmin_batch(c, precision)
            : engine_of(c) == LMMHIP_ENGINE_PERSISTENT ? solve_maxmin_persist(c, precision)
+           : engine_of(c) == LMMHIP_ENGINE_FRONTIER   ? solve_maxmin_frontier(c, precision)
                                                      : solve_maxmin(c, precision);
   if (rc)
     return rc;
@@ -1346,19 +1358,100 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   return poll_ctl(c);  // (the queued tail has run: final words for the stats)
 }
 
+// Frontier engine (lmm_frontier_kernels.hpp): three launches per round, work proportional to the touched
+// constraints and the moving votes.  Slots: 2 fr_vote, 4 fr_sat (+ fr_sat_big), 5 fr_update, 6 the per-chunk
+// control-word copy; 0 / 1 init.
+static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
+  Dev d = c->d;  // (a copy: the frontier's buffers stay out of the context's Dev, which the other engines use)
+  const int64_t nnz = std::max<int64_t>(d.nnz, 1);
+  const int nblk = int((int64_t(d.nC) + kFB - 1) / kFB);  // fr_update / fr_vote / fr_sat workgroups
+  int2* cs = nullptr;
+  int32_t* md = nullptr;
+  int rc = scratch(c, c->fr_c2s, nnz, &cs);
+  rc = rc ? rc : scratch(c, c->fr_pvb, std::max<int64_t>(d.nV, 1), &d.pvb);
+  rc = rc ? rc : scratch(c, c->fr_slot, nnz, &d.vslot);
+  rc = rc ? rc : scratch(c, c->fr_minfl, std::max<int64_t>(d.nC, 1), &d.minfl);
+  rc = rc ? rc : scratch(c, c->fr_key, std::max<int64_t>(d.nC, 1), &d.key32);
+  rc = rc ? rc : scratch(c, c->fr_qa, nnz, &d.fq_a);
+  rc = rc ? rc : scratch(c, c->fr_qb, nnz, &d.fq_b);
+  rc = rc ? rc : scratch(c, c->fr_qn, int64_t(nblk) + 1, &d.fq_n);
+  rc = rc ? rc : scratch(c, c->fr_md, 1, &md);
+  if (rc)
+    return rc;
+  d.csr_cs = cs;
+  if (!c->fr_map_ok) {  // once per uploaded structure
+    HIPCHK(hipMemsetAsync(md, 0, sizeof(int32_t), c->stream));
+    if (d.nnz > 0) {
+      hipLaunchKernelGGL(fr_c2s, dim3(grid_for(d.nC, kBlock / kWave)), dim3(kBlock), 0, c->stream, d, cs, md);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(&c->fr_maxdeg, md, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->fr_map_ok = true;
+  }
+  const bool big = c->fr_maxdeg > kFrBigCh * kWave;
+  const int gC4 = grid_for(d.nC, kBlock / kWave);
+  LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
+  LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
+  if (d.nnz > 0)
+    HIPCHK(hipMemsetAsync(d.vslot, 0xFF, sizeof(uint32_t) * size_t(d.nnz), c->stream));  // kNoVoter
+  if (d.nC > 0)
+    HIPCHK(hipMemsetAsync(d.minfl, 0xFF, sizeof(uint32_t) * size_t(d.nC), c->stream));
+  const int64_t max_rounds = int64_t(d.nV) + 2;  // every round fixes a variable (progress)
+  int64_t r = 0;
+  // pipelined termination polls, as solve_maxmin: chunk k's control words land in a pinned slot behind an
+  // event while chunk k + 1 is queued; rounds queued after the last one return at once (CTL_DONE)
+  int chunk = 2, slot = 0;
+  bool pending = false;
+  int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
+  int32_t* hcd[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; k++)
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
+  const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
+  for (;;) {
+    for (int k = 0; k < chunk; k++, r++) {
+      if (r == 0)
+        LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
+      else
+        LAUNCH(2, r, fr_vote, nblk, kFB, d, int(r));
+      LAUNCH(4, r, fr_sat, nblk, kFB, d, int(r));
+      if (big)
+        LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r));
+      LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec);
+    }
+    LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
+    HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
+    if (pending) {
+      HIPCHK(hipEventSynchronize(c->ev_poll[slot ^ 1]));
+      if (hc[slot ^ 1][CTL_DONE])
+        break;
+    }
+    pending = true;
+    slot ^= 1;
+    if (r > max_rounds)
+      return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
+    if (chunk < 16)
+      chunk *= 2;
+  }
+  return poll_ctl(c);
+}
+
 static int engine_of(const lmmhip_ctx* c) {
-  // the profiling mode times every phase launch: it runs the multi-launch engine
-  if (c->profiling)
-    return LMMHIP_ENGINE_ROUNDS;
-  // LMMHIP_ENGINE=rounds|persistent overrides the context's engine; "auto" (or any other value, which is
-  // ignored) leaves the context's choice in place
+  // LMMHIP_ENGINE=rounds|persistent|frontier overrides the context's engine; "auto" (or any other value,
+  // which is ignored) leaves the context's choice in place
   const char* e = std::getenv("LMMHIP_ENGINE");
+  int eng = c->engine;
   if (e && std::strcmp(e, "rounds") == 0)
-    return LMMHIP_ENGINE_ROUNDS;
+    eng = LMMHIP_ENGINE_ROUNDS;
   if (e && std::strcmp(e, "persistent") == 0)
-    return LMMHIP_ENGINE_PERSISTENT;
-  if (c->engine != LMMHIP_ENGINE_AUTO)
-    return c->engine;
+    eng = LMMHIP_ENGINE_PERSISTENT;
+  if (e && std::strcmp(e, "frontier") == 0)
+    eng = LMMHIP_ENGINE_FRONTIER;
+  // the profiling mode times every phase launch: a multi-launch engine
+  if (c->profiling)
+    return eng == LMMHIP_ENGINE_FRONTIER ? LMMHIP_ENGINE_FRONTIER : LMMHIP_ENGINE_ROUNDS;
+  if (eng != LMMHIP_ENGINE_AUTO)
+    return eng;
   // AUTO (measured): one launch per solve where the host round-trips and launches of the
   // round chain dominate (small systems: a tie at C4, 1e5 variables, and ahead below); the round chain
   // above, where the kernel boundaries (~1.5 us) are cheaper than grid barriers (~4 us) and per-launch
@@ -1369,7 +1462,32 @@ static int engine_of(const lmmhip_ctx* c) {
 // One persistent launch per solve (lmm_persist_kernels.hpp): one 1024-thread workgroup per CU, all
 // resident (the occupancy query admits exactly one per CU); every barrier wait is bounded, so a fault in
 // the protocol ends the launch with CTL_ERR instead of hanging the GPU.
+// Persistent launches are serialised per device, process-wide: a persistent grid needs every CU for one
+// workgroup at once (its barriers rely on co-residency), so two of them running side by side — two Systems
+// on two streams, or two threads — could each hold part of the chip and wait on the other.  Each persistent
+// launch waits (on its own stream, no host blocking) for the previous one's completion event.
+namespace {
+std::mutex g_persist_mu;
+std::map<int, hipEvent_t> g_persist_last;  // device -> completion event of its last persistent launch
+}  // namespace
+
+static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec);
+
+// A barrier wait that times out (CTL_ERR 1: the grid was not co-resident — a long kernel of another
+// process or library held CUs for seconds) is not an error of the system: the solve is re-run by the
+// multi-launch engine, whose results are bit-identical (tests/test_gpu_engines.py).
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
+  c->h_ctl[CTL_ERR] = 0;
+  const int rc = solve_maxmin_persist_once(c, prec);
+  if (rc != LMMHIP_E_HIP || c->h_ctl[CTL_ERR] != 1)
+    return rc;
+  c->persist_fallbacks += 1;
+  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+  c->ev1_done = false;
+  return solve_maxmin(c, prec);
+}
+
+static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec) {
   Dev d = c->d;
   d.vstat = nullptr;
   const bool bits = int64_t(d.nC) <= int64_t(kPBitWords) * 64;
@@ -1409,10 +1527,19 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
   // bounded (CTL_ERR) should they not be.  hipLaunchCooperativeKernel (LMMHIP_PERSIST_COOP=1) runs the same
   // kernel through the runtime's device-wide cooperative queue, whose teardown at process exit crashed inside
   // the HSA runtime under rocprofv3 (SIGSEGV in libamdhip64's exit handler).
-  if (env_int("LMMHIP_PERSIST_COOP", 0))
-    HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
-  else
-    HIPCHK(hipLaunchKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
+  {
+    std::lock_guard<std::mutex> lk(g_persist_mu);
+    hipEvent_t& last = g_persist_last[c->device];
+    if (!last)
+      HIPCHK(hipEventCreateWithFlags(&last, hipEventDisableTiming));
+    else
+      HIPCHK(hipStreamWaitEvent(c->stream, last, 0));  // the previous persistent grid has drained
+    if (env_int("LMMHIP_PERSIST_COOP", 0))
+      HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
+    else
+      HIPCHK(hipLaunchKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
+    HIPCHK(hipEventRecord(last, c->stream));
+  }
   c->stats.kernel_launches[2] += 1;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->ev1_done = true;
@@ -1732,10 +1859,18 @@ int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_
   return 0;
 }
 
+int lmmhip_engine_fallbacks(lmmhip_ctx* c, int64_t* n) {
+  if (!c || !n)
+    return fail(LMMHIP_E_ARG, "null argument");
+  *n = c->persist_fallbacks;
+  return 0;
+}
+
 int lmmhip_ctx_set_engine(lmmhip_ctx* c, int engine) {
   if (!c)
     return fail(LMMHIP_E_ARG, "null context");
-  if (engine != LMMHIP_ENGINE_PERSISTENT && engine != LMMHIP_ENGINE_ROUNDS && engine != LMMHIP_ENGINE_AUTO)
+  if (engine != LMMHIP_ENGINE_PERSISTENT && engine != LMMHIP_ENGINE_ROUNDS && engine != LMMHIP_ENGINE_AUTO &&
+      engine != LMMHIP_ENGINE_FRONTIER)
     return fail(LMMHIP_E_ARG, "unknown maxmin engine");
   c->engine = engine;
   return 0;
@@ -2288,6 +2423,8 @@ int lmmhip_components(lmmhip_ctx* c, int32_t* var_label, int32_t* cnst_label, in
   *ncomp = 0;
   if (n == 0)
     return 0;
+  if (n > INT32_MAX)  // union-find node ids are int32 (lmm_cc_kernels.hpp)
+    return fail(LMMHIP_E_ARG, "components: variables + constraints exceed 2^31 - 1");
   int32_t *par = nullptr, *out = nullptr;
   int64_t *flag = nullptr, *rank = nullptr;
   if (int rc = scratch(c, c->cc_par, n, &par))

@@ -121,6 +121,8 @@ __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64
       s.nvote[c] = int32_t(e - b);  // no element votes yet
       s.chg[c] = uint16_t(0xFFFF);
       s.key[c] = alive ? ratio_key(r) : uint16_t(kDeadKey);
+      if (s.key32)  // (frontier engine)
+        s.key32[c] = alive ? ratio_key32(r) : kDead32;
       alive_cnt += alive;
     }
   }

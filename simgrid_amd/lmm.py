@@ -144,6 +144,7 @@ SIGNATURES = {
     "lmmhip_ctx_set_stream": (I, [P, P]),
     "lmmhip_ctx_use_own_stream": (I, [P]),
     "lmmhip_ctx_set_engine": (I, [P, I]),
+    "lmmhip_engine_fallbacks": (I, [P, PI64]),
     "lmmhip_persist_profile": (I, [P, I, PI64, I64, PI64]),
     "lmmhip_persist_profile_blocks": (I, [P, PI64, I64, PI64, PI64]),
     "lmmhip_fb_shard_owner": (I, [P, I64, ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD,
@@ -173,6 +174,12 @@ class LmmError(RuntimeError):
     pass
 
 
+def _missing_symbol(name):
+    def stub(*_a, **_k):
+        raise LmmError(f"{name} not exported by the LMM_AMD_LIB build ({LIB_PATH})")
+    return stub
+
+
 def lib():
     """Load liblmm_amd.so (built by __graft_entry__.build() / `make -C simgrid_amd/csrc`)."""
     global _lib
@@ -191,6 +198,7 @@ def lib():
         for name, (res, args) in SIGNATURES.items():
             f = getattr(l, name, None)
             if f is None and os.environ.get("LMM_AMD_LIB"):  # measurement A/B against an older build
+                setattr(l, name, _missing_symbol(name))  # a call fails loudly instead of passing garbage
                 continue
             if f is None:
                 raise LmmError(f"{LIB_PATH} does not export {name}: rebuild it")
@@ -473,12 +481,20 @@ class System:
             raise LmmError(lib().lmm_last_error().decode())
         return c
 
-    ENGINE_PERSISTENT, ENGINE_ROUNDS, ENGINE_AUTO = 0, 1, 2
+    ENGINE_PERSISTENT, ENGINE_ROUNDS, ENGINE_AUTO, ENGINE_FRONTIER = 0, 1, 2, 3
 
     def set_engine(self, engine):
         """Max-min engine of this system's device context (lmmhip_ctx_set_engine): ENGINE_PERSISTENT (one
-        launch per solve), ENGINE_ROUNDS (one launch per phase per round) or ENGINE_AUTO (default)."""
+        launch per solve), ENGINE_ROUNDS (one launch per phase per round), ENGINE_FRONTIER (one launch per
+        phase per round, work proportional to what changed) or ENGINE_AUTO (default)."""
         _check_hip(lib().lmmhip_ctx_set_engine(self.device_ctx(), int(engine)))
+
+    def engine_fallbacks(self):
+        """Persistent solves of this system's context re-run by the multi-launch engine after a grid-barrier
+        timeout (lmmhip_engine_fallbacks)."""
+        n = ct.c_int64()
+        _check_hip(lib().lmmhip_engine_fallbacks(self.device_ctx(), ct.byref(n)))
+        return n.value
 
     def device_values(self):
         """Values of the last solve in the device's dense (CSR) order (lmmhip_get_values)."""

@@ -68,6 +68,16 @@ CASES = {
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
+def test_frontier_engine_bit_identical(name):
+    """The frontier engine (votes registered at their target, lmm_frontier_kernels.hpp) takes the same
+    decisions as the round engine: identical values bit for bit and the same number of rounds."""
+    xf, rf = _values(CASES[name], L.System.ENGINE_FRONTIER)
+    xr, rr = _values(CASES[name], L.System.ENGINE_ROUNDS)
+    assert rf == rr
+    assert xf.tobytes() == xr.tobytes(), float(np.max(np.abs(xf - xr)))
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
 def test_engines_bit_identical(name):
     xp, rp = _values(CASES[name], L.System.ENGINE_PERSISTENT)
     xr, rr = _values(CASES[name], L.System.ENGINE_ROUNDS)
@@ -173,3 +183,53 @@ def test_target_ordered_vote_bit_identical(stress, monkeypatch):
         out.append(_values(_synthetic(100000, 1000000, 1, stress), L.System.ENGINE_ROUNDS))
     assert out[0][1] == out[1][1]
     assert out[0][0].tobytes() == out[1][0].tobytes(), float(np.max(np.abs(out[0][0] - out[1][0])))
+
+
+def test_persistent_engine_concurrent_contexts_and_torch():
+    """The persistent engine's grid barriers need all its workgroups co-resident.  Two Systems (two contexts,
+    two streams) solving at the same time from two host threads, and a solve while torch matmuls run on
+    another stream, must return the round engine's values: persistent launches are serialised per device,
+    and a barrier timeout (a grid that could not become co-resident) re-runs the solve on the round engine
+    instead of failing."""
+    import threading
+
+    import torch
+
+    build = _platform(5000, 2)
+    ref, _ = _values(build, L.System.ENGINE_ROUNDS)
+    systems = []
+    for _ in range(2):
+        s = L.System(False)
+        ids = build(s)
+        s.set_engine(L.System.ENGINE_PERSISTENT)
+        systems.append((s, ids))
+    out, errs = [None, None], []
+
+    def run(k):
+        try:
+            s, ids = systems[k]
+            for _ in range(4):
+                s.solve()
+            out[k] = s.values_of(ids)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=100)
+    assert not errs, errs
+    for k in range(2):
+        assert out[k] is not None and out[k].tobytes() == ref.tobytes()
+    assert systems[0][0].engine_fallbacks() == 0 and systems[1][0].engine_fallbacks() == 0
+    # a persistent solve while torch kernels occupy the chip from another stream
+    s, ids = systems[0]
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda")
+    with torch.cuda.stream(side):
+        for _ in range(30):
+            a = torch.tanh(a @ a * 1e-3)
+    s.solve()
+    torch.cuda.synchronize()
+    assert s.values_of(ids).tobytes() == ref.tobytes()
