@@ -231,6 +231,11 @@ int lmmhip_fb_shard_owner(lmmhip_ctx* ctx, int64_t n_own, const int32_t* own_cns
 int lmmhip_fb_shard_begin(lmmhip_ctx* ctx, double precision, int32_t* xnb, double* xmu, int64_t mu_off,
                           double* xrem);
 int lmmhip_fb_shard_step(lmmhip_ctx* ctx, int phase);
+/* After phase 1 of a round (multi-process delta exchange of mu): the (position in xmu, mu) pairs of this
+ * shard's variables listed at the round's start — the only mu values that moved (every variable in round 0).
+ * pos / mu / count are DEVICE buffers on the context's stream (pos and mu hold up to n_var entries; *count must
+ * be zeroed before; it receives the number of pairs).  The other ranks scatter the pairs into their xmu. */
+int lmmhip_fb_shard_pack_mu(lmmhip_ctx* ctx, int32_t* pos, double* mu, int32_t* count);
 int lmmhip_fb_shard_poll(lmmhip_ctx* ctx, int* done, int64_t* rounds); /* synchronises the stream */
 /* Work of the last FairBottleneck solve (one context, or this shard's part), summed over its rounds — the
  * per-round sweeps of fair_bottleneck.cpp:59-144 that SURVEY.md §8(d) prices at 36 B per element + 32 B per

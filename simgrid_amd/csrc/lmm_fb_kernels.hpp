@@ -884,6 +884,26 @@ __global__ void __launch_bounds__(kBlock) fbo_put_mu(Dev s, FbOwner o) {
     o.xmu[o.mu_off + v] = s.vtmp[v];
 }
 
+// phase 1 tail, multi-process delta exchange (multi.py _fb_rounds): the (position in xmu, mu) pairs of this
+// shard's variables listed at the round's start (vstb; every variable in round 0) — the only mu values that
+// changed this round: a delisted variable's mu is constant (fair_bottleneck.cpp:89-105 runs over the list
+// only).  Appended in any order (one atomic per wave on *cnt, zeroed by the caller); the receiving ranks
+// scatter them into their copy of xmu.
+__global__ void __launch_bounds__(kBlock) fbo_pack_mu(Dev s, FbOwner o, int all, int32_t* pos, double* mu,
+                                                      int32_t* cnt) {
+  if (s.ctl[CTL_DONE])
+    return;
+  for (int64_t b = int64_t(blockIdx.x) * kBlock; b < s.nV; b += int64_t(gridDim.x) * kBlock) {  // wave-uniform
+    const int64_t v = b + threadIdx.x;
+    const bool listed = v < s.nV && (all || ((s.vstb[v >> 5] >> (v & 31)) & 1u));
+    const int k = wave_append(listed, cnt);
+    if (listed) {
+      pos[k] = int32_t(o.mu_off + v);
+      mu[k] = s.vtmp[v];
+    }
+  }
+}
+
 // phase 2a: increments of the owned listed constraints' elements (every element: the gathered mu of a
 // delisted variable is its last one), one wave per chunk
 __global__ void __launch_bounds__(kBlock) fbo_acc(Dev s, FbOwner o) {

@@ -1985,6 +1985,18 @@ int lmmhip_fb_shard_step(lmmhip_ctx* c, int phase) {
   return fb_phase(c, phase);
 }
 
+int lmmhip_fb_shard_pack_mu(lmmhip_ctx* c, int32_t* pos, double* mu, int32_t* count) {
+  if (!c || !c->fb_shard)
+    return fail(LMMHIP_E_STATE, "lmmhip_fb_shard_begin first");
+  if (!pos || !mu || !count)
+    return fail(LMMHIP_E_ARG, "null buffer");
+  HIPCHK(hipSetDevice(c->device));
+  Dev& d = c->d;
+  LAUNCH(3, c->fb_round, fbo_pack_mu, grid_for(d.nV, kBlock), kBlock, d, c->fbo, int(c->fb_round == 0), pos, mu,
+         count);
+  return 0;
+}
+
 int lmmhip_fb_work(lmmhip_ctx* c, int64_t* out3) {
   if (!c || !out3)
     return fail(LMMHIP_E_ARG, "null argument");

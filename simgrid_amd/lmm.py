@@ -151,6 +151,7 @@ SIGNATURES = {
                                   ct.POINTER(ct.c_int32), I64, I64]),
     "lmmhip_fb_shard_begin": (I, [P, D, P, P, I64, P]),
     "lmmhip_fb_shard_step": (I, [P, I]),
+    "lmmhip_fb_shard_pack_mu": (I, [P, P, P, P]),
     "lmmhip_fb_shard_poll": (I, [P, PI, PI64]),
     "lmmhip_fb_work": (I, [P, PI64]),
     "lmmhip_components": (I, [P, PI, PI, PI64]),

@@ -298,6 +298,9 @@ class LocalExchange:
     def allgather_(self, buf, n):
         pass
 
+    def gather_pairs_(self, buf, packs):
+        pass  # every shard of the only rank wrote its chunk of buf itself
+
 
 class DistExchange:
     """torch.distributed collectives on numpy data (gloo: CPU tensors, nccl/RCCL: device tensors)."""
@@ -310,6 +313,7 @@ class DistExchange:
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.device = torch.device("cuda", torch.cuda.current_device()) \
             if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        self.wire_bytes = 0  # bytes this rank contributed to the gathers (the FairBottleneck exchange's traffic)
 
     def _reduce(self, x, op):
         import torch
@@ -350,6 +354,7 @@ class DistExchange:
         t = torch.as_tensor(buf) if is_np else buf
         work = t if t.device.type == self.device.type else t.to(self.device)
         mine = work[self.rank * n:(self.rank + 1) * n].clone()
+        self.wire_bytes += mine.numel() * mine.element_size()
         if self.device.type == "cuda":
             self.dist.all_gather_into_tensor(work, mine, group=self.group)
         else:
@@ -358,6 +363,53 @@ class DistExchange:
             work.copy_(torch.cat(parts))
         if work is not t:
             t.copy_(work)
+
+
+    def gather_pairs_(self, buf, packs):
+        """Scatter every rank's (position, value) pairs into `buf` (the gathered mu of the FairBottleneck
+        shards): packs = [(pos, val, count)] of this rank's shards (torch tensors or numpy arrays; count a
+        1-element array / tensor).  Counts all-gathered first, then the pairs padded to the largest count:
+        12 B per listed variable on the wire instead of 8 B per variable of the whole system."""
+        import torch
+
+        dev = self.device
+        lp = len(packs)
+        cnt = torch.tensor([int(c[0]) for _, _, c in packs], dtype=torch.int64).to(dev) if packs and \
+            not isinstance(packs[0][2], torch.Tensor) else \
+            torch.cat([c.to(dev, torch.int64).reshape(1) for _, _, c in packs])
+        allc = torch.empty(self.world * lp, dtype=torch.int64, device=dev)
+        self._gather(allc, cnt)
+        k = int(allc.max().item()) if allc.numel() else 0
+        if k == 0:
+            return
+        spos = torch.full((lp * k,), -1, dtype=torch.int32, device=dev)
+        sval = torch.zeros(lp * k, dtype=torch.float64, device=dev)
+        for i, (pos, val, c) in enumerate(packs):
+            n = int(c[0])
+            if n:
+                spos[i * k:i * k + n] = torch.as_tensor(pos[:n]).to(dev, torch.int32)
+                sval[i * k:i * k + n] = torch.as_tensor(val[:n]).to(dev, torch.float64)
+        rpos = torch.empty(self.world * lp * k, dtype=torch.int32, device=dev)
+        rval = torch.empty(self.world * lp * k, dtype=torch.float64, device=dev)
+        self._gather(rpos, spos)
+        self._gather(rval, sval)
+        ok = rpos >= 0
+        idx, vals = rpos[ok].long(), rval[ok]
+        if isinstance(buf, torch.Tensor):
+            buf[idx.to(buf.device)] = vals.to(buf.device)
+        else:
+            buf[idx.cpu().numpy()] = vals.cpu().numpy()
+
+    def _gather(self, out, mine):
+        import torch
+
+        self.wire_bytes += mine.numel() * mine.element_size()
+        if self.device.type == "cuda":
+            self.dist.all_gather_into_tensor(out, mine, group=self.group)
+        else:
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            self.dist.all_gather(parts, mine, group=self.group)
+            out.copy_(torch.cat(parts))
 
 
 def next_event_date(local_min, exchange):
@@ -523,6 +575,22 @@ class DeviceFbShard:
     def step(self, phase):
         self._check(self.L.lmmhip_fb_shard_step(self.ctx, phase))
 
+    def pack_mu(self):
+        """(pos, mu, count) device tensors: this shard's variables listed at the round's start and their new mu
+        (lmmhip_fb_shard_pack_mu), for the delta exchange of mu."""
+        import torch
+
+        if not hasattr(self, "_dpos"):
+            with torch.cuda.stream(self.stream):
+                self._dpos = torch.empty(max(self.n, 1), dtype=torch.int32, device="cuda")
+                self._dmu = torch.empty(max(self.n, 1), dtype=torch.float64, device="cuda")
+                self._dcnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        with torch.cuda.stream(self.stream):
+            self._dcnt.zero_()
+        self._check(self.L.lmmhip_fb_shard_pack_mu(self.ctx, ct.c_void_p(self._dpos.data_ptr()),
+                                                   ct.c_void_p(self._dmu.data_ptr()), ct.c_void_p(self._dcnt.data_ptr())))
+        return self._dpos, self._dmu, self._dcnt
+
     def poll(self):
         done, rounds = ct.c_int(), ct.c_int64()
         self._check(self.L.lmmhip_fb_shard_poll(self.ctx, ct.byref(done), ct.byref(rounds)))
@@ -567,8 +635,13 @@ def fb_solve_sharded(shards, exchange, gather, poll_every=16):
     return _fb_rounds(shards, exchange, gather, poll_every)
 
 
+FB_DELTA = True  # multi-process FairBottleneck: ship only the listed variables' mu after round 0 (measurement knob)
+
+
 def _fb_rounds(shards, exchange, gather, poll_every):
     lp = len(shards)
+    # a multi-process exchange ships only the listed variables' mu after round 0 (all shards must pack)
+    delta = FB_DELTA and isinstance(exchange, DistExchange) and all(hasattr(sh, "pack_mu") for sh in shards)
     max_rounds = 64 * (gather.xmu.shape[0] + gather.xrem.shape[0]) + 4096
     rounds = 0
     while True:
@@ -583,7 +656,10 @@ def _fb_rounds(shards, exchange, gather, poll_every):
                 sh.xnb[...] = acc
             for sh in shards:
                 sh.step(1)
-            exchange.allgather_(gather.xmu, lp * gather.Pv)
+            if rounds == 0 or not delta:  # round 0: every mu is new
+                exchange.allgather_(gather.xmu, lp * gather.Pv)
+            else:  # later rounds: only the listed variables' mu moved (fair_bottleneck.cpp:89-105)
+                exchange.gather_pairs_(gather.xmu, [sh.pack_mu() for sh in shards])
             for sh in shards:
                 sh.step(2)
             exchange.allgather_(gather.xrem, lp * gather.Pc)

@@ -63,6 +63,7 @@ class NumpyFbShard:
             b = self.vbound > 0
             inc[b] = np.minimum(inc[b], self.vbound[b] - self.x[b])
             lst = self.listed.copy()
+            self.lst_start = lst
             self.mu[lst] = inc[lst]
             self.x[lst] += inc[lst]
             drop = lst & (self.x == self.vbound)
@@ -95,6 +96,12 @@ class NumpyFbShard:
             erased = upd & (self.rem <= 0.0)
             self.inlist[erased] = False
             self.listed[rows[erased[cols]]] = False
+
+    def pack_mu(self):
+        """(positions in xmu, mu, [count]) of the variables listed at the round's start (lmmhip_fb_shard_pack_mu)."""
+        lst = getattr(self, "lst_start", np.zeros(self.nv, bool)) if not self.done else np.zeros(self.nv, bool)
+        v = np.flatnonzero(lst)
+        return (self.mu_off + v).astype(np.int32), self.mu[v].copy(), np.array([len(v)])
 
     def poll(self):
         return self.done, self.rounds

@@ -123,3 +123,37 @@ def test_gloo_world2_device_components(kind, tmp_path):
     for r in range(2):
         x = np.load(tmp_path / f"x{r}.npy")
         assert np.all(np.abs(x - want) <= np.maximum(ABS_TOL, REL_TOL * np.abs(want))), r
+
+
+def test_rccl_world1_exchange_paths():
+    """RCCL itself (torch.distributed's "nccl" backend = RCCL on ROCm), in a world-size-1 group on this GPU:
+    DistExchange's device branch — all_reduce and all_gather_into_tensor of device tensors on the shard
+    stream, ordered with the solver's kernels through lmmhip_ctx_set_stream — drives the constraint-owner
+    sharded FairBottleneck (2 local shards) to the oracle's bytes, and the component-sharded max-min solve and
+    the next-event all-reduce(MIN) to the LocalExchange results."""
+    import torch
+    import torch.distributed as dist
+
+    from tests.test_multi import _free_port, fb_pair, oracle_dense_values, sharded_fb_values
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        ex = M.DistExchange()
+        assert ex.device.type == "cuda"
+        s, o, ovars = fb_pair(seed=6)
+        f = M.export_flat(s)
+        shards = []
+        x, _ = sharded_fb_values(f, ex, 2, device_shard_maker(shards), device=True)
+        for sh in shards:
+            sh.close()
+        want = oracle_dense_values(o, ovars, f)
+        assert x.tobytes() == want.tobytes(), int(np.count_nonzero(x != want))
+        s2, _, _ = build_pair(0)
+        f2 = M.export_flat(s2)
+        xr = M.solve_components(f2, 0, ex)
+        xl = M.solve_components(f2, 0, M.LocalExchange())
+        assert xr.tobytes() == xl.tobytes()
+        assert M.next_event_date(0.25, ex) == 0.25 and M.next_event_date(-1.0, ex) == -1.0
+    finally:
+        dist.destroy_process_group()

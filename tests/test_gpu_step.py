@@ -99,3 +99,13 @@ def test_lazy_glue_matches_heap_oracle(model):
             assert np.array_equal(lzs[k], np.array(ost[k])), (step, k)
         assert np.array_equal(lzs["heap_type"], np.array(ost["heap_type"], np.uint8)), step
     assert pops > 0
+
+
+@pytest.mark.parametrize("variant,name", [(1, "surf_usage"), (2, "surf_usage2")])
+def test_surf_usage_device_matches_reference_tesh(variant, name):
+    """The device step glue (act_lazy_update / act_lazy_min / act_lazy_due, lmm_step_kernels.hpp) over the HIP
+    lmm solve replays teshsuite/surf/<name> (Cas01 + CM02, both LAZY, two_hosts_profiles.xml): every
+    next-event date and every done / failed action of the reference's tesh (tests/surf_scenario.py)."""
+    from tests import surf_scenario as SC
+
+    assert SC.run_surf_usage(SC.DeviceBackend(), variant) == SC.expected(name)

@@ -215,8 +215,17 @@ def _fb_worker(rank, world, port, out_dir, seed):
     try:
         s, _, _ = fb_pair(seed)
         f = M.export_flat(s)
-        x, _ = sharded_fb_values(f, M.DistExchange(), 2, numpy_shard)
+        ex = M.DistExchange()
+        x, shards = sharded_fb_values(f, ex, 2, numpy_shard)
         np.save(os.path.join(out_dir, f"fb{rank}.npy"), x)
+        # bytes this rank put on the wire with the delta exchange of mu vs. the full all-gather every round
+        M.FB_DELTA = False
+        ex_full = M.DistExchange()
+        x_full, _ = sharded_fb_values(f, ex_full, 2, numpy_shard)
+        M.FB_DELTA = True
+        assert x_full.tobytes() == x.tobytes()
+        np.save(os.path.join(out_dir, f"wire{rank}.npy"), np.array([ex.wire_bytes, ex_full.wire_bytes,
+                                                                    shards[0].rounds]))
     finally:
         dist.destroy_process_group()
 
@@ -232,3 +241,5 @@ def test_gloo_world2_fb_sharded(tmp_path, seed):
     for r in range(2):
         x = np.load(tmp_path / f"fb{r}.npy")
         assert x.tobytes() == want.tobytes(), (r, int(np.count_nonzero(x != want)))
+        wire, full, rounds = np.load(tmp_path / f"wire{r}.npy")
+        assert rounds >= 2 and 0 < wire < full, (wire, full, rounds)  # rounds > 0 ship listed mu only

@@ -1,5 +1,7 @@
 """Step-glue restatement (oracle/step_oracle.py) on hand-computed cases (CPU).  The device kernels are
 compared with it bit for bit in tests/test_gpu_step.py."""
+import pytest
+
 from oracle import step_oracle as S
 
 
@@ -97,3 +99,23 @@ def test_lazy_pop_is_the_prefix_within_precision():
         top = min(dates)
         want = [(i, S.EV_FINISHED) for i, d in enumerate(dates) if abs(d - now) < 1e-5] if abs(top - now) < 1e-5 else []
         assert got == want
+
+
+@pytest.mark.parametrize("variant,name", [(1, "surf_usage"), (2, "surf_usage2")])
+def test_surf_usage_oracle_matches_reference_tesh(variant, name):
+    """The step oracle (step_oracle.LazyModel over the LMM oracle) replays teshsuite/surf/<name>: Cas01 + CM02,
+    both LAZY, on two_hosts_profiles.xml with its speed / state profiles — every next-event date (0.2, 0.200016,
+    1, 7.32, 10 ... 130, 132.5) and every done / failed action of the reference's tesh (tests/surf_scenario.py,
+    fixture tests/golden/surf_usage.json)."""
+    from tests import surf_scenario as SC
+
+    assert SC.run_surf_usage(SC.OracleBackend(), variant) == SC.expected(name)
+
+
+def test_surf_usage_profiles_restated():
+    """Profile::from_string's event list (Profile.cpp:65-100): deltas to the next event, LOOPAFTER + first date."""
+    from tests import surf_scenario as SC
+
+    pr = SC.golden()["profiles"]
+    assert SC.profile_from_string(pr["trace_B.txt"]) == [[0.0, -1.0], [10.0, 1.0], [10.0, 0.8], [10.0, 0.4]]
+    assert SC.profile_from_string(pr["trace_A_failure.txt"]) == [[1.0, -1.0], [1.0, -1.0], [9.0, 1.0]]
