@@ -303,6 +303,50 @@ __global__ void __launch_bounds__(kBlock) fbp_csc(Dev s) {
     s.csc_vp[j] = s.vperm[s.csc_v[j]];
 }
 
+// Renumbered variables (one context, round 4): the solve runs on a copy of the CSR whose rows are in the
+// locality order of fb_perm (new id n = vperm[old], order[n] = old), so every per-variable pass — the row
+// minima of fb_var_inc, the listed tests of fbk_count, the delisting stores of fbk_unlist — gets the locality
+// the chains' mu gathers already had; the CSC keeps the reference's element order with csc_v -> csc_vp.  The
+// values are the same bytes (every variable's arithmetic is its own); fbr_unperm writes them back in order.
+__global__ void __launch_bounds__(kBlock) fbr_len(Dev s, const int32_t* __restrict__ order, uint32_t* plen) {
+  for (int64_t n = int64_t(blockIdx.x) * kBlock + threadIdx.x; n <= s.nV; n += int64_t(gridDim.x) * kBlock) {
+    if (n == s.nV) {
+      plen[n] = 0;
+      continue;
+    }
+    const int32_t v = order[n];
+    plen[n] = s.var_ptr[v + 1] - s.var_ptr[v];
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) fbr_rows(Dev s, const int32_t* __restrict__ order,
+                                                   const uint32_t* __restrict__ pvp, int32_t* pc, double* pw) {
+  for (int64_t n = int64_t(blockIdx.x) * kBlock + threadIdx.x; n < s.nV; n += int64_t(gridDim.x) * kBlock) {
+    const int32_t v = order[n];
+    const uint32_t b = s.var_ptr[v], e = s.var_ptr[v + 1], o = pvp[n];
+    for (uint32_t j = b; j < e; j++) {
+      pc[o + (j - b)] = s.csr_c[j];
+      pw[o + (j - b)] = s.csr_w[j];
+    }
+  }
+}
+
+// Per solve (penalties and bounds may move between solves): the per-variable inputs in the new order.
+__global__ void __launch_bounds__(kBlock) fbr_vars(Dev s, const int32_t* __restrict__ order, double* ppen,
+                                                   double* pvb) {
+  for (int64_t n = int64_t(blockIdx.x) * kBlock + threadIdx.x; n < s.nV; n += int64_t(gridDim.x) * kBlock) {
+    const int32_t v = order[n];
+    ppen[n] = s.pen[v];
+    pvb[n] = s.vbound[v];
+  }
+}
+
+// After the solve: x[old] = px[vperm[old]] (s: the context's own arrays).
+__global__ void __launch_bounds__(kBlock) fbr_unperm(Dev s, const double* __restrict__ px) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock)
+    s.x[v] = px[s.vperm[v]];
+}
+
 // :107-127 — per chunk of a listed constraint.  FATPIPE: min of w*mu over ALL its elements (the stale mu of
 // variables that already left the list included) -> pacc.  Shared: the increments w * mu in CSC order into
 // fbd (element-parallel, all gathers of the round spread over the chip), which fbk_update_seq then chains

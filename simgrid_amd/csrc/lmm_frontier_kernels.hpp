@@ -115,7 +115,7 @@ __device__ __forceinline__ uint32_t row_floor32(uint32_t sk, uint32_t mk, double
   return fl <= mk ? 0u : fl;
 }
 
-template <int R>
+template <int R, bool kMinfl = true, bool kEarly = true>
 __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b, uint32_t e, int round) {
   const uint32_t* __restrict__ key = s.key32;
   // (a queued variable is alive: votes are registered only by alive variables, and the slot of a variable
@@ -130,10 +130,12 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
     cc[i] = x.x;
     sl[i] = uint32_t(x.y);
   }
-  uint32_t kk[R];
+  uint32_t kk[R], mf[R];  // keys and registered floors of the row's constraints, their loads in flight together
 #pragma unroll
-  for (int i = 0; i < R; i++)
+  for (int i = 0; i < R; i++) {
     kk[i] = cc[i] >= 0 ? key[cc[i]] : kDead32;
+    mf[i] = kMinfl && kEarly && cc[i] >= 0 ? s.minfl[cc[i]] : 0u;
+  }
   uint32_t mk = kDead32;
 #pragma unroll
   for (int i = 0; i < R; i++)
@@ -204,6 +206,7 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
   uint32_t sk = kDead32;  // min key over the other constraints of the row
   int mult_new = 0;
   uint32_t slot = 0xFFFFFFFFu;  // CSC position of one of v's elements on newt (the smallest)
+  uint32_t mfn = kNoVoter;      // newt's minfl as read with the keys (only decreases within this launch)
 #pragma unroll
   for (int i = 0; i < R; i++) {
     if (cc[i] != newt) {
@@ -211,6 +214,7 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
     } else {
       mult_new++;
       slot = min(slot, sl[i]);
+      mfn = kEarly ? mf[i] : kNoVoter;
     }
   }
   for (uint32_t j = b + R; j < e; j++) {
@@ -220,13 +224,16 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
     } else {
       mult_new++;
       slot = min(slot, uint32_t(x.y));
+      mfn = kNoVoter;  // (read with the keys only for the first R elements: always take the atomic)
     }
   }
   // (a floor of kDead32 — no other alive constraint, unbounded — is stored as kDead32 - 1: the vote then
   // moves only when newt itself dies, exactly as before)
   const uint32_t fl = min(row_floor32(sk, mk, vb, p), kNoVoter - 1u);
   s.vslot[slot] = fl;
-  if (fl < s.minfl[newt])
+  if (kMinfl && !kEarly)
+    mfn = s.minfl[newt];
+  if (kMinfl && fl < mfn)
     atomicMin(&s.minfl[newt], fl);
   if (newt == t)
     return FR_STAY;
@@ -237,15 +244,39 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
   return FR_MOVE;
 }
 
-// Round 0: every variable votes.
+// Round 0: every variable votes (the floors' per-constraint minima come after, from fr_minfl_all).
 __global__ void __launch_bounds__(kBlock) fr_vote_all(Dev s) {
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock)
-    fr_revote<8>(s, int(v), kUnvoted, s.var_ptr[v], s.var_ptr[v + 1], 0);
+    fr_revote<8, false>(s, int(v), kUnvoted, s.var_ptr[v], s.var_ptr[v + 1], 0);
+}
+
+// After round 0's vote: minfl[c] = min of the floors registered in c's slots, 16 lanes per constraint (four
+// constraints per wave; one segmented pass over the slots instead of ~nV atomics).
+__global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
+  const int lane = threadIdx.x & (kWave - 1), gl = lane & 15;
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+  for (int64_t c = wave * 4 + lane / 16; c < s.nC; c += nwaves * 4) {  // group-uniform
+    const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
+    uint32_t m = kNoVoter;
+    for (uint32_t j = b + gl; j < e; j += 64) {
+      uint32_t f[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        f[k] = j + 16 * k < e ? s.vslot[j + 16 * k] : kNoVoter;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        m = min(m, f[k]);
+    }
+    m = grp_umin<16>(m);
+    if (gl == 0)
+      s.minfl[c] = m;
+  }
 }
 
 // Rounds >= 1: the variables fr_update queued in workgroup b's segment (the CSC range of its constraints).
 // Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
-__global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round) {
+template <bool kEarly = true> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round) {
   if (s.ctl[CTL_DONE])
     return;
   if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
@@ -261,7 +292,8 @@ __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round) {
   const uint32_t seg = s.cnst_ptr[int64_t(blockIdx.x) * kFB];
   for (int i = threadIdx.x; i < n; i += kFB) {
     const unsigned long long a = s.fq_a[seg + i], rw = s.fq_b[seg + i];
-    const int o = fr_revote<8>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw), uint32_t(rw >> 32), round);
+    const int o = fr_revote<8, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
+                                             uint32_t(rw >> 32), round);
     if (s.vstat) {
       fr_diag(s, round, 6, true);
       fr_diag(s, round, 4, o == FR_MOVE);
@@ -270,16 +302,149 @@ __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round) {
   }
 }
 
-// Ready test + saturation: workgroup b tests its kFB constraints; the ready ones are collected in LDS with
-// the prefix of their 64-element CSC chunks and the workgroup's waves take the chunks round-robin
-// (sat_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
-__global__ void __launch_bounds__(kFB) fr_sat(Dev s, int round) {
+// Saturation of one 64-element CSC chunk of ready constraint c: saturate_chunk's decisions and arithmetic
+// (maxmin.cpp:578-606), with the loads of the chunk issued before its stores and atomics — the claim and the
+// value are stored last (a wave's loads wait for its older stores / atomics): CSC elements -> variable states
+// -> the claimed rows' elements (kFrSatU x 64 in flight) -> their constraints' packed words, then the
+// decrement pushes and the variables' states.  Deferring the claim is safe: ready constraints share no alive
+// variable, and a variable appears once in c's CSC unless c has a duplicate element (cdup: claimed by
+// atomicCAS, as before).
+constexpr int kFrSatU = 8;
+
+__device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t cend,
+                                             int round, int lane, int* pre, bool dup) {
+  const int q = lane & 3;
+  const uint32_t j = j0 + lane;
+  int32_t lv = -1;
+  double lp = 1.0, lx = 0.0;
+  uint32_t rb = 0, re = 0;
+  if (j < cend) {
+    lv = s.csc_v[j];
+    lp = s.csc_p[j];
+    const unsigned long long row = s.csc_row[j];
+    rb = uint32_t(row);
+    re = uint32_t(row >> 32);
+    if (s.vstate[lv] != 0)
+      lv = -1;
+    else if (dup && atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
+      lv = -1;
+  }
+  int len = 0;
+  if (lv >= 0) {
+    lx = r / lp;
+    len = int(re - rb);
+  } else {
+    rb = re = 0;
+  }
+  int incl = len;  // inclusive wave scan of the row lengths
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int t = __shfl_up(incl, o, kWave);
+    if (lane >= o)
+      incl += t;
+  }
+  const int total = __shfl(incl, kWave - 1, kWave);
+  pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
+  __builtin_amdgcn_wave_barrier();
+  for (int f0 = 0; f0 < total; f0 += kFrSatU * kWave) {  // wave-uniform (one pass up to 512 elements)
+    int32_t cc[kFrSatU];
+    int ol[kFrSatU];
+    double ww[kFrSatU];
+#pragma unroll
+    for (int u = 0; u < kFrSatU; u++) {
+      const int f = f0 + u * kWave + lane;
+      int o = 0;  // owner lane: last lane with pre <= f
+#pragma unroll
+      for (int step = kWave / 2; step > 0; step >>= 1)
+        if (pre[o + step] <= f)
+          o += step;
+      ol[u] = o;
+      const uint32_t k = uint32_t(__shfl(int(rb), o, kWave)) + uint32_t(f - pre[o]);
+      cc[u] = f < total ? s.csr_c[k] : -1;
+      ww[u] = f < total ? s.csr_w[k] : 0.0;
+    }
+    int32_t cx[kFrSatU];
+#pragma unroll
+    for (int u = 0; u < kFrSatU; u++)
+      cx[u] = cc[u] >= 0 ? s.cexp[cc[u]] : kCexpDead;  // scales, policy and liveness in one word
+#pragma unroll
+    for (int u = 0; u < kFrSatU; u++) {
+      const double ox = __shfl(lx, ol[u], kWave);
+      const double op = __shfl(lp, ol[u], kWave);
+      bool fat = false;
+      long long a0 = 0, a1 = 0;  // fixed-point decrements (CstRec)
+      int32_t tc = cc[u];
+      if (tc >= 0 && (tc == c || (cx[u] & kCexpDead)))
+        tc = -1;
+      if (tc >= 0) {
+        s.ctouch[tc] = 1;  // receives decrements this round (fr_update reads its record)
+        fat = cx[u] & kCexpFat;
+        a0 = (long long)dec_q(ww[u] * ox, cexp_rem(cx[u]));
+        a1 = fat ? (long long)fat_bits(ww[u] / op) : (long long)dec_q(ww[u] / op, cexp_use(cx[u]));
+      }
+      const int nel = total - f0 - u * kWave;
+#pragma unroll
+      for (int t = 0; t < kWave / 16; t++) {  // each element's pushes by a quad of lanes: one atomic request
+        if (t * 16 >= nel)
+          break;
+        const int e = t * 16 + (lane >> 2);
+        const int ec = __shfl(tc, e, kWave);
+        const int ef = __shfl(int(fat), e, kWave);
+        const long long e0 = __shfl(a0, e, kWave);
+        const long long e1 = __shfl(a1, e, kWave);
+        if (ec >= 0 && q < 3 && (!ef || q == 2))
+          atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
+        if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
+          atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
+      }
+    }
+  }
+  if (lv >= 0) {  // the claim and the value, last
+    if (!dup)
+      s.vstate[lv] = round + 1;
+    s.x[lv] = lx;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// The collected ready constraints' chunks, round-robin over the workgroup's waves (sat_flush with fr_sat_chunk).
+template <int NB, bool kOld>
+__device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L) {
+  constexpr int NBW = NB / kWave;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int ta = L.na, tb = L.nb;
+  for (int g = w; g < tb; g += NBW) {  // wave-uniform
+    int k = 0;  // last collected entry whose first chunk is <= g
+#pragma unroll
+    for (int step = NB / 2; step > 0; step >>= 1)
+      if (k + step < ta && L.rr[k + step] <= g)
+        k += step;
+    const int32_t cc = L.rc[k];
+    const int ch = g - L.rr[k];
+    const double r = ld_rlx(&s.cst[cc].ratio);  // wave-uniform address: keep it off the scalar cache
+    if (kOld)  // (measurement: the multi-launch engine's chunk body)
+      saturate_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
+                     s.cdup[cc] != 0);
+    else
+      fr_sat_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
+                   s.cdup[cc] != 0);
+    if (ch == 0 && lane == 0)
+      s.ctouch[cc] = 2;
+  }
+}
+
+// Ready test + saturation: workgroup b tests its kFS constraints; the ready ones are collected in LDS with
+// the prefix of their 64-element CSC chunks and the workgroup's 16 waves take the chunks round-robin
+// (fr_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
+constexpr int kFS = 1024;
+
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round) {
   if (s.ctl[CTL_DONE])
     return;
-  __shared__ SatLds<kFB, kFB> L;
-  constexpr int NBW = kFB / kWave;
+  __shared__ SatLds<kFS, kFS> L;
+  constexpr int NBW = kFS / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  const int64_t c = int64_t(blockIdx.x) * kFB + threadIdx.x;
+  const int64_t c = int64_t(blockIdx.x) * kFS + threadIdx.x;
   bool rdy = false;
   int nch = 0;
   if (c < s.nC && s.key32[c] != kDead32 && s.nvote[c] == 0) {
@@ -327,7 +492,7 @@ __global__ void __launch_bounds__(kFB) fr_sat(Dev s, int round) {
   }
   __syncthreads();
   if (ta)  // workgroup-uniform
-    sat_flush<kFB, kFB>(s, round, L);
+    fr_flush<kFS, kOld>(s, round, L);
 }
 
 // The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
@@ -351,7 +516,7 @@ __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round) {
     const uint32_t ce = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
     for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += kFrBigWaves * kWave)
-      saturate_chunk(s, c, r, base, ce, round, lane, wpre[w], dup);
+      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre[w], dup);
     if (k == 0 && lane == 0)
       s.ctouch[c] = 2;
   }
@@ -363,7 +528,10 @@ __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round) {
 // kFrScanU x 64 slots in flight — and the voters whose floor the key reached are queued for fr_vote in the
 // workgroup's segment (fq_a: variable | old target << 32, fq_b: CSR row), their slots cleared; minfl becomes
 // the min floor of the voters that stay.
-constexpr int kFrScanU = 4;
+// Every load of the pass is issued before its first store (a wave's loads wait for its older stores and
+// atomics, MI355X_MICROARCH.md `s_waitcnt vmcnt`): constraint state -> slots -> queued variables' rows, then
+// the stores of the new state, the queue and the cleared slots.
+constexpr int kFrScanU = 8;
 
 __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
@@ -424,23 +592,16 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
     if (lane == l)
       fuse = m;
   }
+  // the new state, in registers (stored after the scan's loads)
   uint32_t nk = okey;
   bool alive = false;
+  double r0 = rem, u0 = use, rnew = 0.0;
   if (sat) {
-    s.key32[c] = kDead32;
-    s.cexp[c] = kCexpDead;
-    s.ctouch[c] = 0;
-    s.cst[c].ratio = dinf();
     nk = kDead32;
   } else if (live) {
     if (!tch) {
       alive = true;
     } else {
-      CstRec* rec = s.cst + c;
-      s.ctouch[c] = 0;
-      rec->drem = rec->duse = rec->dcnt = 0;
-      s.nvote[c] = nv - int(qz);
-      double r0 = rem, u0;
       if (!fat) {
         u0 = use - dec_val(qy, cexp_use(ce));
         r0 -= dec_val(qx, cexp_rem(ce));
@@ -451,18 +612,12 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
       } else {
         u0 = fuse;
       }
-      rec->rem = r0;
-      rec->use = u0;
       if (!(u0 > prec) || !(r0 > bnd * prec)) {
-        rec->ratio = dinf();
-        s.key32[c] = kDead32;
-        s.cexp[c] = kCexpDead;
         nk = kDead32;
+        rnew = dinf();
       } else {
-        const double r = r0 / u0;
-        rec->ratio = r;
-        nk = ratio_key32(r);
-        s.key32[c] = nk;
+        rnew = r0 / u0;
+        nk = ratio_key32(rnew);
         alive = true;
       }
     }
@@ -487,7 +642,7 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
   mf[threadIdx.x] = kNoVoter;
   __syncthreads();  // (qn, pre, mf)
   const uint32_t seg = s.cnst_ptr[int64_t(blockIdx.x) * kFB];
-  for (int f0 = 0; f0 < total; f0 += kFrScanU * kWave) {  // wave-uniform
+  for (int f0 = 0; f0 < total; f0 += kFrScanU * kWave) {  // wave-uniform (one pass up to 512 slots)
     int ol[kFrScanU];
     uint32_t jj[kFrScanU];
     uint32_t fl[kFrScanU];
@@ -503,30 +658,54 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
       jj[u] = uint32_t(__shfl(int(cb), o, kWave)) + uint32_t(f - pre[w][o]);
       fl[u] = f < total ? s.vslot[jj[u]] : kNoVoter;
     }
+    bool q[kFrScanU];
+    int32_t qv[kFrScanU];
+    unsigned long long qr[kFrScanU];
+#pragma unroll
+    for (int u = 0; u < kFrScanU; u++) {  // the queued voters' variable and row, loads in flight together
+      const uint32_t okk = uint32_t(__shfl(int(nk), ol[u], kWave));
+      q[u] = fl[u] != kNoVoter && fl[u] <= okk;
+      if (fl[u] != kNoVoter && !q[u])
+        atomicMin(&mf[w * kWave + ol[u]], fl[u]);
+      qv[u] = q[u] ? s.csc_v[jj[u]] : 0;
+      qr[u] = q[u] ? s.csc_row[jj[u]] : 0ull;
+    }
 #pragma unroll
     for (int u = 0; u < kFrScanU; u++) {
-      const uint32_t okk = uint32_t(__shfl(int(nk), ol[u], kWave));
-      const bool q = fl[u] != kNoVoter && fl[u] <= okk;
-      if (fl[u] != kNoVoter && !q)
-        atomicMin(&mf[w * kWave + ol[u]], fl[u]);
-      const unsigned long long m = __ballot(q);
-      if (s.vstat && m && lane == 0)
+      const unsigned long long m = __ballot(q[u]);
+      if (!m)
+        continue;
+      if (s.vstat && lane == 0)
         atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 3, __popcll(m));
       int base = 0;
-      if (m) {
-        if (lane == 0)
-          base = atomicAdd(&qn, __popcll(m));
-        base = __shfl(base, 0, kWave);
-      }
-      if (q) {
-        const uint32_t j = jj[u];
+      if (lane == 0)
+        base = atomicAdd(&qn, __popcll(m));
+      base = __shfl(base, 0, kWave);
+      if (q[u]) {
         const int pos = base + __popcll(m & ((1ull << lane) - 1));
-        s.fq_a[seg + pos] = (unsigned long long)uint32_t(s.csc_v[j]) |
-                            ((unsigned long long)uint32_t(gbase + ol[u]) << 32);
-        s.fq_b[seg + pos] = s.csc_row[j];
-        s.vslot[j] = kNoVoter;
+        s.fq_a[seg + pos] = (unsigned long long)uint32_t(qv[u]) | ((unsigned long long)uint32_t(gbase + ol[u]) << 32);
+        s.fq_b[seg + pos] = qr[u];
+        s.vslot[jj[u]] = kNoVoter;
       }
     }
+  }
+  // ---- the stores of the new state ----
+  if (sat) {
+    s.key32[c] = kDead32;
+    s.cexp[c] = kCexpDead;
+    s.ctouch[c] = 0;
+    s.cst[c].ratio = dinf();
+  } else if (tch) {
+    CstRec* rec = s.cst + c;
+    s.ctouch[c] = 0;
+    rec->drem = rec->duse = rec->dcnt = 0;
+    s.nvote[c] = nv - int(qz);
+    rec->rem = r0;
+    rec->use = u0;
+    rec->ratio = rnew;
+    s.key32[c] = nk;
+    if (nk == kDead32)
+      s.cexp[c] = kCexpDead;
   }
   __syncthreads();  // (mf, qn)
   if (scan)

@@ -151,6 +151,8 @@ struct lmmhip_ctx {
   Scr fb_longl;                                   // solve_fair: the long shared constraints (fb_long_list)
   Scr fbp_k0, fbp_k1, fbp_v0, fbp_v1, fbp_tmp, fbp_perm, fbp_cscvp, fbp_mu;  // solve_fair: locality order (fb_perm)
   bool fb_perm_ok = false;                        // the order matches the uploaded system
+  Scr fbr_vp, fbr_c, fbr_w, fbr_pen, fbr_vb, fbr_x;  // solve_fair: the renumbered CSR copy (fb_renum)
+  bool fb_renum_ok = false;
   // frontier engine (lmm_frontier_kernels.hpp): CSR -> CSC map of the uploaded structure, vote slots, floors,
   // re-vote queue; the map and the largest CSC degree are rebuilt after every structural change
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
@@ -255,7 +257,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc})
@@ -441,6 +443,7 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
 static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, bool elem_done = false) {
   Dev& d = c->d;
   c->fb_perm_ok = false;
+  c->fb_renum_ok = false;
   c->fr_map_ok = false;
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
@@ -1363,8 +1366,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
 // control-word copy; 0 / 1 init.
 static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   Dev d = c->d;  // (a copy: the frontier's buffers stay out of the context's Dev, which the other engines use)
+  if (!c->vote_diag)  // per-round diagnostic counters only on request (LMMHIP_VOTE_DIAG): they cost atomics
+    d.vstat = nullptr;
   const int64_t nnz = std::max<int64_t>(d.nnz, 1);
-  const int nblk = int((int64_t(d.nC) + kFB - 1) / kFB);  // fr_update / fr_vote / fr_sat workgroups
+  const int nblk = int((int64_t(d.nC) + kFB - 1) / kFB);  // fr_update / fr_vote workgroups
+  const int nblkS = int(std::max<int64_t>(1, (int64_t(d.nC) + kFS - 1) / kFS));  // fr_sat workgroups
   int2* cs = nullptr;
   int32_t* md = nullptr;
   int rc = scratch(c, c->fr_c2s, nnz, &cs);
@@ -1390,6 +1396,11 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
     c->fr_map_ok = true;
   }
   const bool big = c->fr_maxdeg > kFrBigCh * kWave;
+  // measurement knobs (defaults = the measured best): the re-vote reads the floors with the keys; the
+  // saturation's workgroup size and chunk body (the round engine's saturate_chunk)
+  const bool mf_early = env_int("LMMHIP_FR_MFEARLY", 1) != 0;
+  const int sat_b = env_int("LMMHIP_FR_SATB", kFS) == 256 ? 256 : kFS;
+  const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
@@ -1410,11 +1421,22 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
   for (;;) {
     for (int k = 0; k < chunk; k++, r++) {
-      if (r == 0)
+      if (r == 0) {
         LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
+        LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
+      } else if (mf_early) {
+        LAUNCH(2, r, fr_vote<true>, nblk, kFB, d, int(r));
+      } else {
+        LAUNCH(2, r, fr_vote<false>, nblk, kFB, d, int(r));
+      }
+      if (sat_b == 256 && sat_old)
+        LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r));
+      else if (sat_b == 256)
+        LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r));
+      else if (sat_old)
+        LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r));
       else
-        LAUNCH(2, r, fr_vote, nblk, kFB, d, int(r));
-      LAUNCH(4, r, fr_sat, nblk, kFB, d, int(r));
+        LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r));
       if (big)
         LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r));
       LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec);
@@ -1695,6 +1717,59 @@ static int fb_perm(lmmhip_ctx* c) {
   return 0;
 }
 
+// The renumbered copy of the system for the one-context solve (lmm_fb_kernels.hpp fbr_*): the CSR rows in the
+// locality order of fb_perm (once per uploaded structure), the penalties and bounds every solve.  Fills `r`
+// with the Dev the rounds run on.  LMMHIP_FB_RENUM=0 keeps the original order (measurement knob).
+static int fb_renum(lmmhip_ctx* c, Dev* r, double** px) {
+  Dev& d = c->d;
+  *r = d;
+  *px = nullptr;
+  if (!d.mu_p || d.nV == 0 || !env_int("LMMHIP_FB_RENUM", 1))
+    return 0;
+  const int32_t* order = static_cast<const int32_t*>(c->fbp_v1.p);  // the sort's values: old id of new id n
+  uint32_t* pvp = nullptr;
+  int32_t* pc = nullptr;
+  double *pw = nullptr, *ppen = nullptr, *pvb = nullptr;
+  const int64_t nnz = std::max<int64_t>(d.nnz, 1);
+  int rc = scratch(c, c->fbr_vp, int64_t(d.nV) + 1, &pvp);
+  rc = rc ? rc : scratch(c, c->fbr_c, nnz, &pc);
+  rc = rc ? rc : scratch(c, c->fbr_w, nnz, &pw);
+  rc = rc ? rc : scratch(c, c->fbr_pen, d.nV, &ppen);
+  rc = rc ? rc : scratch(c, c->fbr_vb, d.nV, &pvb);
+  rc = rc ? rc : scratch(c, c->fbr_x, d.nV, px);
+  if (rc)
+    return rc;
+  if (!c->fb_renum_ok) {
+    uint32_t* plen = nullptr;
+    if ((rc = scratch(c, c->fbp_k1, int64_t(d.nV) + 1, reinterpret_cast<unsigned long long**>(&plen))))
+      return rc;  // (fb_perm's key scratch, free once the order is known)
+    hipLaunchKernelGGL(fbr_len, dim3(grid_for(int64_t(d.nV) + 1, kBlock)), dim3(kBlock), 0, c->stream, d, order, plen);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0;
+    HIPCHK(scan_u32(nullptr, tb, plen, pvp, int64_t(d.nV) + 1, c->stream));
+    uint8_t* t = nullptr;
+    if ((rc = scratch(c, c->rs_tmp, int64_t(tb), &t)))
+      return rc;
+    HIPCHK(scan_u32(t, tb, plen, pvp, int64_t(d.nV) + 1, c->stream));
+    hipLaunchKernelGGL(fbr_rows, dim3(grid_for(d.nV, kBlock)), dim3(kBlock), 0, c->stream, d, order, pvp, pc, pw);
+    HIPCHK(hipGetLastError());
+    c->fb_renum_ok = true;
+  }
+  hipLaunchKernelGGL(fbr_vars, dim3(grid_for(d.nV, kBlock)), dim3(kBlock), 0, c->stream, d, order, ppen, pvb);
+  HIPCHK(hipGetLastError());
+  r->var_ptr = pvp;
+  r->csr_c = pc;
+  r->csr_w = pw;
+  r->pen = ppen;
+  r->vbound = pvb;
+  r->csc_v = d.csc_vp;
+  r->mu_p = nullptr;
+  r->x = *px;
+  return 0;
+}
+
+static int solve_fair_rounds(lmmhip_ctx* c, double prec);
+
 static int solve_fair(lmmhip_ctx* c, double prec) {
   c->fb_shard = false;
   // shared constraints of at least this many elements get their increments precomputed element-parallel
@@ -1717,6 +1792,23 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   c->d.xmin = c->xmin_own;
   if (int rc = fb_perm(c))
     return rc;
+  Dev rn{};
+  double* px = nullptr;
+  if (int rc = fb_renum(c, &rn, &px))
+    return rc;
+  if (!px)
+    return solve_fair_rounds(c, prec);
+  const Dev saved = c->d;  // the rounds run on the renumbered copy; the context's Dev comes back after
+  c->d = rn;
+  const int rc = solve_fair_rounds(c, prec);
+  c->d = saved;
+  if (rc)
+    return rc;
+  LAUNCH(6, c->fb_round, fbr_unperm, grid_for(c->d.nV, kBlock), kBlock, c->d, px);
+  return 0;
+}
+
+static int solve_fair_rounds(lmmhip_ctx* c, double prec) {
   if (int rc = fb_begin(c, prec))
     return rc;
   // The reference's rounds are not bounded by the system size (FATPIPE remaining can shrink

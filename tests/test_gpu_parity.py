@@ -323,3 +323,32 @@ def test_c_client_drives_a_solve():
     r = subprocess.run([build_c_drive()], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "abi_drive: ok" in r.stdout
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_synthetic_full_size_vs_oracle_sample():
+    """C2 at FULL size (1e6 x 1e7 x 8, seed 1) against the oracle's own solve of the same system, made once in
+    the build container (tests/golden/make_c2_full_sample.py; ~45 min of the O(rounds x constraints) reference
+    loop, maxmin.cpp:560-680): a fixed random sample of 1e5 variables within K.ABS_TOL / K.REL_TOL, and the
+    saturated-constraint set (maxmin.cpp print()'s test over every constraint) identical bit for bit."""
+    import os
+
+    from simgrid_amd import multi as M
+
+    path = os.path.join(os.path.dirname(__file__), "golden", "c2_full_sample.npz")
+    fx = np.load(path)
+    s = L.System(False)
+    vids = s.gen_synthetic(1_000_000, 10_000_000, 8, seed=1)
+    f = M.export_flat(s)
+    from tests.golden.make_c2_full_sample import flat_sha256, saturated_bits
+    assert flat_sha256(f) == str(fx["csr_sha256"]), "not the system the oracle solved"
+    assert np.array_equal(f.var_ids, vids)
+    s.solve()
+    x = s.values_of(vids)
+    idx, y = fx["sample_idx"], fx["sample_x"]
+    tol = np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(y))
+    diff = np.abs(x[idx] - y)
+    assert np.all(diff <= tol), (float(diff.max()), int(np.count_nonzero(diff > tol)))
+    got = saturated_bits(f, x, L.get_precision())
+    assert np.array_equal(got, fx["sat_bits"]), int(np.count_nonzero(np.unpackbits(got) != np.unpackbits(fx["sat_bits"])))
