@@ -41,6 +41,7 @@ constexpr int kFB = 256;                 // threads per workgroup = constraints 
 constexpr uint32_t kNoVoter = 0xFFFFFFFFu;  // vslot: no vote registered at this element; minfl: none at all
 constexpr int kFrBigCh = 16;             // constraints of more CSC chunks than this saturate in fr_sat_big
 constexpr int kFrBigWaves = 16;          // waves per big constraint in fr_sat_big
+constexpr int kFVS = 4;                  // fr_update segments (workgroups) per fr_vote workgroup
 
 // CSR element -> (constraint, CSC position) pairs (csr_cs), once per uploaded structure: one wave per
 // constraint, each CSC element finds its CSR element in its variable's row (csc_row); the k-th element of a
@@ -276,7 +277,7 @@ __global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
 
 // Rounds >= 1: the variables fr_update queued in workgroup b's segment (the CSC range of its constraints).
 // Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
-template <bool kEarly = true> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round) {
+template <bool kEarly = true> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
   if (s.ctl[CTL_DONE])
     return;
   if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
@@ -286,12 +287,26 @@ template <bool kEarly = true> __global__ void __launch_bounds__(kFB) fr_vote(Dev
   }
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_PALIVE0 + (round & 1)] = 0;  // this round's fr_update raises it
-  const int n = s.fq_n[blockIdx.x];
-  if (n == 0)
-    return;
-  const uint32_t seg = s.cnst_ptr[int64_t(blockIdx.x) * kFB];
-  for (int i = threadIdx.x; i < n; i += kFB) {
-    const unsigned long long a = s.fq_a[seg + i], rw = s.fq_b[seg + i];
+  // spb (<= kFVS) consecutive segments per workgroup: on C2 ~170 queued rows, one pass, and the launch's
+  // workgroups resident at once; small systems keep one segment per workgroup (more workgroups)
+  const int64_t nseg = (int64_t(s.nC) + kFB - 1) / kFB;
+  int n[kFVS], pre[kFVS + 1];
+  uint32_t seg[kFVS];
+  pre[0] = 0;
+#pragma unroll
+  for (int k = 0; k < kFVS; k++) {
+    const int64_t sg = int64_t(blockIdx.x) * spb + k;
+    n[k] = k < spb && sg < nseg ? s.fq_n[sg] : 0;
+    seg[k] = k < spb && sg < nseg ? s.cnst_ptr[sg * kFB] : 0u;
+    pre[k + 1] = pre[k] + n[k];
+  }
+  for (int i = threadIdx.x; i < pre[kFVS]; i += kFB) {
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < kFVS; q++)
+      k += i >= pre[q];
+    const uint32_t at = seg[k] + uint32_t(i - pre[k]);
+    const unsigned long long a = s.fq_a[at], rw = s.fq_b[at];
     const int o = fr_revote<8, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
                                              uint32_t(rw >> 32), round);
     if (s.vstat) {

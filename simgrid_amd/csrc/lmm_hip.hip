@@ -1398,7 +1398,9 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const bool big = c->fr_maxdeg > kFrBigCh * kWave;
   // measurement knobs (defaults = the measured best): the re-vote reads the floors with the keys; the
   // saturation's workgroup size and chunk body (the round engine's saturate_chunk)
-  const bool mf_early = env_int("LMMHIP_FR_MFEARLY", 1) != 0;
+  const bool mf_early = env_int("LMMHIP_FR_MFEARLY", 0) != 0;
+  // fr_vote: segments per workgroup, so that the grid still covers the chip twice (C2: 4, small systems: 1)
+  const int spb = int(std::max<int64_t>(1, std::min<int64_t>(kFVS, int64_t(nblk) / (2 * int64_t(c->n_cu)))));
   const int sat_b = env_int("LMMHIP_FR_SATB", kFS) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
@@ -1425,9 +1427,9 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
         LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
         LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
       } else if (mf_early) {
-        LAUNCH(2, r, fr_vote<true>, nblk, kFB, d, int(r));
+        LAUNCH(2, r, fr_vote<true>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       } else {
-        LAUNCH(2, r, fr_vote<false>, nblk, kFB, d, int(r));
+        LAUNCH(2, r, fr_vote<false>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       }
       if (sat_b == 256 && sat_old)
         LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r));
