@@ -27,7 +27,8 @@ OUT = os.path.join(ROOT, "gpurun_out")
 SOLVE_MARK = {"c2": "mm_init_vars", "c2_stress": "mm_init_vars", "c3": "mm_batch_lds", "c4": "mm_persist",
               "c5": "fb_init"}
 # kernels of the upload / device flatten (before the timed region), not of a solve
-NOT_SOLVE = ("rs_", "rocprim", "__amd_rocclr_copyBuffer", "mm_elem_usage", "mm_dup_check", "mm_batch_check")
+NOT_SOLVE = ("rs_", "rocprim", "__amd_rocclr_copyBuffer", "mm_elem_usage", "mm_dup_check", "mm_batch_check",
+             "fr_c2s")
 
 
 def load(path):

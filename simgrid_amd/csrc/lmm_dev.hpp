@@ -188,6 +188,9 @@ struct Dev {
   unsigned long long* fq_a;  // [nnz] re-vote queue, one segment per fr_update workgroup: variable | target << 32
   unsigned long long* fq_b;  // [nnz]   and the variable's CSR row (begin | end << 32)
   int32_t* fq_n;             // [nC / kFB + 1] queued variables per segment
+  // multi-launch engine (round 4): the alive row of each variable in the buffer in use (maintained by
+  // mm_init_vars and cmp_write), so that mm_saturate retires the rows of the variables it fixes (null: off)
+  int32_t* rowof;
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };

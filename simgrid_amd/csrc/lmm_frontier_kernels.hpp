@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
 
 // Rounds >= 1: the variables fr_update queued in workgroup b's segment (the CSC range of its constraints).
 // Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
-template <bool kEarly = true> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
+template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
   if (s.ctl[CTL_DONE])
     return;
   if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
@@ -307,7 +307,7 @@ template <bool kEarly = true> __global__ void __launch_bounds__(kFB) fr_vote(Dev
       k += i >= pre[q];
     const uint32_t at = seg[k] + uint32_t(i - pre[k]);
     const unsigned long long a = s.fq_a[at], rw = s.fq_b[at];
-    const int o = fr_revote<8, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
+    const int o = fr_revote<R, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
                                              uint32_t(rw >> 32), round);
     if (s.vstat) {
       fr_diag(s, round, 6, true);

@@ -156,6 +156,7 @@ struct lmmhip_ctx {
   // frontier engine (lmm_frontier_kernels.hpp): CSR -> CSC map of the uploaded structure, vote slots, floors,
   // re-vote queue; the map and the largest CSC degree are rebuilt after every structural change
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
+  Scr mm_rowof;  // solve_maxmin: alive row of each variable (saturation retires fixed variables' rows)
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
@@ -257,7 +258,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc})
@@ -1226,6 +1227,19 @@ static int env_int(const char* name, int dflt) {
 
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
+  struct RowofOff {  // the other engines never see the row map (their compactions do not maintain it)
+    Dev& d;
+    ~RowofOff() { d.rowof = nullptr; }
+  } rowof_off{d};
+  // the saturation retires the rows of the variables it fixes (row map kept by init / cmp_write; not with
+  // the target-ordered regroups, whose unpack would have to maintain it too).  LMMHIP_RETIRE=0: off.
+  d.rowof = nullptr;
+  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) == 0 && env_int("LMMHIP_RETIRE", 1)) {
+    int32_t* ro = nullptr;
+    if (int rc = scratch(c, c->mm_rowof, std::max<int64_t>(d.nV, 1), &ro))
+      return rc;
+    d.rowof = ro;
+  }
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   const int gC = grid_for(d.nC, kBlock);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
@@ -1252,6 +1266,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // (mm_vote_tgt), regrouped after the first chunk and then every tgt_every rounds by a radix sort on
   // (target + 1) / 16, instead of the bitmap-filter vote on order-preserving compactions
   const bool tgt = (c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) != 0;
+
   const int tgt_every = env_int("LMMHIP_TGT_EVERY", 16);
   const uint32_t tg_dead = uint32_t((int64_t(d.nC) + 1) >> 4) + 1;
   const int tg_bits = 32 - __builtin_clz(tg_dead);
@@ -1399,6 +1414,8 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   // measurement knobs (defaults = the measured best): the re-vote reads the floors with the keys; the
   // saturation's workgroup size and chunk body (the round engine's saturate_chunk)
   const bool mf_early = env_int("LMMHIP_FR_MFEARLY", 0) != 0;
+  // re-votes keep 16 row elements in registers when the mean row is longer than 8 (LMMHIP_FR_R16=0: 8)
+  const bool long_rows = c->group > 8 && env_int("LMMHIP_FR_R16", 1) != 0;
   // fr_vote: segments per workgroup, so that the grid still covers the chip twice (C2: 4, small systems: 1)
   const int spb = int(std::max<int64_t>(1, std::min<int64_t>(kFVS, int64_t(nblk) / (2 * int64_t(c->n_cu)))));
   const int sat_b = env_int("LMMHIP_FR_SATB", kFS) == 256 ? 256 : kFS;
@@ -1426,6 +1443,8 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       if (r == 0) {
         LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
         LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
+      } else if (long_rows) {  // (LV08 routes: ~12 elements per row)
+        LAUNCH(2, r, (fr_vote<false, 16>), (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       } else if (mf_early) {
         LAUNCH(2, r, fr_vote<true>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       } else {

@@ -142,6 +142,8 @@ __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t
     s.vstate[v] = 0;
     s.rtgt[0][v] = kUnvoted;
     const_cast<int32_t*>(s.cvar[0])[v] = int32_t(v) | (s.vbound[v] > 0 ? int32_t(0x80000000u) : 0);
+    if (s.rowof)
+      s.rowof[v] = int32_t(v);  // buffer 0 is the CSR itself
   }
 }
 
@@ -953,11 +955,14 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
 // c's ratio is left in place (the other waves of c read it; the dead key hides it from later readers).
 constexpr int kSatU = 4;
 
+// retire (multi-launch engine, round 4): the buffer's row targets; each claimed variable's alive row (rowof) is
+// marked kRetired, so the next vote's filter skips it instead of queueing a re-vote that only finds the
+// variable fixed (~6.4e4 rows per C2 round).
 __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
-                                               int round, int lane, int* pre, bool dup) {
+                                               int round, int lane, int* pre, bool dup, int32_t* retire = nullptr) {
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
-  int32_t lv = -1;
+  int32_t lv = -1, ro = 0;
   double lp = 1.0, lx = 0.0;
   uint32_t rb = 0, re = 0;
   if (j < ce) {
@@ -968,6 +973,8 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     const unsigned long long row = s.csc_row[j];
     rb = uint32_t(row);
     re = uint32_t(row >> 32);
+    if (retire)
+      ro = s.rowof[lv];  // (issued with the state's load)
     if (s.vstate[lv] != 0)
       lv = -1;
     else if (!dup)
@@ -980,6 +987,8 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     lx = r / lp;
     s.x[lv] = lx;
     len = int(re - rb);
+    if (retire)
+      retire[ro] = kRetired;
   } else {
     rb = re = 0;
   }
@@ -1156,12 +1165,12 @@ __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t
 // Multi-launch engine: saturation of mm_ready's list, K waves per ready constraint (chunks k, k + K, ...)
 // spread evenly over the whole grid — the ready list is global here, so the work balances across workgroups.
 template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int k, int round, int lane,
-                                                              int* pre) {
+                                                              int* pre, int32_t* retire) {
   const double r = ld_rlx(&s.cst[c].ratio);  // wave-uniform address: keep it off the scalar cache
   const uint32_t ce = s.cnst_ptr[c + 1];
   const bool dup = s.cdup[c] != 0;
   for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
-    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup);
+    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup, retire);
   if (k == 0 && lane == 0)  // c leaves the light table: mm_update (the owner of key / chg) retires it
     s.ctouch[c] = 2;
 }
@@ -1213,6 +1222,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
   const int64_t chunk = chunk_of(s.ctl[CTL_NCL0 + cb], ready_blocks);
+  int32_t* retire = s.rowof ? s.rtgt[s.ctl[CTL_BUF]] : nullptr;
   for (int64_t g = wave; g < int64_t(total) * K; g += nwaves) {
     const int64_t i = g / K;
     const int k = int(g % K);
@@ -1221,7 +1231,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
     for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
       if (lo + step < ready_blocks && pre[lo + step] <= i)
         lo += step;
-    saturate_one<K>(s, s.ready[lo * chunk + (i - pre[lo])], k, round, lane, wpre[w]);
+    saturate_one<K>(s, s.ready[lo * chunk + (i - pre[lo])], k, round, lane, wpre[w], retire);
   }
 }
 
@@ -1592,6 +1602,8 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s) {
     if (al) {
       const int o = pr + xr;
       ovar[o] = v;
+      if (s.rowof)
+        s.rowof[rvar(v)] = o;
       s.rtgt[out][o] = s.rtgt[in][row];
       s.skey[out][o] = s.skey[in][row];
       orow[o] = uint32_t(pe + xe);
