@@ -185,7 +185,8 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
  *     barriers, termination decided on the device, no host round-trip;
  *   LMMHIP_ENGINE_ROUNDS — one launch per phase per round, the host polling termination every few
  *     rounds (also the engine of the profiling mode, which times every phase launch);
- *   LMMHIP_ENGINE_AUTO (default) — persistent up to 2^18 variables, rounds above.
+ *   LMMHIP_ENGINE_AUTO (default) — persistent up to 2^14 variables, frontier (below) up to 2^18, rounds
+ *     above.
  * All give bit-identical results.  The environment variable LMMHIP_ENGINE=rounds|persistent overrides. */
 #define LMMHIP_ENGINE_PERSISTENT 0
 #define LMMHIP_ENGINE_ROUNDS 1

@@ -24,7 +24,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 # one launch per solve of each workload's engine: the number of solves in a counter run
-SOLVE_MARK = {"c2": "mm_init_vars", "c2_stress": "mm_init_vars", "c3": "mm_batch_lds", "c4": "mm_persist",
+SOLVE_MARK = {"c2": "mm_init_vars", "c2_stress": "mm_init_vars", "c3": "mm_batch_lds", "c4": "fr_init_vars",
               "c5": "fb_init"}
 # kernels of the upload / device flatten (before the timed region), not of a solve
 NOT_SOLVE = ("rs_", "rocprim", "__amd_rocclr_copyBuffer", "mm_elem_usage", "mm_dup_check", "mm_batch_check",

@@ -31,7 +31,8 @@
 using namespace lmmdev;
 
 constexpr unsigned kPersistProfCap = 1 << 16;  // barriers covered by lmmhip_persist_profile
-constexpr int64_t kAutoPersistVars = 1 << 18;   // LMMHIP_ENGINE_AUTO: persistent up to this many variables
+constexpr int64_t kAutoPersistVars = 1 << 18;   // LMMHIP_ENGINE_AUTO: one of the single-GPU small-system engines up to
+constexpr int64_t kAutoPersistMaxVars = 1 << 14;  // this many variables: persistent up to 2^14, frontier above
 
 namespace {
 
@@ -1232,9 +1233,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     ~RowofOff() { d.rowof = nullptr; }
   } rowof_off{d};
   // the saturation retires the rows of the variables it fixes (row map kept by init / cmp_write; not with
-  // the target-ordered regroups, whose unpack would have to maintain it too).  LMMHIP_RETIRE=0: off.
+  // the target-ordered regroups, whose unpack would have to maintain it too).  Opt-in (LMMHIP_RETIRE=1):
+  // measured on C2 at 26.8 ms vs 26.2 ms without (the extra row-map load and store per fixed variable
+  // cost more than the re-vote rows they save -- most fixed variables' rows are already off the list).
   d.rowof = nullptr;
-  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) == 0 && env_int("LMMHIP_RETIRE", 1)) {
+  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) == 0 && env_int("LMMHIP_RETIRE", 0)) {
     int32_t* ro = nullptr;
     if (int rc = scratch(c, c->mm_rowof, std::max<int64_t>(d.nV, 1), &ro))
       return rc;
@@ -1499,7 +1502,11 @@ static int engine_of(const lmmhip_ctx* c) {
   // round chain dominate (small systems: a tie at C4, 1e5 variables, and ahead below); the round chain
   // above, where the kernel boundaries (~1.5 us) are cheaper than grid barriers (~4 us) and per-launch
   // grids keep 32 waves per CU in flight instead of 16
-  return int64_t(c->d.nV) <= kAutoPersistVars ? LMMHIP_ENGINE_PERSISTENT : LMMHIP_ENGINE_ROUNDS;
+  // round 4: the frontier engine between the two (C4, 1e5 LV08 flows: 3.54 ms against 4.34 persistent and
+  // 4.48 rounds), the round engine above (C2: 25.8 against 28.2 frontier)
+  if (int64_t(c->d.nV) <= kAutoPersistMaxVars)
+    return LMMHIP_ENGINE_PERSISTENT;
+  return int64_t(c->d.nV) <= kAutoPersistVars ? LMMHIP_ENGINE_FRONTIER : LMMHIP_ENGINE_ROUNDS;
 }
 
 // One persistent launch per solve (lmm_persist_kernels.hpp): one 1024-thread workgroup per CU, all
@@ -1745,7 +1752,7 @@ static int fb_renum(lmmhip_ctx* c, Dev* r, double** px) {
   Dev& d = c->d;
   *r = d;
   *px = nullptr;
-  if (!d.mu_p || d.nV == 0 || !env_int("LMMHIP_FB_RENUM", 1))
+  if (!d.mu_p || d.nV == 0 || !env_int("LMMHIP_FB_RENUM", 0))
     return 0;
   const int32_t* order = static_cast<const int32_t*>(c->fbp_v1.p);  // the sort's values: old id of new id n
   uint32_t* pvp = nullptr;

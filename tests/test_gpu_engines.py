@@ -178,11 +178,14 @@ def test_target_ordered_vote_bit_identical(stress, monkeypatch):
     bitmap-filter vote over order-preserving compactions give the same bytes: the row order
     changes no vote.  1e5 x 1e6 x 8 (the C2/10 system: 25+ regroups)."""
     out = []
-    for tgt in ("1", "0"):
+    # (LMMHIP_TGT, LMMHIP_RETIRE): the opt-in row retirement by the saturation must not change a byte either
+    for tgt, retire in (("1", "0"), ("0", "0"), ("0", "1")):
         monkeypatch.setenv("LMMHIP_TGT", tgt)
+        monkeypatch.setenv("LMMHIP_RETIRE", retire)
         out.append(_values(_synthetic(100000, 1000000, 1, stress), L.System.ENGINE_ROUNDS))
-    assert out[0][1] == out[1][1]
-    assert out[0][0].tobytes() == out[1][0].tobytes(), float(np.max(np.abs(out[0][0] - out[1][0])))
+    for o in out[1:]:
+        assert out[0][1] == o[1]
+        assert out[0][0].tobytes() == o[0].tobytes(), float(np.max(np.abs(out[0][0] - o[0])))
 
 
 def test_persistent_engine_concurrent_contexts_and_torch():
