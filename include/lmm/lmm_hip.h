@@ -111,9 +111,14 @@ int lmmhip_res_values(lmmhip_ctx* ctx, int64_t n, double* values, uint8_t* reset
  * D2H runs at full PCIe rate and the caller scatters from them without another copy. */
 int lmmhip_res_values_pinned(lmmhip_ctx* ctx, int64_t n, const double** values, const uint8_t** reset);
 /* Number of lmmhip_res_flatten calls served by the refresh path (same constraint list and precision,
- * no element record / slab change / bound crossing the part test since the last flatten: only the
- * dense penalties and bounds are rewritten). */
+ * no element record / slab change since the last flatten, and no constraint bound crossing the part
+ * test (maxmin.cpp:523-525) in a way that changes the member set: only the dense penalties and bounds
+ * are rewritten).  Replaces nothing in the reference (its lmm_solve re-reads the lists every time). */
 int lmmhip_res_refreshes(lmmhip_ctx* ctx, int64_t* n);
+/* Of those, the calls that also had part-test crossings since the last flatten (judged on the device by
+ * rs_cross_check: the flattened system lists every listed constraint a member lies on, whatever its
+ * bound, so a crossing that leaves the member set as it is keeps the structure). */
+int lmmhip_res_cross_refreshes(lmmhip_ctx* ctx, int64_t* n);
 /* Inspection: download the flattened system the next lmmhip_solve runs on (from lmmhip_upload or
  * lmmhip_res_flatten).  counts3 = {n_var, n_cnst, nnz}; null arrays are skipped (sizes first). */
 int lmmhip_flat_download(lmmhip_ctx* ctx, int64_t* counts3, uint32_t* var_ptr, int32_t* csr_c, double* csr_w,

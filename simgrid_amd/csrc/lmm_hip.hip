@@ -140,11 +140,13 @@ struct lmmhip_ctx {
   int64_t res_flat_nv = 0;                      // variable slots covered by that flatten
   // refresh path of lmmhip_res_flatten: the last flatten's list and precision, host-side structural
   // flag (element records shipped since), device flags of rs_apply_v / rs_apply_c (kResStruct / kResPenalty)
+  // res_dirty: [0] flags, [1] fair error, [2] "mixed" member (rs_mark), [3] part-test crossings since the
+  // last flatten, [4 ..) their constraint ids (kResCrossCap, rs_apply_c)
   std::vector<int32_t> res_last_list;
   double res_last_prec = -1.0;
   bool res_struct_host = true;
   int32_t* res_dirty = nullptr;
-  int64_t res_refreshes = 0;
+  int64_t res_refreshes = 0, res_cross_refreshes = 0;
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
@@ -161,7 +163,8 @@ struct lmmhip_ctx {
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
-      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch, rs_rowpen, rs_posd, rs_cls, rs_lanyc;
+      rs_ro, rs_rowid, rs_kidx, rs_skey, rs_sval, rs_vout, rs_tmp, rs_lzero, rs_nck, rs_cch, rs_rowpen, rs_posd, rs_cls, rs_lanyc,
+      rs_outc;
 };
 
 static void free_owner(lmmhip_ctx* c) {
@@ -262,7 +265,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
-                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc})
+                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc})
     if (b->p)
       (void)hipFree(b->p);
   for (lmmhip_ctx::Scr& b : c->rs_stage)
@@ -656,6 +659,21 @@ template <class T> static int res_grow(lmmhip_ctx* c, T** p, int64_t used, int64
   return 0;
 }
 
+// Integer knob from the environment (A/B switches, documented where read).
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+// Flags and crossing list of the delta batches (lmmhip_ctx::res_dirty), zeroed on first use.
+static int res_dirty_alloc(lmmhip_ctx* c) {
+  if (c->res_dirty)
+    return 0;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), (4 + kResCrossCap) * sizeof(int32_t)));
+  HIPCHK(hipMemsetAsync(c->res_dirty, 0, 4 * sizeof(int32_t), c->stream));
+  return 0;
+}
+
 template <class T> static int stage(lmmhip_ctx* c, int slot, const T* host, int64_t n, const T** out) {
   T* d = nullptr;
   if (int rc = scratch(c, c->rs_stage[slot], n, &d))
@@ -741,11 +759,8 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
       return rc;
     c->res_capC = cap;
   }
-  if (!c->res_dirty) {
-    // flags, fair error, "mixed" variable (rs_mark), spare
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 4 * sizeof(int32_t)));
-    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 4 * sizeof(int32_t), c->stream));
-  }
+  if (int rc = res_dirty_alloc(c))
+    return rc;
   if (ne || n_var_total > c->res_nV || n_cnst_total > c->res_nC)
     c->res_struct_host = true;
   c->res_nE = std::max(c->res_nE, n_elem_total);
@@ -780,7 +795,8 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
     int rc = stage(c, 9, c_id, nc, &did) | stage(c, 10, c_bound, nc, &db) | stage(c, 11, c_flags, nc, &dfl);
     if (rc)
       return rc;
-    RS_LAUNCH(rs_apply_c, nc, nc, did, db, dfl, r, c->res_last_prec < 0 ? 1e-5 : c->res_last_prec, c->res_dirty);
+    RS_LAUNCH(rs_apply_c, nc, nc, did, db, dfl, r, c->res_last_prec < 0 ? 1e-5 : c->res_last_prec, c->res_dirty,
+              c->res_dirty + 3, c->res_dirty + 4);
   }
   HIPCHK(hipStreamSynchronize(c->stream));  // host delta arrays are borrowed for the call only
   return 0;
@@ -801,31 +817,51 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   HIPCHK(hipStreamSynchronize(c->stream));
   const ResDev& r = c->res;
   const int64_t nl = n_list, nvs = c->res_nV;
-  // Refresh path: same list, same precision, no element record and no slab / part change since the
-  // last flatten -> the structure (CSR/CSC, dense maps, reset mask) stands; only penalties, variable
-  // bounds and constraint bounds / policies are rewritten in dense order.
+  // Refresh path: same list, same precision, no element record and no slab change since the last
+  // flatten, and no constraint-bound crossing of the part test that changes the member set (rs_cross_check)
+  // -> the structure (CSR/CSC, dense maps, reset mask) stands; only penalties, variable bounds and
+  // constraint bounds / policies are rewritten in dense order.
   if (!fair && c->res_flat && c->res_flat_kind == LMMHIP_KIND_MAXMIN && c->uploaded && !c->res_struct_host &&
       c->res_dirty && precision == c->res_last_prec &&
       nvs == c->res_flat_nv && size_t(nl) == c->res_last_list.size() &&
       (nl == 0 || std::memcmp(c->res_last_list.data(), cnst_list, size_t(nl) * sizeof(int32_t)) == 0)) {
-    int32_t flags = 0;
-    HIPCHK(hipMemcpyAsync(&flags, c->res_dirty, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    int32_t fl4[4] = {0, 0, 0, 0};  // flags, (fair error), mixed, crossings
+    HIPCHK(hipMemcpyAsync(fl4, c->res_dirty, sizeof(fl4), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    int32_t flags = fl4[0];
+    const int32_t nx = fl4[3];
+    if (nx > 0 && (fl4[2] || nx > kResCrossCap || env_int("LMMHIP_RES_CROSS", 1) == 0))
+      flags |= kResStruct;
+    if (!(flags & kResStruct)) {
+      Dev& d = c->d;
+      const int32_t* list = static_cast<const int32_t*>(c->rs_list.p);
+      const int64_t* lany = static_cast<const int64_t*>(c->rs_lany.p);
+      const int64_t* dcl = static_cast<const int64_t*>(c->rs_dcl.p);
+      RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, nullptr, const_cast<double*>(d.cbound),
+                const_cast<uint8_t*>(d.cflags));
+      if (nx > 0) {  // part-test crossings: structural only if the member set changes
+        const int grid = int(std::min<int64_t>(nx, 2048));
+        hipLaunchKernelGGL(rs_cross_check, dim3(grid), dim3(kBlock), 0, c->stream, nx, c->res_dirty + 4, r,
+                           precision, static_cast<const uint8_t*>(c->rs_cls.p),
+                           static_cast<const uint8_t*>(c->rs_outc.p), static_cast<const int32_t*>(c->rs_posd.p),
+                           d.cnst_ptr, d.csc_v, d.var_ptr, d.csr_c, d.cbound, c->res_dirty);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&flags, c->res_dirty, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+      }
+    }
     if (!(flags & kResStruct)) {
       Dev& d = c->d;
       const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
       const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
-      const int32_t* list = static_cast<const int32_t*>(c->rs_list.p);
-      const int64_t* lany = static_cast<const int64_t*>(c->rs_lany.p);
-      const int64_t* dcl = static_cast<const int64_t*>(c->rs_dcl.p);
       RS_LAUNCH(rs_refresh_v, nvs, nvs, r, vm, dv, const_cast<double*>(d.pen), const_cast<double*>(d.vbound));
-      RS_LAUNCH(rs_cmeta, nl, nl, list, r, lany, dcl, nullptr, const_cast<double*>(d.cbound),
-                const_cast<uint8_t*>(d.cflags));
       if ((flags & kResPenalty) && d.nnz > 0)
         RS_LAUNCH(mm_elem_usage, d.nnz, d, 0);
       HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
+      HIPCHK(hipMemsetAsync(c->res_dirty + 3, 0, sizeof(int32_t), c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
       c->res_refreshes++;
+      c->res_cross_refreshes += nx > 0;
       if (counts3) {
         counts3[0] = d.nV;
         counts3[1] = d.nC;
@@ -835,7 +871,7 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     }
   }
   int32_t *pos, *list, *posd;
-  uint8_t *lpart, *vrst, *lzero, *cls = nullptr, *lanyc = nullptr;
+  uint8_t *lpart, *vrst, *lzero, *cls = nullptr, *lanyc = nullptr, *outc = nullptr;
   int64_t *lany, *dcl, *cdeg, *cptr, *vm, *dv, *rl, *ro;
   int rc = scratch(c, c->rs_pos, c->res_nC, &pos) | scratch(c, c->rs_list, nl, &list) |
            scratch(c, c->rs_lzero, nl, &lzero) |
@@ -846,7 +882,8 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
            scratch(c, c->rs_rl, nvs + 1, &rl) | scratch(c, c->rs_ro, nvs + 1, &ro) |
            scratch(c, c->rs_posd, std::max<int64_t>(c->res_nC, 1), &posd);
   if (!fair)
-    rc |= scratch(c, c->rs_cls, c->res_nC, &cls) | scratch(c, c->rs_lanyc, c->res_nC, &lanyc);
+    rc |= scratch(c, c->rs_cls, c->res_nC, &cls) | scratch(c, c->rs_lanyc, c->res_nC, &lanyc) |
+          scratch(c, c->rs_outc, c->res_nC, &outc);
   if (rc)
     return rc;
   if (nl)
@@ -854,13 +891,12 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   if (c->res_nC)
     HIPCHK(hipMemsetAsync(pos, 0xFF, size_t(c->res_nC) * sizeof(int32_t), c->stream));
   HIPCHK(hipMemsetAsync(cdeg, 0, size_t(nl + 1) * sizeof(int64_t), c->stream));
-  if (!c->res_dirty) {
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->res_dirty), 4 * sizeof(int32_t)));
-    HIPCHK(hipMemsetAsync(c->res_dirty, 0, 4 * sizeof(int32_t), c->stream));
-  }
+  if (int rc = res_dirty_alloc(c))
+    return rc;
   if (!fair && c->res_nC) {
     HIPCHK(hipMemsetAsync(cls, 0, size_t(c->res_nC), c->stream));
     HIPCHK(hipMemsetAsync(lanyc, 0, size_t(c->res_nC), c->stream));
+    HIPCHK(hipMemsetAsync(outc, 0, size_t(c->res_nC), c->stream));
   }
   RS_LAUNCH(rs_pos, nl, nl, list, r, precision, int(fair), pos, lpart, lany, lzero, cls);
   if (fair) {
@@ -868,7 +904,7 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     RS_LAUNCH(rs_mark_fair, nvs, nvs, r, pos, lany, lzero, vrst, vm, c->res_dirty + 1);
   } else {
     HIPCHK(hipMemsetAsync(c->res_dirty + 2, 0, sizeof(int32_t), c->stream));
-    RS_LAUNCH(rs_mark, nvs, nvs, r, cls, lanyc, vrst, vm, rl, c->res_dirty + 2);
+    RS_LAUNCH(rs_mark, nvs, nvs, r, cls, lanyc, outc, vrst, vm, rl, c->res_dirty + 2);
     RS_LAUNCH(rs_lany_list, nl, nl, list, lanyc, lany);
   }
   if ((rc = dev_scan(c, lany, dcl, nl + 1)))
@@ -957,8 +993,10 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   c->res_last_list.assign(cnst_list, cnst_list + nl);
   c->res_last_prec = precision;
   c->res_struct_host = false;
-  if (c->res_dirty)
+  if (c->res_dirty) {
     HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->res_dirty + 3, 0, sizeof(int32_t), c->stream));
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
   if (counts3) {
     counts3[0] = nV;
@@ -982,6 +1020,13 @@ int lmmhip_res_refreshes(lmmhip_ctx* c, int64_t* n) {
   if (!c || !n)
     return fail(LMMHIP_E_ARG, "null argument");
   *n = c->res_refreshes;
+  return 0;
+}
+
+int lmmhip_res_cross_refreshes(lmmhip_ctx* c, int64_t* n) {
+  if (!c || !n)
+    return fail(LMMHIP_E_ARG, "null argument");
+  *n = c->res_cross_refreshes;
   return 0;
 }
 
@@ -1221,11 +1266,6 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
 
 // Slots: 0 mm_init_cnsts, 1 mm_init_vars, 2 mm_vote, 3 mm_ready, 4 mm_saturate, 5 mm_update,
 // 6 compaction.
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
-}
-
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
   struct RowofOff {  // the other engines never see the row map (their compactions do not maintain it)

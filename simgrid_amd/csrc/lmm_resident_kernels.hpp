@@ -7,10 +7,13 @@
 // records a mutation touched (the delta log: rs_apply_*), and rebuilds the solver's CSR / CSC on the
 // device with the exact selection rules of System::flatten_maxmin (lmm_system.cpp, which follows
 // lmm_solve's init, maxmin.cpp:509-540):
-//   * listed constraint c (active set, or the modified set in selective mode), in list order, is part
-//     of the system iff bound > bound * prec and an enabled element with w > 0 lies on it;
-//   * a variable is part of the system iff it has such an element; its CSR row is its slab in slot
-//     order, keeping the elements with w > 0 on a constraint that is part of the system;
+//   * a variable is a member iff it has an enabled element with w > 0 on a listed constraint (active
+//     set, or the modified set in selective mode) with bound > bound * prec;
+//   * listed constraint c, in list order, is flattened iff a member has an enabled element with w > 0
+//     on it (whatever its bound: the solver's init applies the bound test, so a bound crossing it keeps
+//     the structure unless it changes the member set -- rs_cross_check);
+//   * a member's CSR row is its slab in slot order, keeping the elements with w > 0 on a flattened
+//     constraint;
 //   * every variable with an enabled element on a listed constraint has its value reset to 0;
 //   * dense constraint ids follow the list order, dense variable ids ascending variable ids, and the
 //     CSC lists a constraint's elements in CSR order (stable radix sort) — the very arrays the host
@@ -53,9 +56,13 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // Structural-change flags of a delta batch (read by lmmhip_res_flatten's refresh path): bit0 = the
-// system's structure may have changed (slab moved / resized, a constraint's bound crossed the "part"
-// test at the last flatten's precision), bit1 = a penalty changed (per-element usage w/p is stale).
+// system's structure may have changed (slab moved / resized, or more part-test crossings than the
+// crossing list holds), bit1 = a penalty changed (per-element usage w/p is stale).  A constraint bound
+// that crosses the "part" test at the last flatten's precision is appended to the crossing list
+// instead (rs_apply_c): the flattened structure only changes when the crossing changes the member set,
+// which rs_cross_check decides on the device.
 constexpr int kResStruct = 1, kResPenalty = 2;
+constexpr int kResCrossCap = 4096;  // crossing-list capacity (ids since the last flatten)
 
 __global__ void __launch_bounds__(kBlock)
     rs_apply_v(int64_t n, const int32_t* __restrict__ id, const int64_t* __restrict__ eb,
@@ -79,12 +86,17 @@ __global__ void __launch_bounds__(kBlock)
 
 __global__ void __launch_bounds__(kBlock)
     rs_apply_c(int64_t n, const int32_t* __restrict__ id, const double* __restrict__ b,
-               const uint8_t* __restrict__ fl, ResDev r, double prec, int32_t* dirty) {
+               const uint8_t* __restrict__ fl, ResDev r, double prec, int32_t* dirty, int32_t* xn, int32_t* xlist) {
   int f = 0;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
     const double ob = r.c_bound[id[i]], nb = b[i];
-    if ((ob > ob * prec) != (nb > nb * prec))
-      f |= kResStruct;
+    if ((ob > ob * prec) != (nb > nb * prec)) {
+      const int32_t k = atomicAdd(xn, 1);
+      if (k < kResCrossCap)
+        xlist[k] = id[i];
+      else
+        f |= kResStruct;
+    }
     r.c_bound[id[i]] = nb;
     r.c_fl[id[i]] = fl[i];
   }
@@ -114,15 +126,19 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // Per variable slot: value reset (enabled element on a listed constraint, maxmin.cpp:509-514) and
-// membership (such an element with w > 0 on a part constraint, :527-538); marks the constraints that
-// have one (lanyc by constraint id, plain stores of 1: the race is benign; rs_lany_list puts them in list
-// order).  One gather per element, of the 1-byte class cls[c] written by rs_pos.  The row length is the
-// number of those elements unless a member also has a disabled element of weight > 0
+// membership (such an element with w > 0 on a part constraint, :527-538).  Marks the constraints a
+// member has an enabled element of w > 0 on, part or not (System::flatten_maxmin's superset rule:
+// lanyc by constraint id, plain stores of 1: the race is benign; rs_lany_list puts them in list order),
+// and, for a non-member, the listed constraints it has such an element on (outc: a bound of one of
+// those crossing the part test would make it a member -- rs_cross_check).  One gather per element, of
+// the 1-byte class cls[c] written by rs_pos; the second pass over the slab (a member's non-part or a
+// non-member's listed constraints) only runs for the few slabs that have such an element.  The row
+// length is the number of marked elements unless a member also has a disabled element of weight > 0
 // (System::flatten_maxmin takes every element of a member whose constraint is marked, enabled or not):
 // *mixed then asks rs_rowlen for the full count.
 __global__ void __launch_bounds__(kBlock)
-    rs_mark(int64_t nv, ResDev r, const uint8_t* __restrict__ cls, uint8_t* lanyc, uint8_t* vrst, int64_t* vm,
-            int64_t* rl, int32_t* mixed) {
+    rs_mark(int64_t nv, ResDev r, const uint8_t* __restrict__ cls, uint8_t* lanyc, uint8_t* outc, uint8_t* vrst,
+            int64_t* vm, int64_t* rl, int32_t* mixed) {
   bool mix = false;
   for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v <= nv; v += int64_t(gridDim.x) * kBlock) {
     if (v == nv) {
@@ -131,7 +147,7 @@ __global__ void __launch_bounds__(kBlock)
       break;
     }
     uint8_t rst = 0;
-    int64_t cnt = 0;
+    int64_t cnt = 0, cnt1 = 0;  // enabled w > 0 elements on part / on listed non-part constraints
     bool dis = false;
     const int64_t b = r.v_ebase[v];
     const int n = r.v_n[v];
@@ -159,15 +175,27 @@ __global__ void __launch_bounds__(kBlock)
         if (!k[u])
           continue;
         rst = 1;
-        if (w[u] > 0 && k[u] == 2) {
-          cnt++;
-          lanyc[p[u]] = 1;
+        if (w[u] > 0) {
+          if (k[u] == 2) {
+            cnt++;
+            lanyc[p[u]] = 1;
+          } else {
+            cnt1++;
+          }
         }
+      }
+    }
+    if (cnt1) {  // listed non-part constraints: in the flat when v is a member, else v is one of their outsiders
+      uint8_t* mark = cnt ? lanyc : outc;
+      for (int i = 0; i < n; i++) {
+        const int32_t p = r.e_cnst[b + i];
+        if ((r.e_fl[b + i] & kResElemEnabled) && r.e_w[b + i] > 0 && cls[p] == 1)
+          mark[p] = 1;
       }
     }
     vrst[v] = rst;
     vm[v] = cnt > 0;
-    rl[v] = cnt;
+    rl[v] = cnt > 0 ? cnt + cnt1 : 0;
     mix |= cnt > 0 && dis;
   }
   if (mix)
@@ -398,6 +426,52 @@ __global__ void __launch_bounds__(kBlock)
       continue;
     pen[dv[v]] = r.v_pen[v];
     vbound[dv[v]] = r.v_bound[v];
+  }
+}
+
+// Refresh path with part-test crossings (rs_apply_c's list, after rs_cmeta rewrote the dense bounds): does
+// a crossing change the member set?  One workgroup per crossing constraint c (block-uniform branches):
+//   * c not listed at the last flatten (cls 0): its bound plays no part;
+//   * c passes the part test now: a non-member with an enabled element of w > 0 on c (outc, rs_mark) would
+//     become a member -> structural;
+//   * c fails it now: each member on c (its CSC column) must keep an element on a constraint that still
+//     passes it, else it leaves the member set -> structural.  The dense rows are the members' enabled
+//     elements of w > 0 on flattened constraints (the host skips this check when a member also has a
+//     disabled one, rs_mark's *mixed), and the dense bounds are current, so several crossings since the
+//     last flatten are judged together.
+// Otherwise the member set, hence the flattened constraints (listed ones a member has such an element on)
+// and the rows, are what a full flatten would build, and only the bounds changed.
+__global__ void __launch_bounds__(kBlock)
+    rs_cross_check(int32_t nx, const int32_t* __restrict__ xlist, ResDev r, double prec,
+                   const uint8_t* __restrict__ cls, const uint8_t* __restrict__ outc, const int32_t* __restrict__ posd,
+                   const uint32_t* __restrict__ cnst_ptr, const int32_t* __restrict__ csc_v,
+                   const uint32_t* __restrict__ var_ptr, const int32_t* __restrict__ csr_c,
+                   const double* __restrict__ cbound, int32_t* dirty) {
+  for (int32_t i = blockIdx.x; i < nx; i += gridDim.x) {
+    const int32_t c = xlist[i];
+    if (cls[c] == 0)
+      continue;
+    const double b = r.c_bound[c];
+    if (b > b * prec) {
+      if (threadIdx.x == 0 && outc[c])
+        atomicOr(dirty, kResStruct);
+      continue;
+    }
+    const int32_t dc = posd[c];
+    if (dc < 0)
+      continue;
+    bool lost = false;
+    for (uint32_t j = cnst_ptr[dc] + threadIdx.x; j < cnst_ptr[dc + 1]; j += kBlock) {
+      const int32_t v = csc_v[j];
+      bool keep = false;
+      for (uint32_t k = var_ptr[v]; k < var_ptr[v + 1] && !keep; k++) {
+        const double cb = cbound[csr_c[k]];
+        keep = cb > cb * prec;
+      }
+      lost |= !keep;
+    }
+    if (lost)
+      atomicOr(dirty, kResStruct);
   }
 }
 

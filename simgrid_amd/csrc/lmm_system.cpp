@@ -697,9 +697,13 @@ std::vector<Id> System::solve_constraint_list() const {
   return list;
 }
 
-// Active part of lmm_solve's init (maxmin.cpp:509-540): enabled elements with w > 0 on listed
-// constraints with bound > bound*prec.  Values of every variable seen through an enabled element
-// of a listed constraint are reset to 0 (maxmin.cpp:509-514).
+// Active part of lmm_solve's init (maxmin.cpp:509-540).  Members: variables with an enabled element
+// of w > 0 on a listed constraint with bound > bound*prec (the "part" test, :523-525).  Values of every
+// variable seen through an enabled element of a listed constraint are reset to 0 (:509-514).
+// Constraints: every listed constraint on which a member has an enabled element of w > 0, whether it
+// passes the part test or not -- the device init applies that test itself (init_cnsts_waves: such a
+// constraint starts dead, as it never enters cnst_light_tab, :545-554), so a bound that crosses it
+// leaves the flattened structure as it is and the resident refresh path still applies.
 void System::flatten_maxmin(Flat& f, const std::vector<Id>& list) {
   const double prec = maxmin_precision;
   const int32_t coff = int32_t(f.cbound.size());
@@ -709,12 +713,10 @@ void System::flatten_maxmin(Flat& f, const std::vector<Id>& list) {
   for (Id c : list) {
     const CnstRec& k = cnsts_[c];
     const bool part = k.bound > k.bound * prec;
-    bool any = false;
     for (Id e = k.en_head; e != kNone; e = elems_[e].next) {
       const ElemRec& x = elems_[e];
       values_[x.var] = 0.0;
       if (part && x.weight > 0) {
-        any = true;
         vmark[x.var] = 1;
         if (selective_ && !vars_[x.var].in_modified_set) {  // maxmin.cpp:536-538
           vars_[x.var].in_modified_set = true;
@@ -722,6 +724,12 @@ void System::flatten_maxmin(Flat& f, const std::vector<Id>& list) {
         }
       }
     }
+  }
+  for (Id c : list) {
+    const CnstRec& k = cnsts_[c];
+    bool any = false;
+    for (Id e = k.en_head; e != kNone && !any; e = elems_[e].next)
+      any = elems_[e].weight > 0 && vmark[elems_[e].var];
     if (any) {
       dense_c[c] = coff + nc++;
       f.cbound.push_back(k.bound);

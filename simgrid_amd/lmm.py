@@ -128,6 +128,7 @@ SIGNATURES = {
     "lmmhip_res_flatten_fair": (I, [P, I64, ct.POINTER(ct.c_int32), PI64]),
     "lmmhip_res_values_pinned": (I, [P, I64, ct.POINTER(P), ct.POINTER(P)]),
     "lmmhip_res_refreshes": (I, [P, PI64]),
+    "lmmhip_res_cross_refreshes": (I, [P, PI64]),
     "lmmhip_flat_download": (I, [P, PI64, P, P, P, P, P, P, P, P, P, P]),
     "lmmhip_solve": (I, [P, I, D]),
     "lmmhip_set_batch": (I, [P, I64, PI64, PI64]),

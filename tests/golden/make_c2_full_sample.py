@@ -14,6 +14,13 @@ light-table rescan is O(rounds x constraints), maxmin.cpp:663-680).  The fixture
   * `oracle_rounds`, `oracle_seconds`: the oracle's sequential round count and solve time.
 
 Run from the repo root (CPU only, ~30 GB of host memory at peak):  python tests/golden/make_c2_full_sample.py
+
+Round 4 changed the flattened system's constraint rule (System::flatten_maxmin: every listed constraint a
+member lies on is flattened, whatever its bound; the ~1000 zero-bound constraints of C2 start dead in the
+solver's init instead of being left out).  The oracle solution does not depend on the flatten, so the fixture
+was converted rather than re-solved (`--convert-superset`): the new flat, filtered back to the constraints that
+pass the part test, must hash to the stored `csr_sha256` of the old rule; the zero-bound constraints are
+saturated by the reference's test (0 - usage > 0 never holds) and the other bits keep their order.
 """
 import hashlib
 import os
@@ -51,6 +58,46 @@ def saturated_bits(f, x, prec):
         use = np.where(fat, mx, use)
     sat = ~(f.cbound - use > f.cbound * prec)
     return np.packbits(sat.astype(np.uint8))
+
+
+def part_only(f, prec):
+    """`f` without the constraints that fail the part test (the pre-round-4 flatten rule)."""
+    from simgrid_amd import multi as M
+
+    keep = f.cbound > f.cbound * prec
+    newid = np.cumsum(keep) - 1
+    ek = keep[f.cnst_idx]
+    rows = np.repeat(np.arange(len(f.penalty)), np.diff(f.var_ptr))
+    var_ptr = np.zeros(len(f.penalty) + 1, np.int64)
+    np.cumsum(np.bincount(rows[ek], minlength=len(f.penalty)), out=var_ptr[1:])
+    return M.Flat(var_ptr, newid[f.cnst_idx[ek]].astype(np.int32), f.weight[ek], f.penalty, f.vbound,
+                  f.cbound[keep], f.cflags[keep], f.var_ids), keep
+
+
+def convert_superset():
+    import __graft_entry__
+
+    __graft_entry__.build()
+    from simgrid_amd import lmm as L
+    from simgrid_amd import multi as M
+
+    L.set_precision(1e-5)
+    fx = dict(np.load(OUT))
+    ps = L.System(False)
+    ps.gen_synthetic(NC, NV, K, seed=SEED)
+    f = M.export_flat(ps)
+    del ps
+    old, keep = part_only(f, 1e-5)
+    assert flat_sha256(old) == str(fx["csr_sha256"]), "the part-only filter does not give the solved system"
+    old_bits = np.unpackbits(fx["sat_bits"])[: int(keep.sum())].astype(bool)
+    sat = np.ones(len(f.cbound), bool)
+    sat[keep] = old_bits
+    fx["sat_bits"] = np.packbits(sat.astype(np.uint8))
+    fx["csr_sha256"] = np.array(flat_sha256(f))
+    fx["n_saturated"] = np.int64(sat.sum())
+    np.savez_compressed(OUT, **fx)
+    print(f"converted {OUT}: {len(f.cbound)} constraints ({int((~keep).sum())} zero-bound), "
+          f"{int(sat.sum())} saturated", flush=True)
 
 
 def main():
@@ -91,4 +138,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--convert-superset" in sys.argv:
+        convert_superset()
+    else:
+        main()

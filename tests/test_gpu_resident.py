@@ -231,3 +231,89 @@ def test_resident_refresh_path_bounds_and_penalties():
     _flat_equal(_split_solve(a), _split_solve(b))
     L._check_hip(L.lib().lmmhip_res_refreshes(a.device_ctx(), ct.byref(nref)))
     assert nref.value == 4
+
+
+def _counters(s):
+    import ctypes as ct
+
+    n, x = ct.c_int64(), ct.c_int64()
+    L._check_hip(L.lib().lmmhip_res_refreshes(s.device_ctx(), ct.byref(n)))
+    L._check_hip(L.lib().lmmhip_res_cross_refreshes(s.device_ctx(), ct.byref(x)))
+    return n.value, x.value
+
+
+def test_resident_refresh_path_part_crossings():
+    """A constraint bound crossing the part test (maxmin.cpp:523-525) keeps the flattened structure unless it
+    changes the member set (every listed constraint a member lies on is flattened whatever its bound; the
+    solver's init starts the failing ones dead): the device decides (rs_cross_check) and the result must
+    equal the host flatten bit for bit, and the values the oracle's, on both outcomes.
+    c0 .. c3 (bound 1), v0 on c0 + c1, v1 on c1 only, v2 on c2 + c3, v3 (bound 0.25) on c1 + c2."""
+    ops = [("cnst", i, 1.0) for i in range(4)]
+    ops += [("var", 0, 1.0, -1.0, 2), ("var", 1, 1.0, -1.0, 1), ("var", 2, 2.0, -1.0, 2), ("var", 3, 1.0, 0.25, 2)]
+    ops += [("expand", 0, 0, 1.0), ("expand", 1, 0, 2.0), ("expand", 1, 1, 1.0), ("expand", 2, 2, 1.0),
+            ("expand", 3, 2, 0.5), ("expand", 1, 3, 1.0), ("expand", 2, 3, 1.0)]
+    a, csa, vsa = K.replay(L, ops)
+    a.set_resident(True)
+    b, csb, vsb = K.replay(L, ops)
+    b.set_resident(False)
+    o, cso, vso = K.replay(O, ops)
+    # (bounds set this step, refresh path expected, with part-test crossings)
+    steps = [
+        ({0: 0.0}, True, True),              # v0 keeps c1
+        ({0: 2.0}, True, True),              # c0 back: its only enabled element is v0's, a member
+        ({1: 0.0}, False, False),            # v1 only lies on c1: it leaves the member set
+        ({3: 5.0}, True, False),             # no crossing (c1 flattened though failing the part test)
+        ({1: 1.0}, False, False),            # v1 (an outsider of c1 at the last flatten) joins again
+        ({2: 0.0, 3: 0.0}, False, False),    # v2 loses both of its constraints in one step
+        ({2: 0.0, 3: 4.0}, False, False),    # v2 joins again through c3
+        ({1: 0.0, 0: 3.0}, False, False),    # v1 and v3 leave (v3's c2 is still at 0)
+        ({2: 0.0, 0: 5.0}, True, False),     # no crossing
+        ({1: 1.0}, False, False),            # v1 and v3 join again
+        ({0: 0.0}, True, True),              # v0 keeps c1
+    ]
+    _flat_equal(_split_solve(a), _split_solve(b))
+    o.solve()
+    for step, (bounds, refresh, cross) in enumerate(steps):
+        n0, x0 = _counters(a)
+        for k, bd in bounds.items():
+            a.update_constraint_bound(csa[k], bd)
+            b.update_constraint_bound(csb[k], bd)
+            o.update_constraint_bound(cso[k], bd)
+        _flat_equal(_split_solve(a), _split_solve(b))
+        o.solve()
+        worst, bad = K.compare_values(vsa, vsb)
+        assert not bad, (step, worst, bad[:5])
+        worst, bad = K.compare_values(vsa, vso)
+        assert not bad, (step, worst, bad[:5])
+        n1, x1 = _counters(a)
+        assert (n1 - n0, x1 - x0) == (int(refresh), int(cross)), (step, bounds)
+
+
+def test_resident_refresh_path_zero_bound_churn():
+    """The C2 generator's bounds (~1/1000 of the constraints at 0) under random constraint-bound updates drawn
+    from the same law, so that steps cross the part test both ways: the device flatten equals the host
+    flatten and the values agree at every step, and most crossing steps stay on the refresh path."""
+    nC, nV = 20000, 200000
+    a = L.System(False)
+    a.set_resident(True)
+    va = a.gen_synthetic(nC, nV, k=8, seed=11)
+    b = L.System(False)
+    b.set_resident(False)
+    vb = b.gen_synthetic(nC, nV, k=8, seed=11)
+    rng = np.random.default_rng(9)
+    _flat_equal(_split_solve(a), _split_solve(b))
+    n0, x0 = _counters(a)
+    zero = 0
+    for step in range(6):
+        ids = rng.choice(nC, 400, replace=False)
+        bnds = 10.0 * rng.integers(0, 1001, len(ids)) / 1001.0
+        bnds[:2] = 0.0  # at least two crossings (or zero-to-zero moves) per step
+        zero += int(np.count_nonzero(bnds == 0))
+        for c, bd in zip(ids, bnds):
+            a.update_constraint_bound(L.Constraint(a, int(c)), float(bd))
+            b.update_constraint_bound(L.Constraint(b, int(c)), float(bd))
+        _flat_equal(_split_solve(a), _split_solve(b))
+        xa, xb = a.values_of(va), b.values_of(vb)
+        assert np.all(np.abs(xa - xb) <= np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(xb))), step
+    n1, x1 = _counters(a)
+    assert n1 - n0 == 6 and x1 - x0 >= 5, (n1 - n0, x1 - x0, zero)
