@@ -1338,6 +1338,10 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // words — the GPU never idles on the host.  A chunk queued after the last round is a run of launches
   // that return at once (CTL_DONE).
   int chunk = 2, slot = 0;
+  // rounds queued per poll: the host learns of termination one chunk late, so up to 2 x chunk_max no-op
+  // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C2 25.96-25.99 ms at 16, 26.01 at 8,
+  // 26.15-26.20 at 4
+  const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 16));
   bool pending = false;
   int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
   int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
@@ -1413,8 +1417,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     slot ^= 1;
     if (r > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
-    if (chunk < 16)
-      chunk *= 2;
+    if (chunk < chunk_max)
+      chunk = std::min(2 * chunk, chunk_max);
   }
   return poll_ctl(c);  // (the queued tail has run: final words for the stats)
 }
@@ -1475,6 +1479,10 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   // pipelined termination polls, as solve_maxmin: chunk k's control words land in a pinned slot behind an
   // event while chunk k + 1 is queued; rounds queued after the last one return at once (CTL_DONE)
   int chunk = 2, slot = 0;
+  // rounds queued per poll: the host learns of termination one chunk late, so up to 2 x chunk_max no-op
+  // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C4 3.48 ms at 8, 3.51-3.53 at 4, 3.55 at 16
+  // (short rounds: the no-op tail is a larger share)
+  const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 8));
   bool pending = false;
   int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
   int32_t* hcd[2] = {nullptr, nullptr};
@@ -1516,8 +1524,8 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
     slot ^= 1;
     if (r > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
-    if (chunk < 16)
-      chunk *= 2;
+    if (chunk < chunk_max)
+      chunk = std::min(2 * chunk, chunk_max);
   }
   return poll_ctl(c);
 }
