@@ -1431,7 +1431,7 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   if (!c->vote_diag)  // per-round diagnostic counters only on request (LMMHIP_VOTE_DIAG): they cost atomics
     d.vstat = nullptr;
   const int64_t nnz = std::max<int64_t>(d.nnz, 1);
-  const int nblk = int((int64_t(d.nC) + kFB - 1) / kFB);  // fr_update / fr_vote workgroups
+  const int nblk = int((int64_t(d.nC) + kFB - 1) / kFB);  // fr_update / fr_vote (/ fr_sat<256>) workgroups
   const int nblkS = int(std::max<int64_t>(1, (int64_t(d.nC) + kFS - 1) / kFS));  // fr_sat workgroups
   int2* cs = nullptr;
   int32_t* md = nullptr;
@@ -1465,7 +1465,10 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const bool long_rows = c->group > 8 && env_int("LMMHIP_FR_R16", 1) != 0;
   // fr_vote: segments per workgroup, so that the grid still covers the chip twice (C2: 4, small systems: 1)
   const int spb = int(std::max<int64_t>(1, std::min<int64_t>(kFVS, int64_t(nblk) / (2 * int64_t(c->n_cu)))));
-  const int sat_b = env_int("LMMHIP_FR_SATB", kFS) == 256 ? 256 : kFS;
+  // fr_sat workgroup: kFS threads (the round-4 choice on C2-size systems) unless that leaves the chip mostly
+  // idle — C4 (25 workgroups of kFS): 3.37-3.40 ms with 256-thread workgroups against 3.49
+  const int sat_b0 = int64_t(nblkS) >= 2 * int64_t(c->n_cu) ? kFS : 256;
+  const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
