@@ -830,7 +830,7 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     HIPCHK(hipStreamSynchronize(c->stream));
     int32_t flags = fl4[0];
     const int32_t nx = fl4[3];
-    if (nx > 0 && (fl4[2] || nx > kResCrossCap || env_int("LMMHIP_RES_CROSS", 1) == 0))
+    if (nx < 0 || (nx > 0 && (fl4[2] || nx > kResCrossCap || env_int("LMMHIP_RES_CROSS", 1) == 0)))
       flags |= kResStruct;
     if (!(flags & kResStruct)) {
       Dev& d = c->d;

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(kBlock)
     const double ob = r.c_bound[id[i]], nb = b[i];
     if ((ob > ob * prec) != (nb > nb * prec)) {
       const int32_t k = atomicAdd(xn, 1);
-      if (k < kResCrossCap)
+      if (k >= 0 && k < kResCrossCap)  // (k < 0: the count wrapped after 2^31 crossings without a flatten)
         xlist[k] = id[i];
       else
         f |= kResStruct;
