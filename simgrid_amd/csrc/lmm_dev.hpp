@@ -191,6 +191,7 @@ struct Dev {
   // multi-launch engine (round 4): the alive row of each variable in the buffer in use (maintained by
   // mm_init_vars and cmp_write), so that mm_saturate retires the rows of the variables it fixes (null: off)
   int32_t* rowof;
+  uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
 };

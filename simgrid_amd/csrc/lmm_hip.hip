@@ -160,6 +160,7 @@ struct lmmhip_ctx {
   // re-vote queue; the map and the largest CSC degree are rebuilt after every structural change
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
   Scr mm_rowof;  // solve_maxmin: alive row of each variable (saturation retires fixed variables' rows)
+  Scr mm_crec[3];  // solve_maxmin: packed row records (LMMHIP_CREC)
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
@@ -262,7 +263,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc})
@@ -1268,10 +1269,25 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
 // 6 compaction.
 static int solve_maxmin(lmmhip_ctx* c, double prec) {
   Dev& d = c->d;
-  struct RowofOff {  // the other engines never see the row map (their compactions do not maintain it)
-    Dev& d;
-    ~RowofOff() { d.rowof = nullptr; }
+  struct RowofOff {  // the other engines never see the row map / row records (their compactions do not
+    Dev& d;          // maintain them)
+    ~RowofOff() {
+      d.rowof = nullptr;
+      d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
+    }
   } rowof_off{d};
+  // packed row records for the re-votes (vote_row: the row's variable and CSR range from one 8-B record and
+  // its successor instead of the cvar / crow arrays, one line per re-vote less): C2 25.94-26.00 vs 26.10-26.17
+  // ms, stress 28.83 vs 29.13 (same box).  Not with the target-ordered regroups; LMMHIP_CREC=0: off.
+  d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
+  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) == 0 && env_int("LMMHIP_CREC", 1)) {
+    for (int k = 0; k < 3; k++) {
+      uint2* p = nullptr;
+      if (int rc = scratch(c, c->mm_crec[k], int64_t(d.nV) + 1, &p))
+        return rc;
+      d.crec[k] = p;
+    }
+  }
   // the saturation retires the rows of the variables it fixes (row map kept by init / cmp_write; not with
   // the target-ordered regroups, whose unpack would have to maintain it too).  Opt-in (LMMHIP_RETIRE=1):
   // measured on C2 at 26.8 ms vs 26.2 ms without (the extra row-map load and store per fixed variable

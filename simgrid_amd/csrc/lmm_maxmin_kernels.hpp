@@ -141,7 +141,10 @@ __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t
     s.x[v] = 0.0;
     s.vstate[v] = 0;
     s.rtgt[0][v] = kUnvoted;
-    const_cast<int32_t*>(s.cvar[0])[v] = int32_t(v) | (s.vbound[v] > 0 ? int32_t(0x80000000u) : 0);
+    const int32_t cv = int32_t(v) | (s.vbound[v] > 0 ? int32_t(0x80000000u) : 0);
+    const_cast<int32_t*>(s.cvar[0])[v] = cv;
+    if (s.crec[0])
+      s.crec[0][v] = make_uint2(uint32_t(cv), s.var_ptr[v]);
     if (s.rowof)
       s.rowof[v] = int32_t(v);  // buffer 0 is the CSR itself
   }
@@ -152,6 +155,8 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_NROWS + 0] = s.nV;
     s.ctl[CTL_NELEM + 0] = int32_t(s.nnz);
+    if (s.crec[0])
+      s.crec[0][s.nV] = make_uint2(0u, s.var_ptr[s.nV]);
   }
 }
 
@@ -442,10 +447,20 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   uint16_t* __restrict__ skey = s.skey[buf];
   // (key: s.key, or its copy in LDS — persistent engine, small systems)
   const int t = rtgt[row];
-  const int32_t cv = cvar[row];
+  int32_t cv;
+  uint32_t b, e;
+  if (!kCsr && s.crec[buf]) {  // (the row's variable and CSR range from one 8-B record and its successor)
+    const uint2 r0 = s.crec[buf][row], r1 = s.crec[buf][row + 1];
+    cv = int32_t(r0.x);
+    b = r0.y;
+    e = r1.y;
+  } else {
+    cv = cvar[row];
+    // (target-ordered buffers 1 / 2 keep each row's CSR range in crow / rend; buffer 0 is the CSR itself)
+    b = crow[row];
+    e = kCsr && buf != 0 ? s.rend[buf][row] : crow[row + 1];
+  }
   const int v = rvar(cv);
-  // (target-ordered buffers 1 / 2 keep each row's CSR range in crow / rend; buffer 0 is the CSR itself)
-  const uint32_t b = crow[row], e = kCsr && buf != 0 ? s.rend[buf][row] : crow[row + 1];
   const int32_t vst = s.vstate[v];
   const bool bnd = rbounded(cv);
   const double vb = bnd ? s.vbound[v] : -1.0;
@@ -1533,6 +1548,8 @@ __global__ void __launch_bounds__(1024) cmp_scan(Dev s, int nblk, int pct) {
       s.ctl[CTL_NROWS + out] = sa[t];
       s.ctl[CTL_NELEM + out] = sb[t];
       const_cast<uint32_t*>(s.crow[out])[sa[t]] = uint32_t(sb[t]);
+      if (s.crec[out])
+        s.crec[out][sa[t]] = make_uint2(0u, uint32_t(sb[t]));
     }
   }
 }
@@ -1602,6 +1619,8 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s) {
     if (al) {
       const int o = pr + xr;
       ovar[o] = v;
+      if (s.crec[out])
+        s.crec[out][o] = make_uint2(uint32_t(v), uint32_t(pe + xe));
       if (s.rowof)
         s.rowof[rvar(v)] = o;
       s.rtgt[out][o] = s.rtgt[in][row];
