@@ -1247,7 +1247,12 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
         LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
         LAUNCH(7, r, mm_vote_diagcount, grid_for((int64_t(d.nC) + 63) / 64, kBlock), kBlock, d, int(r));
       }
-      LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, int(r));
+      if (d.crec[0])
+        LAUNCH(2, r, (mm_vote_lane<kVBlock, true, 0, true>), c->n_cu, kVBlock, d, int(r));
+      else
+        LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, int(r));
+    } else if (d.crec[0]) {
+      LAUNCH(2, r, (mm_vote_lane<kBlock, false, 0, true>), grid, kBlock, d, int(r));
     } else {
       LAUNCH(2, r, (mm_vote_lane<kBlock, false>), grid, kBlock, d, int(r));
     }

@@ -136,6 +136,8 @@ __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
     atomicAdd(&s.ctl[CTL_ALIVE_C], alive_cnt);
 }
 
+// kRec: also the packed row records of buffer 0 (the multi-launch engine's init only).
+template <bool kRec = false>
 __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t nthreads) {
   for (int64_t v = t; v < s.nV; v += nthreads) {
     s.x[v] = 0.0;
@@ -143,7 +145,7 @@ __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t
     s.rtgt[0][v] = kUnvoted;
     const int32_t cv = int32_t(v) | (s.vbound[v] > 0 ? int32_t(0x80000000u) : 0);
     const_cast<int32_t*>(s.cvar[0])[v] = cv;
-    if (s.crec[0])
+    if (kRec && s.crec[0])
       s.crec[0][v] = make_uint2(uint32_t(cv), s.var_ptr[v]);
     if (s.rowof)
       s.rowof[v] = int32_t(v);  // buffer 0 is the CSR itself
@@ -151,7 +153,7 @@ __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t
 }
 
 __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
-  init_vars_range(s, int64_t(blockIdx.x) * kBlock + threadIdx.x, int64_t(gridDim.x) * kBlock);
+  init_vars_range<true>(s, int64_t(blockIdx.x) * kBlock + threadIdx.x, int64_t(gridDim.x) * kBlock);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_NROWS + 0] = s.nV;
     s.ctl[CTL_NELEM + 0] = int32_t(s.nnz);
@@ -437,7 +439,9 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
 // rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
 // kCsr: the row's elements are read from the CSR (target-ordered rows, mm_vote_tgt: a row keeps its variable id
 // and CSR range); otherwise from the buffer's own row copy.
-template <int R, bool kCsr = false>
+// kRec: the row's variable and CSR range from the packed records (crec; the multi-launch engine's short-row
+// vote only — other instantiations, e.g. the persistent kernel, keep their register budget).
+template <int R, bool kCsr = false, bool kRec = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems, const uint16_t* __restrict__ key) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
@@ -449,7 +453,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   const int t = rtgt[row];
   int32_t cv;
   uint32_t b, e;
-  if (!kCsr && s.crec[buf]) {  // (the row's variable and CSR range from one 8-B record and its successor)
+  if (kRec) {  // (the row's variable and CSR range from one 8-B record and its successor)
     const uint2 r0 = s.crec[buf][row], r1 = s.crec[buf][row + 1];
     cv = int32_t(r0.x);
     b = r0.y;
@@ -589,7 +593,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 constexpr int kQW = 2 * kWave;  // per-wave queue capacity
 constexpr int kDiagSlot = kMaxBlocks - 4;  // vstat block slots kDiagSlot.. hold the vote diagnostics (kDiag)
 
-template <bool kBits, int R, int F, int kDiag>
+template <bool kBits, int R, int F, int kDiag, bool kRec = false>
 __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
                                           const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
                                           const uint16_t* __restrict__ key) {
@@ -660,13 +664,13 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
         if (kDiag == 0)
-          vote_row<R>(s, buf, round, row, st_rows, st_elems, key);
+          vote_row<R, false, kRec>(s, buf, round, row, st_rows, st_elems, key);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   if (kDiag == 0 && lane < qn)
-    vote_row<R>(s, buf, round, qw[lane], st_rows, st_elems, key);
+    vote_row<R, false, kRec>(s, buf, round, qw[lane], st_rows, st_elems, key);
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
     for (int k = 0; k < 4; k++) {
@@ -729,7 +733,8 @@ __global__ void __launch_bounds__(kBlock) mm_vote_diagcount(Dev s, int round) {
 // Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
 // to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
-template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
+template <int B, bool kBits, int kDiag = 0, bool kRec = false>
+__global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (s.ctl[CTL_DONE])
     return;
   const int buf = s.ctl[CTL_BUF];
@@ -757,8 +762,8 @@ template <int B, bool kBits, int kDiag = 0> __global__ void __launch_bounds__(B)
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
   if (lo < hi)
-    vote_waves<kBits, 8, kFilt, kDiag>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW, &st_rows,
-                                       &st_elems, s.key);
+    vote_waves<kBits, 8, kFilt, kDiag, kRec>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
+                                             &st_rows, &st_elems, s.key);
   if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
