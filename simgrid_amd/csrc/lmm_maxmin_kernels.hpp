@@ -686,23 +686,38 @@ constexpr int kBitWords = 17408;  // LDS bitmap capacity of the multi-launch vot
 
 // The changed-constraint bitmap into LDS (16 B per thread per step).
 #ifndef LMM_BITS_UNROLL
-#define LMM_BITS_UNROLL 1  // steps with their loads in flight together (build knob, measurement)
+#define LMM_BITS_UNROLL 2  // steps with their loads in flight together (build knob, measurement)
 #endif
-template <int B> __device__ __forceinline__ void load_bits(const Dev& s, uint64_t* bits) {
+// Every CU copies the same ~125 KB at the start of every vote; starting each workgroup's copy at its own offset
+// lets an XCD's CUs miss on different lines of the freshly written bitmap instead of all waiting on the same
+// ones: C2 25.50-25.59 ms (2 loads in flight) / 25.56-25.59 (1) against 25.76-25.88 without (same box; 2 loads
+// in flight alone: 25.85); on a second box 25.30-25.31 against 25.45-25.50, 4 in flight 26.75 (stress 28.29
+// vs 28.56).  Build knob LMM_BITS_STAGGER=0: the plain copy.
+#ifndef LMM_BITS_STAGGER
+#define LMM_BITS_STAGGER 1
+#endif
+// (the multi-launch vote instantiates the staggered copy; the persistent kernel keeps the plain one, whose
+// registers it cannot spare at its 128-VGPR budget)
+template <int B, bool kStagger = false, int kU = 1>
+__device__ __forceinline__ void load_bits(const Dev& s, uint64_t* bits) {
   const int n16 = (s.nC + 127) / 128;
   const uint4* __restrict__ src = reinterpret_cast<const uint4*>(s.chgbits);
   uint4* dst = reinterpret_cast<uint4*>(bits);
-  constexpr int kU = LMM_BITS_UNROLL;
+  const int off = kStagger && n16 > 0 ? int((int64_t(blockIdx.x) * 4099 * B) % n16) : 0;
   for (int i0 = threadIdx.x; i0 < n16; i0 += kU * B) {
     uint4 t[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++)
-      if (i0 + u * B < n16)
-        t[u] = src[i0 + u * B];
+      if (i0 + u * B < n16) {
+        const int i = kStagger ? (i0 + u * B + off) % n16 : i0 + u * B;
+        t[u] = src[i];
+      }
 #pragma unroll
     for (int u = 0; u < kU; u++)
-      if (i0 + u * B < n16)
-        dst[i0 + u * B] = t[u];
+      if (i0 + u * B < n16) {
+        const int i = kStagger ? (i0 + u * B + off) % n16 : i0 + u * B;
+        dst[i] = t[u];
+      }
   }
 }
 
@@ -744,7 +759,7 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (threadIdx.x == 0)
     st_rows = st_elems = 0;
   if (kBits)
-    load_bits<B>(s, bits);
+    load_bits<B, LMM_BITS_STAGGER != 0, LMM_BITS_UNROLL>(s, bits);
   __syncthreads();
   if (kDiag == 2) {  // measurement only: the bitmap load alone, and the changed-constraint count
     if (kBits && blockIdx.x == 0 && s.vstat && round < kStatRounds) {
