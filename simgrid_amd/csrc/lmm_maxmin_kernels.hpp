@@ -168,18 +168,6 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
 // key(b*p) implies ratio[t] < b*p: the bound test of maxmin.cpp:587 stays false).  0 marks a "sensitive"
 // row whose vote depends on the target's exact ratio (a key-level tie with another constraint or with the
 // bound level), re-evaluated whenever the target is touched.
-// Ready queue (multi-launch engine, short rows): a constraint whose count of elements voting elsewhere
-// reaches 0 is queued for the round `qround` when it gets there — in the vote (a moving vote's returning
-// atomic) or in the update (the fixed variables' elements leaving it) — instead of being found by a pass over
-// the alive list (mm_ready).  One entry per constraint and round (rqst); mm_saturate_q re-checks each entry
-// (alive, still nothing voting elsewhere) after the vote, so an entry made stale by a later move is skipped.
-__device__ __forceinline__ void rdq_push(const Dev& s, int32_t c, int qround) {
-  if (atomicExch(&s.rqst[c], qround) != qround) {
-    const int q = qround & 1;
-    s.rdq[q][atomicAdd(&s.ctl[CTL_RDQ0 + q], 1)] = c;
-  }
-}
-
 __device__ __forceinline__ unsigned row_floor(unsigned sk, unsigned mk, double vb, double p) {
   unsigned fl = sk;
   if (vb > 0)
@@ -453,7 +441,7 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
 // and CSR range); otherwise from the buffer's own row copy.
 // kRec: the row's variable and CSR range from the packed records (crec; the multi-launch engine's short-row
 // vote only — other instantiations, e.g. the persistent kernel, keep their register budget).
-template <int R, bool kCsr = false, bool kRec = false, bool kRdq = false>
+template <int R, bool kCsr = false, bool kRec = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems, const uint16_t* __restrict__ key) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
@@ -586,12 +574,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     return;
   if (t >= 0 && kt != kDeadKey)
     atomicAdd(&s.nvote[t], mult_old);
-  if (kRdq) {
-    if (atomicSub(&s.nvote[newt], mult_new) == mult_new)  // nothing votes elsewhere any more: ready
-      rdq_push(s, newt, round);
-  } else {
-    atomicSub(&s.nvote[newt], mult_new);
-  }
+  atomicSub(&s.nvote[newt], mult_new);
   rtgt[row] = newt;
 }
 
@@ -610,7 +593,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 constexpr int kQW = 2 * kWave;  // per-wave queue capacity
 constexpr int kDiagSlot = kMaxBlocks - 4;  // vstat block slots kDiagSlot.. hold the vote diagnostics (kDiag)
 
-template <bool kBits, int R, int F, int kDiag, bool kRec = false, bool kRdq = false>
+template <bool kBits, int R, int F, int kDiag, bool kRec = false>
 __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
                                           const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
                                           const uint16_t* __restrict__ key) {
@@ -681,13 +664,13 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
         if (kDiag == 0)
-          vote_row<R, false, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key);
+          vote_row<R, false, kRec>(s, buf, round, row, st_rows, st_elems, key);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   if (kDiag == 0 && lane < qn)
-    vote_row<R, false, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key);
+    vote_row<R, false, kRec>(s, buf, round, qw[lane], st_rows, st_elems, key);
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
     for (int k = 0; k < 4; k++) {
@@ -765,7 +748,7 @@ __global__ void __launch_bounds__(kBlock) mm_vote_diagcount(Dev s, int round) {
 // Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
 // to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
-template <int B, bool kBits, int kDiag = 0, bool kRec = false, bool kRdq = false>
+template <int B, bool kBits, int kDiag = 0, bool kRec = false>
 __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (s.ctl[CTL_DONE])
     return;
@@ -794,8 +777,8 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
   if (lo < hi)
-    vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
-                                                   &st_rows, &st_elems, s.key);
+    vote_waves<kBits, 8, kFilt, kDiag, kRec>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
+                                             &st_rows, &st_elems, s.key);
   if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
@@ -1288,48 +1271,6 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 }
 
 
-// Saturation from the ready queue of this round (rdq; no mm_ready pass): K waves per entry, grid-stride; an
-// entry is saturated when it is still alive with nothing voting elsewhere (every vote of the round is in by
-// now).  Block 0 empties the other parity's queue, which the update of this round fills for the next one.
-template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round) {
-  if (s.ctl[CTL_DONE])
-    return;
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_RDQ0 + ((round + 1) & 1)] = 0;
-  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  const int n = s.ctl[CTL_RDQ0 + (round & 1)];
-  const int32_t* __restrict__ q = s.rdq[round & 1];
-  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  int32_t* retire = s.rowof ? s.rtgt[s.ctl[CTL_BUF]] : nullptr;
-  // the vote's queue (K waves per entry), then the update's candidate words (one wave per 64-bit word, the
-  // word's few candidates one after the other with all their chunks)
-  const int64_t na = int64_t(n) * K, nw = (int64_t(s.nC) + 63) / 64;
-  for (int64_t g = wave; g < na + nw; g += nwaves) {  // wave-uniform
-    if (g < na) {
-      const int32_t c = q[g / K];
-      const int k = int(g % K);
-      if (s.key[c] == kDeadKey || s.nvote[c] != 0)
-        continue;
-      if (k == 0 && lane == 0)
-        s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-      saturate_one<K>(s, c, k, round, lane, wpre[w], retire);
-      continue;
-    }
-    unsigned long long m = s.rbits[g - na];
-    while (m) {  // wave-uniform
-      const int32_t c = int32_t((g - na) * 64 + (__ffsll((long long)m) - 1));
-      m &= m - 1;
-      if (s.key[c] == kDeadKey || s.nvote[c] != 0)
-        continue;
-      if (lane == 0)
-        s.ctl[CTL_LASTR] = round;
-      saturate_one<1>(s, c, 0, round, lane, wpre[w], retire);
-    }
-  }
-}
-
 // Round phase 4 — constraint update: maxmin.cpp:603-658, one wave = 64 consecutive constraints (identity
 // order), so the changed-constraint bitmap the next vote reads is one ballot per wave.  A bit is set when
 // the constraint's 16-bit KEY changed or it left the light table (the only events that can move a
@@ -1340,7 +1281,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
 // K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups (key and touch
 // flag, then — touched constraints only — record, flags, scale, votes) is issued before any of them is
 // used, so a wave keeps K times the memory requests in flight.
-template <int K, bool kRdq = false>
+template <int K>
 __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
                                              bool* touch) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -1401,7 +1342,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       if (lane == l)
         fuse = m;
     }
-    bool changed = false, rdy = false;
+    bool changed = false;
     CstRec* rec = s.cst + c;
     if (sat) {
       s.key[c] = kDeadKey;
@@ -1417,8 +1358,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
         *touch = true;
         s.ctouch[c] = 0;
         rec->drem = rec->duse = rec->dcnt = 0;
-        const int nvn = nv[k] - int(qz[k]);
-        s.nvote[c] = nvn;
+        s.nvote[c] = nv[k] - int(qz[k]);
         s.chg[c] = uint16_t(round);
         double r0 = rem[k], u0;
         if (!fat) {
@@ -1445,28 +1385,19 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
           s.key[c] = uint16_t(nk);
           changed = nk != okey[k];
           alive++;
-          if (kRdq && nvn == 0) {  // its last elements voting elsewhere left with fixed variables: ready next
-            rdy = true;            // round (rbits; the stamp keeps the vote from queueing it a second time)
-            s.rqst[c] = round + 1;
-          }
         }
       }
     }
     const unsigned long long word = __ballot(changed);
     if (lane == 0)
       s.chgbits[gbase >> 6] = word;
-    if (kRdq) {
-      const unsigned long long rw = __ballot(rdy);
-      if (lane == 0)
-        s.rbits[gbase >> 6] = rw;
-    }
   }
   return alive;
 }
 
 // balive[block] = constraints of the block's range still in the light table (read by mm_done; plain
 // stores, no global atomic).
-template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1480,7 +1411,7 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
        base += 2 * stride)  // wave-uniform; two groups of 64 constraints per step, loads in flight together
-    alive += update_groups<2, kRdq>(s, base, stride, round, prec, &any_touch);
+    alive += update_groups<2>(s, base, stride, round, prec, &any_touch);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
