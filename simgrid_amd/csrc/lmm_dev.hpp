@@ -25,7 +25,7 @@ enum : int {
   CTL_NELEM = 7,     // alive-row buffer element counts (3 buffers)
   CTL_ALIVE_C = 10,  // maxmin: constraints still in the light table
   CTL_NREADY = 11,   // maxmin: ready-list length of the current round
-  CTL_NTOUCH0 = 12,  // maxmin: touched-list lengths, per round parity (2 words)
+  CTL_RDQ0 = 12,     // multi-launch maxmin: the vote's ready-queue lengths, per round parity (2 words; rdq)
   CTL_NCL0 = 14,     // maxmin: alive-constraint list lengths (2 buffers)
   CTL_LASTR = 16,    // maxmin: last round that fixed a variable (+1 = rounds)
   CTL_PALIVE0 = 17,  // persistent maxmin: constraints alive after round r's update, per round parity (2 words)
@@ -191,6 +191,10 @@ struct Dev {
   // multi-launch engine (round 4): the alive row of each variable in the buffer in use (maintained by
   // mm_init_vars and cmp_write), so that mm_saturate retires the rows of the variables it fixes (null: off)
   int32_t* rowof;
+  int32_t* rdq[2];   // round engine, short rows (LMMHIP_RDQ): constraints the vote made ready, by round parity
+  int32_t* rqst;     // [nC] the round a constraint was last queued for (one entry per constraint and round)
+  int32_t* useg;     // [blocks x kUSeg] the update's ready candidates for the next round, a segment per workgroup
+  int32_t* ucnt;     // [blocks] their counts
   uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements

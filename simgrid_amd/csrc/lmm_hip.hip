@@ -161,6 +161,7 @@ struct lmmhip_ctx {
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
   Scr mm_rowof;  // solve_maxmin: alive row of each variable (saturation retires fixed variables' rows)
   Scr mm_crec[3];  // solve_maxmin: packed row records (LMMHIP_CREC)
+  Scr mm_rdq[2], mm_rqst, mm_useg, mm_ucnt;  // solve_maxmin: ready queue / update segments (LMMHIP_RDQ)
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
@@ -263,7 +264,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc})
@@ -1247,10 +1248,14 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
         LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
         LAUNCH(7, r, mm_vote_diagcount, grid_for((int64_t(d.nC) + 63) / 64, kBlock), kBlock, d, int(r));
       }
-      if (d.crec[0])
+      if (d.rdq[0])
+        LAUNCH(2, r, (mm_vote_lane<kVBlock, true, 0, true, true>), c->n_cu, kVBlock, d, int(r));
+      else if (d.crec[0])
         LAUNCH(2, r, (mm_vote_lane<kVBlock, true, 0, true>), c->n_cu, kVBlock, d, int(r));
       else
         LAUNCH(2, r, (mm_vote_lane<kVBlock, true>), c->n_cu, kVBlock, d, int(r));
+    } else if (d.rdq[0]) {
+      LAUNCH(2, r, (mm_vote_lane<kBlock, false, 0, true, true>), grid, kBlock, d, int(r));
     } else if (d.crec[0]) {
       LAUNCH(2, r, (mm_vote_lane<kBlock, false, 0, true>), grid, kBlock, d, int(r));
     } else {
@@ -1279,6 +1284,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     ~RowofOff() {
       d.rowof = nullptr;
       d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
+      d.rdq[0] = d.rdq[1] = nullptr;
+      d.rqst = d.useg = d.ucnt = nullptr;
     }
   } rowof_off{d};
   // packed row records for the re-votes (vote_row: the row's variable and CSR range from one 8-B record and
@@ -1292,6 +1299,28 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         return rc;
       d.crec[k] = p;
     }
+  }
+  // ready constraints without the mm_ready pass: the update's workgroups (at most kMaxBlocks, each updating
+  // at most kUSeg constraints) list them for the next round, the vote queues the ones it makes ready (C2
+  // 25.07-25.22 vs 25.34-25.39 ms, stress 28.29 vs 28.46, same box; LMMHIP_RDQ=0: the mm_ready pass)
+  d.rdq[0] = d.rdq[1] = nullptr;
+  d.rqst = d.useg = d.ucnt = nullptr;
+  const int64_t gU_rdq = grid_for(d.nC, kBlock);  // (<= kMaxBlocks)
+  const int64_t per_blk = int64_t(kBlock) * ((int64_t(d.nC) + gU_rdq * kBlock - 1) / (gU_rdq * kBlock));
+  if (d.crec[0] && env_int("LMMHIP_RDQ", 1) && per_blk <= kUSeg && env_int("LMMHIP_UPD_BLOCKS", c->tune_upd) == 0) {
+    int32_t *q0 = nullptr, *q1 = nullptr, *st = nullptr, *sg = nullptr, *uc = nullptr;
+    const int64_t n = std::max<int64_t>(d.nC, 1);
+    if (int rc = scratch(c, c->mm_rdq[0], n, &q0) | scratch(c, c->mm_rdq[1], n, &q1) |
+                 scratch(c, c->mm_rqst, n, &st) | scratch(c, c->mm_useg, gU_rdq * kUSeg, &sg) |
+                 scratch(c, c->mm_ucnt, kMaxBlocks, &uc))
+      return rc;
+    HIPCHK(hipMemsetAsync(st, 0xFF, size_t(n) * sizeof(int32_t), c->stream));
+    HIPCHK(hipMemsetAsync(uc, 0, size_t(kMaxBlocks) * sizeof(int32_t), c->stream));
+    d.rdq[0] = q0;
+    d.rdq[1] = q1;
+    d.rqst = st;
+    d.useg = sg;
+    d.ucnt = uc;
   }
   // the saturation retires the rows of the variables it fixes (row map kept by init / cmp_write; not with
   // the target-ordered regroups, whose unpack would have to maintain it too).  Opt-in (LMMHIP_RETIRE=1):
@@ -1316,6 +1345,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat);
   auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
+  const int gUq = int(gU_rdq);          // (ready-queue mode: at most kUSeg constraints per workgroup)
   // mm_saturate: waves per ready constraint and the grid's block cap (measurement knobs)
   const int sat_k = env_int("LMMHIP_SAT_WAVES", c->sat_waves);
   const int sat_max = env_int("LMMHIP_SAT_GRID_MAX", kMaxBlocks);
@@ -1378,6 +1408,16 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         LAUNCH(2, r, mm_vote_tgt<kBlock>, gv, kBlock, d, int(r));
       } else if (int rc = launch_vote(c, r, nrows))
         return rc;
+      if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
+        if (sat_k == 1)
+          LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
+        else if (sat_k == 2)
+          LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        else
+          LAUNCH(4, r, mm_saturate_q<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        LAUNCH(5, r, mm_update<true>, gUq, kBlock, d, int(r), prec);
+        continue;
+      }
       LAUNCH(3, r, mm_ready, gL, kBlock, d);
       if (sat_k == 1)
         LAUNCH(4, r, mm_saturate<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gL);
@@ -1385,9 +1425,9 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         LAUNCH(4, r, mm_saturate<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gL);
       else
         LAUNCH(4, r, mm_saturate<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gL);
-      LAUNCH(5, r, mm_update, gU, kBlock, d, int(r), prec);
+      LAUNCH(5, r, mm_update<false>, gU, kBlock, d, int(r), prec);
     }
-    LAUNCH(6, r, mm_done, 1, kBlock, d, gU);
+    LAUNCH(6, r, mm_done, 1, kBlock, d, d.rdq[0] ? gUq : gU);
     bool cl = false, cm = false;
     if (r - last_clist >= cl_every && ncl > 4096) {  // alive-constraint list (order not preserved)
       LAUNCH(6, r, mm_clist, std::min(gL, 2 * c->n_cu), kBlock, d, 0);

@@ -168,6 +168,20 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
 // key(b*p) implies ratio[t] < b*p: the bound test of maxmin.cpp:587 stays false).  0 marks a "sensitive"
 // row whose vote depends on the target's exact ratio (a key-level tie with another constraint or with the
 // bound level), re-evaluated whenever the target is touched.
+// Ready constraints without the mm_ready pass (LMMHIP_RDQ): a constraint whose count of elements voting
+// elsewhere reaches 0 is ready in the round the count gets there.  The update (the fixed variables' elements
+// leaving it) lists such constraints in its workgroup's segment (useg / ucnt: mm_ready's output format, LDS
+// appends, no global atomics); the vote (a moving vote's atomicSub, made returning) queues the ones it makes
+// ready (rdq, one entry per constraint and round through the rqst stamps, which the update sets too).
+// mm_saturate_q re-checks every entry after the vote (alive, nothing voting elsewhere).
+constexpr int kUSeg = 1024;  // update candidates per workgroup segment (>= the constraints a workgroup updates)
+__device__ __forceinline__ void rdq_push(const Dev& s, int32_t c, int qround) {
+  if (atomicExch(&s.rqst[c], qround) != qround) {
+    const int q = qround & 1;
+    s.rdq[q][atomicAdd(&s.ctl[CTL_RDQ0 + q], 1)] = c;
+  }
+}
+
 __device__ __forceinline__ unsigned row_floor(unsigned sk, unsigned mk, double vb, double p) {
   unsigned fl = sk;
   if (vb > 0)
@@ -441,7 +455,7 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
 // and CSR range); otherwise from the buffer's own row copy.
 // kRec: the row's variable and CSR range from the packed records (crec; the multi-launch engine's short-row
 // vote only — other instantiations, e.g. the persistent kernel, keep their register budget).
-template <int R, bool kCsr = false, bool kRec = false>
+template <int R, bool kCsr = false, bool kRec = false, bool kRdq = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems, const uint16_t* __restrict__ key) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
@@ -574,7 +588,12 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     return;
   if (t >= 0 && kt != kDeadKey)
     atomicAdd(&s.nvote[t], mult_old);
-  atomicSub(&s.nvote[newt], mult_new);
+  if (kRdq) {
+    if (atomicSub(&s.nvote[newt], mult_new) == mult_new)  // nothing votes elsewhere any more: ready
+      rdq_push(s, newt, round);
+  } else {
+    atomicSub(&s.nvote[newt], mult_new);
+  }
   rtgt[row] = newt;
 }
 
@@ -593,7 +612,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 constexpr int kQW = 2 * kWave;  // per-wave queue capacity
 constexpr int kDiagSlot = kMaxBlocks - 4;  // vstat block slots kDiagSlot.. hold the vote diagnostics (kDiag)
 
-template <bool kBits, int R, int F, int kDiag, bool kRec = false>
+template <bool kBits, int R, int F, int kDiag, bool kRec = false, bool kRdq = false>
 __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
                                           const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
                                           const uint16_t* __restrict__ key) {
@@ -664,13 +683,13 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
         if (kDiag == 0)
-          vote_row<R, false, kRec>(s, buf, round, row, st_rows, st_elems, key);
+          vote_row<R, false, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   if (kDiag == 0 && lane < qn)
-    vote_row<R, false, kRec>(s, buf, round, qw[lane], st_rows, st_elems, key);
+    vote_row<R, false, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key);
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
     for (int k = 0; k < 4; k++) {
@@ -748,7 +767,7 @@ __global__ void __launch_bounds__(kBlock) mm_vote_diagcount(Dev s, int round) {
 // Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
 // to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
-template <int B, bool kBits, int kDiag = 0, bool kRec = false>
+template <int B, bool kBits, int kDiag = 0, bool kRec = false, bool kRdq = false>
 __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (s.ctl[CTL_DONE])
     return;
@@ -777,8 +796,8 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   const int64_t lo = int64_t(blockIdx.x) * per;
   const int64_t hi = lo + per < nrows ? lo + per : nrows;
   if (lo < hi)
-    vote_waves<kBits, 8, kFilt, kDiag, kRec>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
-                                             &st_rows, &st_elems, s.key);
+    vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
+                                                   &st_rows, &st_elems, s.key);
   if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
@@ -1271,6 +1290,77 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 }
 
 
+// Saturation without the mm_ready pass (LMMHIP_RDQ): the update's per-workgroup candidate segments (ublocks of
+// them, mm_saturate's prefix and binary search over their counts) then the vote's queue; K waves per entry;
+// an entry is saturated when it is still alive with nothing voting elsewhere (every vote of the round is in).
+// Block 0 empties the other parity's vote queue, which the next round's vote fills.
+template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_RDQ0 + ((round + 1) & 1)] = 0;
+  __shared__ int pre[kMaxBlocks + 1];
+  __shared__ int wsum[kBlock / kWave];
+  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
+  constexpr int kPer = kMaxBlocks / kBlock;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int loc[kPer];
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int seg = threadIdx.x * kPer + k;
+    loc[k] = seg < ublocks ? s.ucnt[seg] : 0;
+    sum += loc[k];
+  }
+  int incl = sum;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int t = __shfl_up(incl, o, kWave);
+    if (lane >= o)
+      incl += t;
+  }
+  if (lane == kWave - 1)
+    wsum[w] = incl;
+  __syncthreads();
+  int acc = incl - sum, total = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / kWave; i++) {
+    acc += i < w ? wsum[i] : 0;
+    total += wsum[i];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    pre[threadIdx.x * kPer + k] = acc;
+    acc += loc[k];
+  }
+  __syncthreads();
+  const int nq = s.ctl[CTL_RDQ0 + (round & 1)];
+  const int32_t* __restrict__ q = s.rdq[round & 1];
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+  int32_t* retire = s.rowof ? s.rtgt[s.ctl[CTL_BUF]] : nullptr;
+  for (int64_t g = wave; g < (int64_t(total) + nq) * K; g += nwaves) {  // wave-uniform
+    const int64_t i = g / K;
+    const int k = int(g % K);
+    int32_t c;
+    if (i < total) {
+      int lo = 0;  // last segment with pre[seg] <= i
+#pragma unroll
+      for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
+        if (lo + step < ublocks && pre[lo + step] <= i)
+          lo += step;
+      c = s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
+    } else {
+      c = q[i - total];
+    }
+    if (s.key[c] == kDeadKey || s.nvote[c] != 0)
+      continue;
+    if (k == 0 && lane == 0)
+      s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
+    saturate_one<K>(s, c, k, round, lane, wpre[w], retire);
+  }
+}
+
 // Round phase 4 — constraint update: maxmin.cpp:603-658, one wave = 64 consecutive constraints (identity
 // order), so the changed-constraint bitmap the next vote reads is one ballot per wave.  A bit is set when
 // the constraint's 16-bit KEY changed or it left the light table (the only events that can move a
@@ -1281,9 +1371,9 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 // K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups (key and touch
 // flag, then — touched constraints only — record, flags, scale, votes) is issued before any of them is
 // used, so a wave keeps K times the memory requests in flight.
-template <int K>
+template <int K, bool kRdq = false>
 __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
-                                             bool* touch) {
+                                             bool* touch, int* ucnt_sh = nullptr, int32_t* ulist = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
   unsigned okey[K], tf[K];
 #pragma unroll
@@ -1358,7 +1448,8 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
         *touch = true;
         s.ctouch[c] = 0;
         rec->drem = rec->duse = rec->dcnt = 0;
-        s.nvote[c] = nv[k] - int(qz[k]);
+        const int nvn = nv[k] - int(qz[k]);
+        s.nvote[c] = nvn;
         s.chg[c] = uint16_t(round);
         double r0 = rem[k], u0;
         if (!fat) {
@@ -1385,6 +1476,10 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
           s.key[c] = uint16_t(nk);
           changed = nk != okey[k];
           alive++;
+          if (kRdq && nvn == 0) {  // its last elements voting elsewhere left with fixed variables: ready next
+            ulist[atomicAdd(ucnt_sh, 1)] = int32_t(c);  // round (the stamp keeps the vote from queueing it too)
+            s.rqst[c] = round + 1;
+          }
         }
       }
     }
@@ -1397,26 +1492,34 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
 
 // balive[block] = constraints of the block's range still in the light table (read by mm_done; plain
 // stores, no global atomic).
-__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_ROUNDS] += 1;
-  __shared__ int alive_cnt;
+  __shared__ int alive_cnt, ucnt_sh;
+  __shared__ int32_t ulist[kRdq ? kUSeg : 1];
   if (threadIdx.x == 0)
-    alive_cnt = 0;
+    alive_cnt = ucnt_sh = 0;
   __syncthreads();
   int alive = 0;
   bool any_touch = false;
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
        base += 2 * stride)  // wave-uniform; two groups of 64 constraints per step, loads in flight together
-    alive += update_groups<2>(s, base, stride, round, prec, &any_touch);
+    alive += update_groups<2, kRdq>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
   if (threadIdx.x == 0)
     s.balive[blockIdx.x] = alive_cnt;
+  if (kRdq) {  // the workgroup's ready candidates for the next round into its segment
+    const int n = ucnt_sh;
+    for (int i = threadIdx.x; i < n; i += kBlock)
+      s.useg[int64_t(blockIdx.x) * kUSeg + i] = ulist[i];
+    if (threadIdx.x == 0)
+      s.ucnt[blockIdx.x] = n;
+  }
   if (__syncthreads_or(any_touch) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
 }

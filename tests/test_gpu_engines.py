@@ -178,12 +178,15 @@ def test_target_ordered_vote_bit_identical(stress, monkeypatch):
     bitmap-filter vote over order-preserving compactions give the same bytes: the row order
     changes no vote.  1e5 x 1e6 x 8 (the C2/10 system: 25+ regroups)."""
     out = []
-    # (LMMHIP_TGT, LMMHIP_RETIRE, LMMHIP_CREC): the opt-in row retirement by the saturation and the packed row
-    # records must not change a byte either
-    for tgt, retire, crec in (("1", "0", "0"), ("0", "0", "0"), ("0", "1", "0"), ("0", "0", "1"), ("0", "1", "1")):
+    # (LMMHIP_TGT, LMMHIP_RETIRE, LMMHIP_CREC, LMMHIP_RDQ): the row retirement by the saturation, the packed row
+    # records and the ready constraints listed by the update and the vote (no mm_ready pass) must not change a
+    # byte either
+    for tgt, retire, crec, rdq in (("1", "0", "0", "0"), ("0", "0", "0", "0"), ("0", "1", "1", "0"),
+                                   ("0", "0", "1", "0"), ("0", "0", "1", "1"), ("0", "1", "1", "1")):
         monkeypatch.setenv("LMMHIP_TGT", tgt)
         monkeypatch.setenv("LMMHIP_RETIRE", retire)
         monkeypatch.setenv("LMMHIP_CREC", crec)
+        monkeypatch.setenv("LMMHIP_RDQ", rdq)
         out.append(_values(_synthetic(100000, 1000000, 1, stress), L.System.ENGINE_ROUNDS))
     for o in out[1:]:
         assert out[0][1] == o[1]
