@@ -454,3 +454,52 @@ def flow_ops(p):
                 vpen=np.ascontiguousarray(vpen, dtype=np.float64), vbound=np.ascontiguousarray(vbound),
                 vn=vn, eptr=eptr, ecnst=C[mask].astype(np.int32), ew=W[mask].astype(np.float64),
                 eadd=A[mask].astype(np.uint8))
+
+
+# ---- one link / one communication over explicit links (the pingpong replay, tests/pingpong_scenario.py) ----
+def net_factors(model):
+    """(latency factor, bandwidth factor, weight_S) of network_cm02.cpp:36-64: LV08 13.01 / 0.97 / 20537,
+    CM02 1 / 1 / 0."""
+    if model == LV08:
+        return 13.01, 0.97, 20537.0
+    if model == CM02:
+        return 1.0, 1.0, 0.0
+    raise ValueError(f"not a CM02-family network model: {model}")
+
+
+def link_new(sys, model, bw, fatpipe=False):
+    """NetworkCm02Link's constraint (network_cm02.cpp:282-295) on an oracle System: bandwidth factor * bw."""
+    c = sys.constraint_new(None, net_factors(model)[1] * bw)
+    if fatpipe:
+        c.unshare()
+    return c
+
+
+def communicate(sys, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False):
+    """NetworkCm02Model::communicate (network_cm02.cpp:165-274), its LMM part, on an oracle System:
+    route = [(constraint, bw, lat)] in route order (route_to sums the latencies), back = the back route's
+    constraints (crosstraffic, weight 0.05).  Returns (variable, dict(latency, lat_current, sharing_penalty,
+    bound)); the variable has penalty 0 while the latency is unpaid (1.0 without latency), or with `paid`
+    the sharing penalty update_actions_state restores (network_cm02.cpp:105-146)."""
+    lat_factor, _, weight_s = net_factors(model)
+    lat = 0.0
+    for _, _, l in route:
+        lat += l
+    sharing_penalty = lat  # action->sharing_penalty_ = latency (network_cm02.cpp:188)
+    if weight_s > 0:      # std::accumulate over the route (network_cm02.cpp:196-201)
+        for _, bw, _ in route:
+            sharing_penalty = sharing_penalty + weight_s / bw
+    lat_current = lat
+    latency = lat * lat_factor  # latency_ *= get_latency_factor(size) (network_cm02.cpp:208-209)
+    if rate < 0:
+        bound = tcp_gamma / (2.0 * lat_current) if lat_current > 0 else -1.0
+    else:
+        bound = min(rate, tcp_gamma / (2.0 * lat_current)) if lat_current > 0 else rate
+    pen = (sharing_penalty if paid else 0.0) if latency > 0 else 1.0
+    v = sys.variable_new(None, pen, -1.0, len(route) + len(back))
+    sys.update_variable_bound(v, bound)
+    for c, _, _ in route:
+        sys.expand(c, v, 1.0)
+    for c in back:
+        sys.expand(c, v, 0.05)
+    return v, dict(latency=latency, lat_current=lat_current, sharing_penalty=sharing_penalty, bound=bound)

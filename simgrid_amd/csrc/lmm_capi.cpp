@@ -481,4 +481,57 @@ int64_t lmm_gen_platform_flows(lmm_sys* s, const lmm_platform_params* p, int64_t
   }
 }
 
+int64_t lmm_link_new(lmm_sys* s, int model, double bw, int fatpipe) {
+  try {
+    if (!s)
+      throw std::invalid_argument("null system");
+    Builder b{&s->sys};
+    return lmm_plat::link_constraint(b, model, bw, fatpipe != 0);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int64_t lmm_communicate(lmm_sys* s, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
+                        const double* route_lat, int64_t n_back, const int64_t* back_cnst, double rate,
+                        double tcp_gamma, int paid, lmm_comm_info* out) {
+  try {
+    if (!s || n_route < 0 || n_back < 0 || (n_route && (!route_cnst || !route_bw || !route_lat)) ||
+        (n_back && !back_cnst))
+      throw std::invalid_argument("lmm_communicate: bad arguments");
+    Builder b{&s->sys};
+    std::vector<lmm_plat::Link> links;
+    std::vector<Id> cn;
+    std::vector<int> route, back;
+    double lat = 0.0;  // route_to accumulates the route's latencies in route order
+    for (int64_t i = 0; i < n_route; i++) {
+      if (!cnst_ok(s, route_cnst[i]))
+        throw std::invalid_argument("lmm_communicate: bad route constraint");
+      links.push_back({route_bw[i], route_lat[i], false});
+      cn.push_back(Id(route_cnst[i]));
+      route.push_back(int(i));
+      lat += route_lat[i];
+    }
+    for (int64_t i = 0; i < n_back; i++) {
+      if (!cnst_ok(s, back_cnst[i]))
+        throw std::invalid_argument("lmm_communicate: bad back-route constraint");
+      cn.push_back(Id(back_cnst[i]));
+      back.push_back(int(n_route + i));
+    }
+    lmm_plat::Comm a;
+    const Id v = lmm_plat::communicate(b, model, links, cn, route, back, lat, rate, tcp_gamma, paid != 0, &a);
+    if (out) {
+      out->latency = a.latency;
+      out->lat_current = a.lat_current;
+      out->sharing_penalty = a.sharing_penalty;
+      out->bound = a.bound;
+    }
+    return v;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 }  // extern "C"

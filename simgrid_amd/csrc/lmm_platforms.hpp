@@ -491,6 +491,68 @@ inline size_t n_constraints(const Platform& plat, const Params& p) {
   return plat.links.size() + (p.model == L07 ? size_t(plat.n_hosts) : 0);
 }
 
+// The network model's factors (network_cm02.cpp:36-64): LV08 = latency factor 13.01, bandwidth factor 0.97,
+// weight_S 20537; CM02 = 1, 1, 0.
+struct NetFactors {
+  double latency, bandwidth, weight_s;
+};
+inline NetFactors net_factors(int model) {
+  if (model == LV08)
+    return {13.01, 0.97, 20537.0};
+  if (model == CM02)
+    return {1.0, 1.0, 0.0};
+  throw std::invalid_argument("not a CM02-family network model: " + std::to_string(model));
+}
+
+// A link's constraint (NetworkCm02Link, network_cm02.cpp:282-295): bound = bandwidth factor * bandwidth,
+// FATPIPE unshared.
+template <class B>
+typename B::Cnst link_constraint(B& b, int model, double bw, bool fatpipe) {
+  typename B::Cnst c = b.constraint_new(net_factors(model).bandwidth * bw);
+  if (fatpipe)
+    b.unshare(c);
+  return c;
+}
+
+// One communication, NetworkCm02Model::communicate (network_cm02.cpp:165-274): the action's latency (after the
+// latency factor), its sharing penalty (the route latency + weight_S / bw per route link, in route order), the
+// bound (rate < 0: TCP-gamma / (2 * route latency); else min(rate, that)), the variable — penalty 0 while the
+// latency is unpaid (1 without latency), or, `paid`, the state once it is paid (update_actions_state restores
+// the sharing penalty: network_cm02.cpp:105-146) — and its elements: each route link at 1.0, with
+// crosstraffic each back-route link at 0.05.  route / back: indices into `links` and `cn`.
+struct Comm {
+  double latency;          // NetworkAction::latency_ (route latency * latency factor)
+  double lat_current;      // lat_current_ (route latency)
+  double sharing_penalty;  // sharing_penalty_
+  double bound;            // the variable's bound
+};
+template <class B>
+typename B::Var communicate(B& b, int model, const std::vector<Link>& links, const std::vector<typename B::Cnst>& cn,
+                            const std::vector<int>& route, const std::vector<int>& back, double lat, double rate,
+                            double tcp_gamma, bool paid, Comm* out = nullptr) {
+  const NetFactors f = net_factors(model);
+  Comm a;
+  a.sharing_penalty = lat;
+  a.lat_current = lat;
+  if (f.weight_s > 0)
+    for (int l : route)
+      a.sharing_penalty += f.weight_s / links[size_t(l)].bw;
+  a.latency = lat * f.latency;
+  if (rate < 0)
+    a.bound = a.lat_current > 0 ? tcp_gamma / (2.0 * a.lat_current) : -1.0;
+  else
+    a.bound = a.lat_current > 0 ? std::min(rate, tcp_gamma / (2.0 * a.lat_current)) : rate;
+  const double pen = a.latency > 0 ? (paid ? a.sharing_penalty : 0.0) : 1.0;
+  typename B::Var v = b.variable_new(pen, a.bound, int(route.size() + back.size()));
+  for (int l : route)
+    b.expand(cn[size_t(l)], v, 1.0);
+  for (int l : back)
+    b.expand(cn[size_t(l)], v, 0.05);
+  if (out)
+    *out = a;
+  return v;
+}
+
 // Links first (one constraint per link, network_cm02.cpp:286-295 / ptask_L07.cpp:247-255, FATPIPE
 // unshared), then for L07 one CPU constraint per host (ptask_L07.cpp:239-240), then the flows.
 template <class B>
@@ -500,15 +562,17 @@ void flows(B& b, const Platform& plat, const Params& p, std::vector<typename B::
     throw std::invalid_argument("unknown flow model " + std::to_string(p.model));
   if (plat.n_hosts <= 0)
     throw std::invalid_argument("platform without hosts");
-  const bool l07 = p.model == L07, lv08 = p.model == LV08;
-  const double bw_factor = lv08 ? 0.97 : 1.0;
-  const double weight_s = lv08 ? 20537.0 : 0.0;
+  const bool l07 = p.model == L07;
   std::vector<typename B::Cnst> cn;
   cn.reserve(n_constraints(plat, p));
   for (const Link& l : plat.links) {
-    cn.push_back(b.constraint_new((l07 ? 1.0 : bw_factor) * l.bw));
-    if (l.fatpipe)
-      b.unshare(cn.back());
+    if (l07) {
+      cn.push_back(b.constraint_new(l.bw));
+      if (l.fatpipe)
+        b.unshare(cn.back());
+    } else {
+      cn.push_back(link_constraint(b, p.model, l.bw, l.fatpipe));
+    }
   }
   const size_t cpu0 = cn.size();
   if (l07)
@@ -543,18 +607,8 @@ void flows(B& b, const Platform& plat, const Params& p, std::vector<typename B::
       back.clear();
       if (p.crosstraffic)
         plat.route(dst, src, back, nullptr);
-      double pen = 1.0, bound = -1.0;
-      if (lat > 0) {  // penalty = latency + sum(weight_S / bw) once the latency is paid
-        pen = lat;
-        for (int l : route)
-          pen += weight_s / plat.links[size_t(l)].bw;
-        bound = p.tcp_gamma / (2.0 * lat);
-      }
-      v = b.variable_new(pen, bound, int(route.size() + back.size()));
-      for (int l : route)
-        b.expand(cn[size_t(l)], v, 1.0);
-      for (int l : back)
-        b.expand(cn[size_t(l)], v, 0.05);
+      // rate -1 (no user rate), in the state once the latency is paid
+      v = communicate(b, p.model, plat.links, cn, route, back, lat, -1.0, p.tcp_gamma, true);
     }
     if (var_out)
       vars.push_back(v);

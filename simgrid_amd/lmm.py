@@ -39,6 +39,11 @@ def platform_params(topology=FAT_TREE, topo_parameters="", bw=1.25e8, lat=5e-5, 
     return PlatformParams(topology, topo_parameters.encode(), bw, lat, policy, loopback_bw, loopback_lat, limiter_bw,
                           speed, model, int(crosstraffic), n_flows, seed, size_min, size_max, tcp_gamma)
 
+class CommInfo(ct.Structure):
+    """lmm_comm_info (include/lmm/lmm_system.h): a communication's action parameters."""
+    _fields_ = [("latency", D), ("lat_current", D), ("sharing_penalty", D), ("bound", D)]
+
+
 class LmmhipStats(ct.Structure):
     """lmmhip_stats (include/lmm/lmm_hip.h)."""
     _fields_ = [("rounds", I64), ("n_var", I64), ("n_cnst", I64), ("nnz", I64), ("device_ms", D),
@@ -112,6 +117,8 @@ SIGNATURES = {
     "lmm_gen_synthetic": (I64, [P, I64, I64, I, U64, I, I, I, I, PI64]),
     "lmm_platform_size": (I, [ct.POINTER(PlatformParams), PI64, PI64]),
     "lmm_gen_platform_flows": (I64, [P, ct.POINTER(PlatformParams), PI64, PI64]),
+    "lmm_link_new": (I64, [P, I, D, I]),
+    "lmm_communicate": (I64, [P, I, I64, PI64, PD, PD, I64, PI64, D, D, I, P]),
     "lmm_device_count": (I, []),
     "lmm_last_error": (ct.c_char_p, []),
     # include/lmm/lmm_hip.h
@@ -648,6 +655,30 @@ class System:
         if r < 0:
             raise LmmError(lib().lmm_last_error().decode())
         return cs, vs
+
+    def link_new(self, model, bw, fatpipe=False):
+        """A link's constraint (lmm_link_new: NetworkCm02Link, bound = bandwidth factor * bw)."""
+        h = lib().lmm_link_new(self.h, model, bw, int(fatpipe))
+        if h < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return Constraint(self, h)
+
+    def communicate(self, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False):
+        """NetworkCm02Model::communicate's LMM part (lmm_communicate): route = [(Constraint, bw, lat)] in route
+        order, back = the back route's Constraints (crosstraffic).  Returns (Variable, dict(latency, lat_current,
+        sharing_penalty, bound))."""
+        n = len(route)
+        rc = np.array([c.h for c, _, _ in route], dtype=np.int64)
+        rb = np.array([b for _, b, _ in route], dtype=np.float64)
+        rl = np.array([l for _, _, l in route], dtype=np.float64)
+        bc = np.array([c.h for c in back], dtype=np.int64)
+        info = CommInfo()
+        h = lib().lmm_communicate(self.h, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
+                                  rl.ctypes.data_as(PD), len(bc), bc.ctypes.data_as(PI64), rate, tcp_gamma,
+                                  int(paid), ct.byref(info))
+        if h < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return Variable(self, h), {k: getattr(info, k) for k, _ in CommInfo._fields_}
 
     def values_of(self, ids):
         ids = np.ascontiguousarray(ids, dtype=np.int64)

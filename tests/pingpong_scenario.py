@@ -1,0 +1,236 @@
+"""TEST INFRASTRUCTURE ONLY: the reference's s4u-app-pingpong example as a tiny surf engine.
+
+examples/s4u/app-pingpong/s4u-app-pingpong.cpp sends a 1-B message from "pinger" on Tremblay to "ponger" on
+Jupiter, then a 1e9-B message back, over examples/platforms/small_platform.xml (the route Tremblay -> Jupiter
+is link 9: 7.20975 MBps, 1.461517 ms; Full routing is symmetric, so the way back is link 9 too).  Its tesh
+file prints the dates for three network configurations, the reference's own known answer for the LMM flow
+model and for both model-side step paths:
+  * LV08 (the default: latency factor 13.01, bandwidth factor 0.97, weight_S 20537, network_cm02.cpp:36-44),
+    LAZY update (the default "network/optim") -> 0.019014, then 150.178356;
+  * LV08, `--cfg=network/optim:Full` (Model::next_occuring_event_full, Model.cpp:103-129, with the network
+    model's latency term, network_interface.cpp:57-70; update_actions_state_full, network_cm02.cpp:128-163)
+    -> the same dates;
+  * CM02 (factors 1 / 1 / 0, network_cm02.cpp:56-64), LAZY -> 0.001462, then 145.639041.
+The dates exercise the flow construction of NetworkCm02Model::communicate (network_cm02.cpp:165-274): the
+latency factor on the latency hat, the weight_S sharing penalty, the TCP-gamma bound, the 0.05 cross-traffic
+element on the shared link (the flow gets 0.97 * 7.20975e6 / 1.05 B/s), and the link's bandwidth-factor bound
+(network_cm02.cpp:282-295).
+
+What is restated here (test code): the s4u layer of the example reduced to its two communications (each
+starts at the date the previous one finishes, the finished action is destroyed first: Action::~Action frees
+its variable), surf_solve for a single network model (surf_c_bindings.cpp:45-148; no profiles, no CPU
+actions) and the LAZY network step of tests/surf_scenario.py.  The flows themselves are built by the backend
+through the flow code under test: the product's lmm_platforms.hpp `communicate` (lmm_communicate, the code
+that also builds the C4 platform's flows) on the device path, oracle/platforms.py's restatement on the oracle
+path.  Backends:
+  * PingOracle — oracle/pyoracle.py's System + oracle/step_oracle (next_occuring_event_full /
+    update_actions_state_full, LazyModel's real heap);
+  * PingDevice — simgrid_amd.lmm.System (HIP solve) + simgrid_amd.step.DeviceActions (act_next_event /
+    act_update in Full mode, act_lazy_* in Lazy mode).
+"""
+import json
+import os
+
+from tests.surf_scenario import (HEAP_LATENCY, HEAP_NORMAL, HEAP_UNSET, MAXMIN_PREC, MODEL_NET, NO_MAX_DURATION,
+                                 SURF_PREC, TCP_GAMMA, Action, DeviceBackend, Model, OracleBackend)
+
+CM02, LV08 = 0, 1  # lmm_platforms.hpp FlowModel / oracle/platforms.py
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pingpong.json")
+RUNS = {"lv08_lazy": (LV08, "lazy"), "lv08_full": (LV08, "full"), "cm02_lazy": (CM02, "lazy")}
+EV_FINISHED, EV_LATENCY_PAID = 1, 2
+
+
+def golden():
+    """tests/golden/pingpong.json (tests/golden/make_pingpong.py): the tesh lines and link 9."""
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def expected(run):
+    return [tuple(x) for x in golden()["expected"][run]]
+
+
+class FullModel:
+    """A FULL-update network model (NetworkCm02Model with network/optim:Full): no heap, every step solves and
+    scans the started actions."""
+
+    def __init__(self, backend):
+        self.kind, self.backend = MODEL_NET, backend
+        self.sys = backend.new_system(False)  # Full: maxmin-selective-update off (network_cm02.cpp:69-81)
+        self.actions = []
+
+    def started(self):
+        return [a for a in self.actions if a.alive and a.state == Action.STARTED]
+
+    def next_occuring_event(self, now):  # NetworkModel::next_occuring_event_full (network_interface.cpp:57-70)
+        return self.backend.full_next(self)
+
+    def update_actions_state(self, now, delta):  # NetworkCm02Model::update_actions_state_full
+        for a, ev in self.backend.full_update(self, delta):
+            if ev & EV_LATENCY_PAID:
+                self.sys.update_variable_penalty(a.var, a.sharing_penalty)
+            if ev & EV_FINISHED:
+                Model.finish(a, now)
+
+    def unref(self, a):
+        a.alive = False
+        self.sys.variable_free(a.var)
+
+
+class LazyNet(Model):
+    def __init__(self, backend):
+        self.kind, self.backend = MODEL_NET, backend
+        self.sys = backend.new_system(True)  # Lazy: selective update forced (network_cm02.cpp:74-78)
+        self.actions = []
+        self.extra_modified = []
+
+    def update_actions_state(self, now, delta=None):
+        Model.update_actions_state(self, now)
+
+
+class PingPong:
+    """surf with one network model (model, algo) over link 9, and the example's two communications."""
+
+    def __init__(self, backend, model, algo):
+        self.backend, self.model, self.algo, self.now = backend, model, algo, 0.0
+        self.net = LazyNet(backend) if algo == "lazy" else FullModel(backend)
+        link = golden()["route_tremblay_jupiter"]
+        assert len(link) == 1
+        self.bw, self.lat = link[0]["bw"], link[0]["lat"]
+        self.cnst = backend.link_new(self.net.sys, model, self.bw)
+
+    def communicate(self, size):
+        """Tremblay <-> Jupiter: route [link 9], back route [link 9] (crosstraffic, the default)."""
+        a = Action(self.net, size, self.now)
+        a.id = len(self.net.actions) + 1
+        self.backend.register(self.net, a)
+        a.var, info = self.backend.communicate(self.net.sys, self.model, [(self.cnst, self.bw, self.lat)],
+                                               [self.cnst], -1.0, TCP_GAMMA, a.id)
+        a.latency, a.sharing_penalty = info["latency"], info["sharing_penalty"]
+        a.last_update = self.now
+        if self.algo == "lazy" and a.latency > 0:  # the latency-paid event on the heap (network_cm02.cpp:226-234)
+            a.date, a.heap_type = a.latency + a.last_update, HEAP_LATENCY
+        self.net.actions.append(a)
+        return a
+
+    def solve(self):
+        """surf_solve (surf_c_bindings.cpp:45-148) with a single network model and no resource profiles."""
+        delta = self.net.next_occuring_event(self.now)
+        if delta < 0:
+            return -1.0
+        self.now += delta
+        self.net.update_actions_state(self.now, delta)
+        return delta
+
+    def wait(self, a):
+        while a.state == Action.STARTED:
+            assert self.solve() >= 0, "no event while a communication is running"
+        assert a.state == Action.FINISHED
+        self.net.unref(a)  # the finished communication's action is destroyed: its variable leaves the system
+
+
+def run_pingpong(backend, run):
+    """s4u-app-pingpong.cpp: the (clock, actor@host, message) lines it logs in tesh run `run`."""
+    model, algo = RUNS[run]
+    e = PingPong(backend, model, algo)
+    clock = lambda: "%.6f" % e.now  # noqa: E731  ("[%10.6r]")
+    out = [(clock(), "pinger@Tremblay", "Ping from mailbox Mailbox 1 to mailbox Mailbox 2"),
+           (clock(), "ponger@Jupiter", "Pong from mailbox Mailbox 2 to mailbox Mailbox 1")]
+    sent = e.now
+    e.wait(e.communicate(1.0))
+    t1 = e.now
+    out += [(clock(), "ponger@Jupiter", "Task received : small communication (latency bound)"),
+            (clock(), "ponger@Jupiter", " Ping time (latency bound) %f" % (t1 - sent)),
+            (clock(), "ponger@Jupiter", "task_bw->data = %.3f" % t1)]
+    e.wait(e.communicate(1e9))
+    out += [(clock(), "pinger@Tremblay", "Task received : large communication (bandwidth bound)"),
+            (clock(), "pinger@Tremblay", "Pong time (bandwidth bound): %.3f" % (e.now - t1)),
+            (clock(), "maestro@", "Total simulation time: %.3f" % e.now)]
+    return out, e
+
+
+# ---- backends ----
+class PingOracle(OracleBackend):
+    def __init__(self):
+        super().__init__()
+        from oracle import platforms as PL
+        self.PL = PL
+
+    def new_system(self, selective=True):
+        return self.O.System(selective)
+
+    def link_new(self, sys, model, bw):
+        return self.PL.link_new(sys, model, bw)
+
+    def communicate(self, sys, model, route, back, rate, tcp_gamma, _aid):
+        return self.PL.communicate(sys, model, route, back, rate, tcp_gamma)
+
+    def _full(self, model):
+        acts = model.started()
+        st = dict(remains=[a.remains for a in acts], max_duration=[a.max_duration for a in acts],
+                  latency=[a.latency for a in acts], penalty=[a.var.get_penalty() for a in acts],
+                  sharing_penalty=[a.sharing_penalty for a in acts],
+                  flags=[0 if a.var.get_number_of_constraint() else self.S.ACT_NO_CNST for a in acts])
+        return acts, st, [a.var.get_value() for a in acts]
+
+    def full_next(self, model):
+        model.sys.solve()
+        _, st, values = self._full(model)
+        return self.S.next_occuring_event_full(values, st["remains"], st["max_duration"], st["latency"])
+
+    def full_update(self, model, delta):
+        acts, st, values = self._full(model)
+        ev = self.S.update_actions_state_full(1, values, st, delta, MAXMIN_PREC, SURF_PREC)
+        for i, a in enumerate(acts):
+            a.remains, a.max_duration, a.latency = st["remains"][i], st["max_duration"][i], st["latency"][i]
+        return [(a, e) for a, e in zip(acts, ev) if e]
+
+
+class PingDevice(DeviceBackend):
+    def new_system(self, selective=True):
+        return self.L.System(selective)
+
+    def link_new(self, sys, model, bw):
+        return sys.link_new(model, bw)
+
+    def communicate(self, sys, model, route, back, rate, tcp_gamma, aid):
+        v, info = sys.communicate(model, route, back, rate, tcp_gamma)
+        return v, info
+
+    def _full(self, model):
+        import numpy as np
+        D = self.D
+        acts = model.started()
+        vi = np.array([model.__dict__.get("vidx", {}).get(id(a), -1) for a in acts], np.int32)
+        da = D.DeviceActions(model.sys.device_ctx(), vi, remains=[a.remains for a in acts],
+                             max_duration=[a.max_duration for a in acts], latency=[a.latency for a in acts],
+                             penalty=[a.var.get_penalty() for a in acts],
+                             sharing_penalty=[a.sharing_penalty for a in acts],
+                             flags=[0 if a.var.get_number_of_constraint() else D.ACT_NO_CNST for a in acts])
+        return acts, da
+
+    def full_next(self, model):
+        if model.sys.modified:  # System::solve runs lmm_solve only when something changed (maxmin.cpp:487-489)
+            f = self.M.export_flat(model.sys)
+            model.sys.solve()
+            pos = {int(v): i for i, v in enumerate(f.var_ids)}
+            model.vidx = {id(a): pos.get(int(a.var.h), -1) for a in model.actions if a.alive}
+        acts, da = self._full(model)
+        if not acts:
+            return -1.0
+        return da.next_occuring_event(with_latency=True)
+
+    def full_update(self, model, delta):
+        acts, da = self._full(model)
+        if not acts:
+            return []
+        da.update_actions_state(self.D.MODEL_CM02, delta, MAXMIN_PREC, SURF_PREC)
+        st = da.state()
+        for i, a in enumerate(acts):
+            a.remains, a.max_duration = float(st["remains"][i]), float(st["max_duration"][i])
+            a.latency = float(st["latency"][i])
+        return [(a, int(st["events"][i])) for i, a in enumerate(acts) if st["events"][i]]
+
+
+__all__ = ["run_pingpong", "expected", "PingOracle", "PingDevice", "RUNS", "HEAP_UNSET", "HEAP_NORMAL",
+           "NO_MAX_DURATION"]

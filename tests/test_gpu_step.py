@@ -109,3 +109,26 @@ def test_surf_usage_device_matches_reference_tesh(variant, name):
     from tests import surf_scenario as SC
 
     assert SC.run_surf_usage(SC.DeviceBackend(), variant) == SC.expected(name)
+
+
+@pytest.mark.parametrize("run", ["lv08_lazy", "lv08_full", "cm02_lazy"])
+def test_pingpong_device_matches_reference_tesh(run):
+    """examples/s4u/app-pingpong on the device: both communications built by lmm_communicate (the flow code of
+    the C4 platforms, lmm_platforms.hpp), solved by the HIP solver, stepped by the device glue — act_next_event
+    / act_update in Full mode, act_lazy_update / act_lazy_min / act_lazy_due in Lazy mode — print the tesh's
+    lines: LV08 Lazy and Full 0.019014 / 150.178356, CM02 0.001462 / 145.639041 (tests/pingpong_scenario.py)."""
+    from tests import pingpong_scenario as PP
+
+    out, _ = PP.run_pingpong(PP.PingDevice(), run)
+    assert out == PP.expected(run)
+
+
+def test_pingpong_device_dates_equal_oracle():
+    """The device replay's final clock equals the oracle replay's bit for bit in every configuration (the solve
+    of a one-flow system and the element-wise step glue are exact)."""
+    from tests import pingpong_scenario as PP
+
+    for run in PP.RUNS:
+        _, ed = PP.run_pingpong(PP.PingDevice(), run)
+        _, eo = PP.run_pingpong(PP.PingOracle(), run)
+        assert ed.now == eo.now, run
