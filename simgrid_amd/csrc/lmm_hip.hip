@@ -14,6 +14,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lmm/lmm_hip.h"
@@ -99,6 +100,13 @@ struct lmmhip_ctx {
   long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
   int persist_grid = 0;  // workgroups of the persistent launch (one per CU, checked at first use)
   int64_t persist_fallbacks = 0;  // persistent solves re-run by the multi-launch engine (barrier timeout)
+  // co-residency fallback (lmm_persist_kernels.hpp bar_rdv): mapped host word the closed-and-drained launch
+  // rendezvous raises, the streams left behind holding such a launch (its late workgroups still to run), and the
+  // solves left before the persistent engine is tried again on this context
+  int32_t* h_rdv = nullptr;
+  int32_t* d_rdv = nullptr;
+  std::vector<hipStream_t> retired_streams;
+  int64_t persist_cool = 0;
   bool ev1_done = false;  // the solve recorded ev1 itself (right behind its last kernel)
   // block-diagonal batch (lmmhip_set_batch): system offsets on the device, largest system
   int64_t bt_n = 0;
@@ -169,6 +177,30 @@ struct lmmhip_ctx {
       rs_outc;
 };
 
+// Persistent launches are serialised per device, process-wide (solve_maxmin_persist_once): the completion event
+// of each device's last persistent launch, and the number of live contexts on the device (the event is destroyed
+// with the last one, so a device reset between two sets of contexts never leaves a stale event behind).
+namespace {
+std::mutex g_persist_mu;
+std::map<int, hipEvent_t> g_persist_last;  // device -> completion event of its last persistent launch
+std::map<int, int> g_persist_users;        // device -> live contexts
+}  // namespace
+
+static void persist_ctx_ref(int device, int delta) {
+  std::lock_guard<std::mutex> lk(g_persist_mu);
+  int& n = g_persist_users[device];
+  n += delta;
+  if (n <= 0) {
+    g_persist_users.erase(device);
+    auto it = g_persist_last.find(device);
+    if (it != g_persist_last.end()) {
+      if (it->second)
+        (void)hipEventDestroy(it->second);
+      g_persist_last.erase(it);
+    }
+  }
+}
+
 static void free_owner(lmmhip_ctx* c) {
   for (void* p : c->fbo_allocs)
     (void)hipFree(p);
@@ -235,6 +267,10 @@ int lmmhip_ctx_create(int device, lmmhip_ctx** out) {
   if (e == hipSuccess)
     e = hipHostMalloc((void**)&c->h_ctl, 3 * CTL_WORDS * sizeof(int32_t), hipHostMallocDefault);
   if (e == hipSuccess)
+    e = hipHostMalloc((void**)&c->h_rdv, 64, hipHostMallocMapped);
+  if (e == hipSuccess)
+    e = hipHostGetDevicePointer((void**)&c->d_rdv, c->h_rdv, 0);
+  if (e == hipSuccess)
     e = hipEventCreateWithFlags(&c->ev_poll[0], hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipEventCreateWithFlags(&c->ev_poll[1], hipEventDisableTiming);
@@ -246,6 +282,7 @@ int lmmhip_ctx_create(int device, lmmhip_ctx** out) {
     delete c;
     return fail(LMMHIP_E_HIP, std::string("context creation: ") + hipGetErrorString(e));
   }
+  persist_ctx_ref(device, +1);
   *out = c;
   return 0;
 }
@@ -258,6 +295,13 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
   if (c->own_stream && c->own_stream != c->stream)
     (void)hipStreamSynchronize(c->own_stream);
+  for (hipStream_t st : c->retired_streams) {  // a persistent launch whose rendezvous closed: its late workgroups
+    (void)hipStreamSynchronize(st);           // still read the barrier words
+    (void)hipStreamDestroy(st);
+  }
+  if (c->h_rdv)
+    (void)hipHostFree(c->h_rdv);
+  persist_ctx_ref(c->device, -1);
   free_all(c);
   for (void* p : {(void*)c->res.e_cnst, (void*)c->res.e_w, (void*)c->res.e_fl, (void*)c->res.v_ebase,
                   (void*)c->res.v_n, (void*)c->res.v_pen, (void*)c->res.v_bound, (void*)c->res.c_bound,
@@ -1627,38 +1671,44 @@ static int engine_of(const lmmhip_ctx* c) {
 // Persistent launches are serialised per device, process-wide: a persistent grid needs every CU for one
 // workgroup at once (its barriers rely on co-residency), so two of them running side by side — two Systems
 // on two streams, or two threads — could each hold part of the chip and wait on the other.  Each persistent
-// launch waits (on its own stream, no host blocking) for the previous one's completion event.
-namespace {
-std::mutex g_persist_mu;
-std::map<int, hipEvent_t> g_persist_last;  // device -> completion event of its last persistent launch
-}  // namespace
+// launch waits (on its own stream, no host blocking) for the previous one's completion event
+// (g_persist_last, above).
 
-static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec);
+// A persistent solve that cannot run — its launch rendezvous closed because part of the grid could not become
+// resident within LMMHIP_PERSIST_RDV_MS (another kernel or process holding CUs: bar_rdv), or, later, a
+// grid-barrier wait timed out (CTL_ERR 1) — is not an error of the system: the solve is re-run by the
+// multi-launch engine, whose results are bit-identical (tests/test_gpu_engines.py).  The next
+// LMMHIP_PERSIST_COOLDOWN solves of the context then take the multi-launch engine directly (a
+// fallback that did not stick made every later solve under sustained contention pay the wait again).
+static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec, bool* closed);
 
-// A barrier wait that times out (CTL_ERR 1: the grid was not co-resident — a long kernel of another
-// process or library held CUs for seconds) is not an error of the system: the solve is re-run by the
-// multi-launch engine, whose results are bit-identical (tests/test_gpu_engines.py).
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
+  if (c->persist_cool > 0) {
+    c->persist_cool -= 1;
+    return solve_maxmin(c, prec);
+  }
   c->h_ctl[CTL_ERR] = 0;
-  const int rc = solve_maxmin_persist_once(c, prec);
-  if (rc != LMMHIP_E_HIP || c->h_ctl[CTL_ERR] != 1)
+  bool closed = false;
+  const int rc = solve_maxmin_persist_once(c, prec, &closed);
+  if (!closed && (rc != LMMHIP_E_HIP || c->h_ctl[CTL_ERR] != 1))
     return rc;
   c->persist_fallbacks += 1;
+  c->persist_cool = env_int("LMMHIP_PERSIST_COOLDOWN", 64);
   HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
   c->ev1_done = false;
   return solve_maxmin(c, prec);
 }
 
-static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec) {
+static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec, bool* closed) {
   Dev d = c->d;
   d.vstat = nullptr;
   const bool bits = int64_t(d.nC) <= int64_t(kPBitWords) * 64;
-  // registers per row in the re-vote: 8, or 10 for longer mean rows (C4's LV08 routes: 11.7 elements)
-  const bool r16 = c->group > 8;
-  const void* kern = bits ? (r16 ? reinterpret_cast<const void*>(&mm_persist<true, 10>)
-                                 : reinterpret_cast<const void*>(&mm_persist<true, 8>))
-                          : (r16 ? reinterpret_cast<const void*>(&mm_persist<false, 10>)
-                                 : reinterpret_cast<const void*>(&mm_persist<false, 8>));
+  // 8 row elements in registers in the re-vote, longer rows loop over the rest.  (A 10-register variant for
+  // long mean rows — C4's LV08 routes, 11.7 elements, when C4 still ran here — sat at the 128-VGPR budget of a
+  // 1024-thread workgroup and spilled once the launch rendezvous moved ahead of the init; C4 runs on the
+  // frontier engine since round 4, and AUTO keeps this engine for systems of at most 2^14 variables.)
+  const void* kern = bits ? reinterpret_cast<const void*>(&mm_persist<true, 8>)
+                          : reinterpret_cast<const void*>(&mm_persist<false, 8>);
   if (!c->pbar)
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->pbar), BAR_WORDS * sizeof(unsigned)));
   int per_cu = 0;
@@ -1667,8 +1717,6 @@ static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec) {
     return fail(LMMHIP_E_HIP, "persistent maxmin kernel: not one workgroup per CU (occupancy query)");
   const int grid = c->n_cu;
   c->persist_grid = grid;
-  HIPCHK(hipMemsetAsync(c->pbar, 0, BAR_WORDS * sizeof(unsigned), c->stream));
-  HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
   const int max_rounds = int(std::min<int64_t>(int64_t(d.nV) + 2, INT32_MAX - 1));
   const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 16);
   unsigned* barw = c->pbar;
@@ -1683,19 +1731,33 @@ static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec) {
     pt = c->ptime;
   }
   int sysf = env_int("LMMHIP_PERSIST_SYSFENCE", 0);
-  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf};
+  // launch rendezvous deadline (bar_rdv): the grid's workgroups are dispatched within microseconds when the CUs
+  // are free, so 20 ms of waiting means part of the chip is held by someone else
+  long long rdv_ticks = 100000LL * env_int("LMMHIP_PERSIST_RDV_MS", 20);  // 100 MHz wall clock
+  int32_t* hflag = c->d_rdv;
+  void* args[] = {&d, &barw, &prec, const_cast<int*>(&max_rounds), const_cast<int*>(&cmp_every), &pt, &pt_cap, &sysf,
+                  &rdv_ticks, &hflag};
   // A plain launch on the context's stream: the occupancy query above guarantees one workgroup per CU, so the
-  // n_cu workgroups are co-resident once the stream's earlier work has drained, and every barrier wait is
-  // bounded (CTL_ERR) should they not be.  hipLaunchCooperativeKernel (LMMHIP_PERSIST_COOP=1) runs the same
-  // kernel through the runtime's device-wide cooperative queue, whose teardown at process exit crashed inside
-  // the HSA runtime under rocprofv3 (SIGSEGV in libamdhip64's exit handler).
+  // n_cu workgroups are co-resident once the stream's earlier work has drained and nothing else holds CUs; the
+  // rendezvous deadline and the bounded barrier waits cover the case where something does.
+  // hipLaunchCooperativeKernel (LMMHIP_PERSIST_COOP=1) runs the same kernel through the runtime's device-wide
+  // cooperative queue, whose teardown at process exit crashed inside the HSA runtime under rocprofv3 (SIGSEGV
+  // in libamdhip64's exit handler).
   {
     std::lock_guard<std::mutex> lk(g_persist_mu);
     hipEvent_t& last = g_persist_last[c->device];
+    if (last && hipStreamWaitEvent(c->stream, last, 0) != hipSuccess) {  // (a stale event: make a new one)
+      (void)hipGetLastError();
+      (void)hipEventDestroy(last);
+      last = nullptr;
+    }
     if (!last)
       HIPCHK(hipEventCreateWithFlags(&last, hipEventDisableTiming));
-    else
-      HIPCHK(hipStreamWaitEvent(c->stream, last, 0));  // the previous persistent grid has drained
+    // the barrier words are reset behind the previous persistent launch (whose late workgroups, after a closed
+    // rendezvous, still read them)
+    HIPCHK(hipMemsetAsync(c->pbar, 0, BAR_WORDS * sizeof(unsigned), c->stream));
+    HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
+    __atomic_store_n(c->h_rdv, 0, __ATOMIC_RELEASE);
     if (env_int("LMMHIP_PERSIST_COOP", 0))
       HIPCHK(hipLaunchCooperativeKernel(kern, dim3(grid), dim3(kPB), args, 0, c->stream));
     else
@@ -1705,6 +1767,28 @@ static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec) {
   c->stats.kernel_launches[2] += 1;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->ev1_done = true;
+  // wait for the launch, or for its rendezvous to close (the mapped word), whichever comes first
+  for (;;) {
+    const hipError_t q = hipEventQuery(c->ev1);
+    if (q == hipSuccess)
+      break;
+    if (q != hipErrorNotReady)
+      HIPCHK(q);
+    if (__atomic_load_n(c->h_rdv, __ATOMIC_ACQUIRE)) {  // closed: no workgroup of it has written anything
+      // The launch is left behind with its late workgroups (they return at once when they get CUs).  A context
+      // on its own stream moves to a new one, so the fallback and everything after it run on the free CUs now;
+      // a caller-provided stream keeps its order (the fallback then waits for the late workgroups).
+      *closed = true;
+      if (c->stream == c->own_stream) {
+        hipStream_t ns = nullptr;
+        HIPCHK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+        c->retired_streams.push_back(c->own_stream);
+        c->own_stream = c->stream = ns;
+      }
+      return fail(LMMHIP_E_HIP, "persistent maxmin kernel: the launch rendezvous closed (grid not co-resident)");
+    }
+    std::this_thread::yield();
+  }
   if (int rc = poll_ctl(c))
     return rc;
   if (c->h_ctl[CTL_ERR] == 1)

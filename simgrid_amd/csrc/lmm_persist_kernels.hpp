@@ -71,25 +71,62 @@ struct PBar {
   int sysf;                 // 1: system-scope release / acquire (also writes back / invalidates the L2)
 };
 
-// Launch rendezvous: count the workgroups per XCC (for the hierarchical barrier) and wait for all.
-__device__ bool bar_init(PBar& b) {
-  __shared__ int ok_sh;
+// Launch rendezvous with a short deadline ("co-residency"), at kernel start, before any store:
+// a workgroup counts itself in BAR_FLAT with a compare-and-swap unless the rendezvous is closed, then waits until
+// every workgroup of the grid has arrived.  One that has waited `ticks` (wall clock) closes the rendezvous instead
+// — one compare-and-swap on the same word, so the count cannot complete behind it — and tells the host through
+// the mapped word *hflag; every arrived workgroup then leaves, and a late one (held back by another kernel or
+// process occupying CUs, possibly for seconds) finds it closed and returns at once.  None of them has written
+// anything, so the host re-runs the solve with the multi-launch engine right away, on the free CUs.
+constexpr unsigned kRdvClosed = 1u << 20;  // BAR_FLAT: closed flag above the arrival count
+
+// (out of line: inlined into mm_persist, whose round phases sit at the 128-VGPR budget, it tipped it over)
+__device__ __noinline__ int rdv_join(unsigned* w, unsigned xcc, unsigned grid, long long ticks, int32_t* hflag) {
+  unsigned v = ld_rlx(&w[BAR_FLAT]);
+  if (v & kRdvClosed)
+    return 0;
+  // the XCC count first (visible before the arrival: a workgroup that sees the full count reads it); a
+  // workgroup that then finds the rendezvous closed leaves a count nobody reads
+  __hip_atomic_fetch_add(&w[BAR_XSIZE + 16 * xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  for (;;) {
+    const unsigned prev = atomicCAS(&w[BAR_FLAT], v, v + 1);
+    if (prev == v)
+      break;
+    if (prev & kRdvClosed)
+      return 0;
+    v = prev;
+  }
+  const long long t0 = wall_clock64();
+  for (;;) {
+    v = ld_rlx(&w[BAR_FLAT]);
+    if (v & kRdvClosed)
+      return 0;
+    if (v == grid)
+      return 1;
+    if (wall_clock64() - t0 > ticks && atomicCAS(&w[BAR_FLAT], v, v | kRdvClosed) == v) {
+      if (hflag)
+        __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+__device__ bool bar_rdv(PBar& b, long long ticks, int32_t* hflag) {
+  __shared__ int ok_sh;
   if (threadIdx.x == 0) {
-    int ok = 1;
-    b.xcc = xcc_id();
-    __hip_atomic_fetch_add(&b.w[BAR_XSIZE + 16 * b.xcc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(&b.w[BAR_FLAT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ok = spin_geq(&b.w[BAR_FLAT], gridDim.x, b.err);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    b.xsize = ld_rlx(&b.w[BAR_XSIZE + 16 * b.xcc]);
-    b.nx = 0;
-    for (int i = 0; i < 8; i++)
-      b.nx += ld_rlx(&b.w[BAR_XSIZE + 16 * i]) != 0;
+    const int ok = rdv_join(b.w, xcc_id(), gridDim.x, ticks, hflag);
+    if (ok) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      b.xcc = xcc_id();
+      b.xsize = ld_rlx(&b.w[BAR_XSIZE + 16 * b.xcc]);
+      b.nx = 0;
+      for (int i = 0; i < 8; i++)
+        b.nx += ld_rlx(&b.w[BAR_XSIZE + 16 * i]) != 0;
+    }
     ok_sh = ok;
   }
   __syncthreads();
@@ -291,7 +328,8 @@ __device__ void p_compact(const Dev& s, int in, int out, int64_t nrows, unsigned
 
 template <bool kBits, int R>
 __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double prec, int max_rounds,
-                                                  int cmp_every, long long* pt, unsigned pt_cap, int sysf) {
+                                                  int cmp_every, long long* pt, unsigned pt_cap, int sysf,
+                                                  long long rdv_ticks, int32_t* hflag) {
   __shared__ PLds<kBits> L;
   PBar b{barw, &s.ctl[CTL_ERR], 0, 0, 0, pt, pt_cap, sysf};
   if (pt && blockIdx.x == 0 && threadIdx.x == 0)
@@ -300,12 +338,15 @@ __global__ void __launch_bounds__(kPB) mm_persist(Dev s, unsigned* barw, double 
   int32_t* palive = reinterpret_cast<int32_t*>(barw + BAR_PALIVE);
   const int lane = threadIdx.x & (kWave - 1);
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-  // init (maxmin.cpp:509-555) overlapped with the rendezvous
-  init_cnsts_waves(s, prec, pwave(), int64_t(gridDim.x) * kPW);
-  init_vars_range(s, int64_t(blockIdx.x) * kPB + threadIdx.x, int64_t(gridDim.x) * kPB);
-  if (!bar_init(b))
+  // the launch rendezvous before any store: a workgroup that finds it closed (late: the host has fallen back to
+  // the multi-launch engine, which is using the same buffers) or that closes it returns without having written
+  if (!bar_rdv(b, rdv_ticks, hflag))
     return;
   unsigned gen = 0;
+  init_cnsts_waves(s, prec, pwave(), int64_t(gridDim.x) * kPW);  // init (maxmin.cpp:509-555)
+  init_vars_range(s, int64_t(blockIdx.x) * kPB + threadIdx.x, int64_t(gridDim.x) * kPB);
+  if (!grid_sync(b, ++gen))
+    return;
   int buf = 0;
   int64_t nrows = s.nV;
   for (int r = 0;; r++) {

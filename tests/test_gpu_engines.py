@@ -241,3 +241,52 @@ def test_persistent_engine_concurrent_contexts_and_torch():
     s.solve()
     torch.cuda.synchronize()
     assert s.values_of(ids).tobytes() == ref.tobytes()
+
+
+def test_persistent_rendezvous_deadline_falls_back_fast():
+    """A persistent solve whose grid cannot become co-resident (half the CUs held for 2 s by a kernel on another
+    stream, tests/c/occupy.hip) closes its launch rendezvous after LMMHIP_PERSIST_RDV_MS (20 ms) and re-runs on
+    the round engine on the free CUs (lmm_persist_kernels.hpp bar_rdv, lmm_hip.hip solve_maxmin_persist): the
+    values are the round engine's bytes, one fallback is counted, the solve returns in well under the 2 s the
+    held CUs stay busy (< 0.5 s), and the next solve of the context takes the round engine directly (cooldown)
+    instead of waiting again."""
+    import ctypes as ct
+    import os
+    import time
+
+    import torch
+
+    occ = ct.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "libocc.so"))
+    build = _platform(5000, 2)
+    ref, _ = _values(build, L.System.ENGINE_ROUNDS)
+    s = L.System(False)
+    ids = build(s)
+    s.set_engine(L.System.ENGINE_PERSISTENT)
+    s.solve()
+    assert s.engine_fallbacks() == 0 and s.values_of(ids).tobytes() == ref.tobytes()
+    blocks = max(1, occ.occ_cus() // 2)
+    host, dev = ct.POINTER(ct.c_int)(), ct.POINTER(ct.c_int)()
+    assert occ.occ_alloc(blocks, ct.byref(host), ct.byref(dev)) == 0
+    side = torch.cuda.Stream()
+    try:
+        assert occ.occ_launch(ct.c_void_p(side.cuda_stream), blocks, ct.c_double(2.0), host, dev) == 0
+        t0 = time.time()
+        while sum(host[i] for i in range(blocks)) < blocks:  # every holding workgroup is running
+            assert time.time() - t0 < 30, "the holding kernel did not start"
+            time.sleep(0.0005)
+        t = time.perf_counter()
+        s.solve()
+        wall = time.perf_counter() - t
+        vals, fb = s.values_of(ids), s.engine_fallbacks()
+        t = time.perf_counter()
+        s.solve()  # cooldown: the round engine directly
+        wall2 = time.perf_counter() - t
+        vals2, fb2 = s.values_of(ids), s.engine_fallbacks()
+        still_held = sum(host[i] for i in range(blocks)) == blocks and time.time() - t0 < 1.9
+    finally:
+        torch.cuda.synchronize()  # the holding kernel ends, and with it the closed launch's late workgroups
+        occ.occ_free(host)
+    assert vals.tobytes() == ref.tobytes() and vals2.tobytes() == ref.tobytes()
+    assert fb == 1 and fb2 == 1, (fb, fb2)
+    assert wall < 0.5 and wall2 < 0.5, (wall, wall2)
+    assert still_held, "the solves finished only after the holding kernel: the check is void"
