@@ -192,7 +192,9 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
  *     rounds (also the engine of the profiling mode, which times every phase launch);
  *   LMMHIP_ENGINE_AUTO (default) — persistent up to 2^14 variables, frontier (below) up to 2^18, rounds
  *     above.
- * All give bit-identical results.  The environment variable LMMHIP_ENGINE=rounds|persistent overrides. */
+ * All give bit-identical results.  The environment variable LMMHIP_ENGINE=rounds|persistent|frontier overrides
+ * the context's engine ("auto" or any other value leaves it).  In profiling mode (lmmhip_set_profiling) every
+ * phase launch is timed, so a persistent choice runs the ROUNDS engine instead; FRONTIER is kept. */
 #define LMMHIP_ENGINE_PERSISTENT 0
 #define LMMHIP_ENGINE_ROUNDS 1
 #define LMMHIP_ENGINE_AUTO 2
@@ -201,9 +203,13 @@ int lmmhip_ctx_use_own_stream(lmmhip_ctx* ctx);
  *     a touched constraint may have invalidated (no pass over the alive rows; lmm_frontier_kernels.hpp). */
 #define LMMHIP_ENGINE_FRONTIER 3
 int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
-/* Persistent solves of this context that were re-run by the multi-launch engine because a grid-barrier wait
- * timed out (the persistent grid was not co-resident: another process or library held CUs for seconds).
- * Persistent launches of one process are serialised per device, so two Systems never starve each other. */
+/* Persistent solves of this context that were re-run by the multi-launch engine because the persistent grid
+ * could not become co-resident: its launch rendezvous closed after LMMHIP_PERSIST_RDV_MS (default 20 ms) with
+ * part of the grid held back (another kernel, library or process occupying CUs), or a later grid-barrier wait
+ * timed out.  After a closed rendezvous a context on its own stream moves to a new stream, so the re-run starts
+ * at once on the free CUs; the next LMMHIP_PERSIST_COOLDOWN (64) solves of the context use the multi-launch
+ * engine directly.  Persistent launches of one process are serialised per device, so two Systems never starve
+ * each other. */
 int lmmhip_engine_fallbacks(lmmhip_ctx* ctx, int64_t* n);
 /* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the
  * wall-clock time (100 MHz) of the last workgroup's arrival and of workgroup 0's exit.  With t != NULL,

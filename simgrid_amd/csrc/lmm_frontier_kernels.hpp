@@ -54,11 +54,25 @@ __global__ void __launch_bounds__(kBlock) fr_c2s(Dev s, int2* cs, int32_t* maxde
     const uint32_t b = s.cnst_ptr[c], e = s.cnst_ptr[c + 1];
     md = max(md, int(e - b));
     const bool dup = s.cdup[c] != 0;
+    // A constraint with a duplicate element: the k-th occurrence of a variable is found by counting the earlier
+    // ones.  When the column lists its variables in ascending order (the CSC built in CSR order: every upload
+    // path of a max-min system) equal ids are adjacent and only the run before j is scanned; otherwise every
+    // earlier element (O(degree^2) for the column, ADVICE r04: one duplicate on a core link made that seconds).
+    bool sorted_col = true;
+    if (dup) {
+      bool desc = false;
+      for (uint32_t j = b + 1 + lane; j < e; j += kWave)
+        desc |= s.csc_v[j - 1] > s.csc_v[j];
+      sorted_col = __ballot(desc) == 0;
+    }
     for (uint32_t j = b + lane; j < e; j += kWave) {
       const int32_t v = s.csc_v[j];
       const unsigned long long row = s.csc_row[j];
       int occ = 0;
-      if (dup)
+      if (dup && sorted_col)
+        for (uint32_t i = j; i > b && s.csc_v[i - 1] == v; i--)
+          occ++;
+      else if (dup)
         for (uint32_t i = b; i < j; i++)
           occ += s.csc_v[i] == v;
       for (uint32_t k = uint32_t(row); k < uint32_t(row >> 32); k++)

@@ -373,19 +373,21 @@ class DistExchange:
         import torch
 
         dev = self.device
-        lp = len(packs)
-        cnt = torch.tensor([int(c[0]) for _, _, c in packs], dtype=torch.int64).to(dev) if packs and \
-            not isinstance(packs[0][2], torch.Tensor) else \
-            torch.cat([c.to(dev, torch.int64).reshape(1) for _, _, c in packs])
+        lp = len(packs)  # the same on every rank (FbShardPlan: len(shards) parts per rank)
+        if lp == 0:
+            return
+        cnt = torch.cat([torch.as_tensor(c).to(dev, torch.int64).reshape(1) for _, _, c in packs])
         allc = torch.empty(self.world * lp, dtype=torch.int64, device=dev)
         self._gather(allc, cnt)
-        k = int(allc.max().item()) if allc.numel() else 0
+        allc = allc.cpu()  # the round's one host synchronisation: the padded length and this rank's counts
+        k = int(allc.max())
         if k == 0:
             return
+        mine = allc[self.rank * lp:(self.rank + 1) * lp].tolist()
         spos = torch.full((lp * k,), -1, dtype=torch.int32, device=dev)
         sval = torch.zeros(lp * k, dtype=torch.float64, device=dev)
-        for i, (pos, val, c) in enumerate(packs):
-            n = int(c[0])
+        for i, (pos, val, _) in enumerate(packs):
+            n = int(mine[i])
             if n:
                 spos[i * k:i * k + n] = torch.as_tensor(pos[:n]).to(dev, torch.int32)
                 sval[i * k:i * k + n] = torch.as_tensor(val[:n]).to(dev, torch.float64)
@@ -640,8 +642,11 @@ FB_DELTA = True  # multi-process FairBottleneck: ship only the listed variables'
 
 def _fb_rounds(shards, exchange, gather, poll_every):
     lp = len(shards)
-    # a multi-process exchange ships only the listed variables' mu after round 0 (all shards must pack)
+    # a multi-process exchange ships only the listed variables' mu after round 0 (all shards must pack); decided
+    # once for all ranks (a rank shipping pairs while another ships the full vector would mismatch collectives)
     delta = FB_DELTA and isinstance(exchange, DistExchange) and all(hasattr(sh, "pack_mu") for sh in shards)
+    if isinstance(exchange, DistExchange):
+        delta = bool(exchange.min(np.array([float(delta)]))[0] == 1.0)
     max_rounds = 64 * (gather.xmu.shape[0] + gather.xrem.shape[0]) + 4096
     rounds = 0
     while True:

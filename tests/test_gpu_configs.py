@@ -199,6 +199,32 @@ def test_c5_full_size_fixed_point_properties():
     assert (bad_x, infeasible, unstopped) == (0, 0, 0)
 
 
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_c5_full_size_vs_oracle_sample():
+    """C5 at FULL size (1e7 L07 flows on the dragonfly, seed 1) against the oracle's own FairBottleneck solve of
+    the same system, made once in the build container (tests/golden/make_c5_full_sample.py): the flattened
+    system hashes to the one the fixture was made from, and a fixed random sample of 1e5 flows is equal BYTE for
+    byte — the one-context solve runs the reference's floating-point operations in the reference's element
+    order (fair_bottleneck.cpp:23-153), so not a tolerance but the same bits."""
+    import os
+
+    from tests.golden.make_c5_full_sample import flat_sha256
+
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "c5_full_sample.npz"))
+    s = L.System(False, L.System.FAIR_BOTTLENECK)
+    _, vs = s.gen_platform_flows(L.platform_params(model=L.L07, n_flows=int(fx["n_flows"]), seed=1, **C5_PLATFORM))
+    f = M.export_flat(s)
+    assert flat_sha256(f) == str(fx["flat_sha256"]), "not the system the oracle solved"
+    del f
+    s.solve()
+    x = s.values_of(vs)
+    idx, y = fx["sample_idx"], fx["sample_x"]
+    assert x[idx].tobytes() == y.tobytes(), (int(np.count_nonzero(x[idx] != y)), s.last_stats()["rounds"],
+                                             int(fx["oracle_rounds"]))
+    assert bool(np.all(x > 0)) == bool(fx["all_positive"])
+
+
 def test_c5_fixed_point_properties_hold_on_the_oracle_solution():
     """The property check itself, validated where the oracle runs: the oracle's values pass it."""
     p = dict(model=L.L07, n_flows=20_000, seed=3, **C5_PLATFORM)

@@ -290,3 +290,34 @@ def test_persistent_rendezvous_deadline_falls_back_fast():
     assert fb == 1 and fb2 == 1, (fb, fb2)
     assert wall < 0.5 and wall2 < 0.5, (wall, wall2)
     assert still_held, "the solves finished only after the holding kernel: the check is void"
+
+
+def test_frontier_duplicate_elements_on_a_high_degree_constraint():
+    """A constraint holding two elements of each of its 40,000 variables (cdup, as a route crossing a link twice
+    or a flow's cross-traffic element on its own link): the frontier engine's CSR -> CSC map (fr_c2s) counts a
+    variable's earlier occurrences over the run of equal ids only, so the first solve stays fast (ADVICE r04:
+    the full rescan was O(degree^2) in one wave), and the values equal the round engine's bit for bit."""
+    import time
+
+    def build(s):
+        big = s.constraint_new(None, 1e6)
+        vs = []
+        for i in range(40_000):
+            c = s.constraint_new(None, 1.0 + (i % 97))
+            v = s.variable_new(None, 1.0 + (i % 3), -1.0, 3)
+            s.expand(big, v, 1.0)
+            s.expand(c, v, 1.0)
+            s.expand(big, v, 0.05 * (1 + i % 5))
+            vs.append(v.h)
+        return np.array(vs, dtype=np.int64)
+
+    s = L.System(False)
+    ids = build(s)
+    s.set_engine(L.System.ENGINE_FRONTIER)
+    t = time.perf_counter()
+    s.solve()
+    first = time.perf_counter() - t
+    xf = s.values_of(ids)
+    xr, _ = _values(build, L.System.ENGINE_ROUNDS)
+    assert xf.tobytes() == xr.tobytes(), float(np.max(np.abs(xf - xr)))
+    assert first < 2.0, first
