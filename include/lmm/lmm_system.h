@@ -170,7 +170,8 @@ int64_t lmm_gen_platform_flows(lmm_sys* s, const lmm_platform_params* p, int64_t
  * flows above use (lmm_platforms.hpp: link_constraint, communicate).
  * lmm_link_new replaces NetworkCm02Link's constraint (network_cm02.cpp:282-295): bound = bandwidth factor
  * (model 0 CM02: 1, 1 LV08: 0.97) * bw, FATPIPE unshared; returns the constraint id or -1.
- * lmm_communicate replaces the LMM part of NetworkCm02Model::communicate (network_cm02.cpp:165-274): the route
+ * lmm_communicate replaces the LMM part of NetworkCm02Model::communicate (network_cm02.cpp:165-274), the
+ * variable carrying the opaque `id` (the reference passes the action, network_cm02.cpp:221-229): the route
  * (constraints, link bandwidths and latencies, in route order) at weight 1.0 and the back route (crosstraffic)
  * at 0.05; penalty 0 while the latency is unpaid (paid = 0) or the sharing penalty (paid = 1; 1.0 without
  * latency); bound from rate (< 0: none) and TCP-gamma.  Returns the variable id or -1; *out gets the action's
@@ -179,7 +180,7 @@ typedef struct lmm_comm_info {
   double latency, lat_current, sharing_penalty, bound;
 } lmm_comm_info;
 int64_t lmm_link_new(lmm_sys* s, int model, double bw, int fatpipe);
-int64_t lmm_communicate(lmm_sys* s, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
+int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
                         const double* route_lat, int64_t n_back, const int64_t* back_cnst, double rate,
                         double tcp_gamma, int paid, lmm_comm_info* out);
 

@@ -39,10 +39,11 @@ struct Builder {
   using Cnst = Id;
   using Var = Id;
   System* s;
+  void* var_id = nullptr;  // the opaque id (Action*) of the variables it creates
   Cnst constraint_new(double b) { return s->constraint_new(nullptr, b); }
   void set_concurrency_limit(Cnst c, int l) { s->set_concurrency_limit(c, l); }
   void unshare(Cnst c) { s->unshare(c); }
-  Var variable_new(double p, double b, int n) { return s->variable_new(nullptr, p, b, size_t(n)); }
+  Var variable_new(double p, double b, int n) { return s->variable_new(var_id, p, b, size_t(n)); }
   void set_concurrency_share(Var v, int sh) { s->set_concurrency_share(v, sh); }
   void expand(Cnst c, Var v, double w) { s->expand(c, v, w); }
   void expand_add(Cnst c, Var v, double w) { s->expand_add(c, v, w); }
@@ -493,14 +494,14 @@ int64_t lmm_link_new(lmm_sys* s, int model, double bw, int fatpipe) {
   }
 }
 
-int64_t lmm_communicate(lmm_sys* s, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
+int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
                         const double* route_lat, int64_t n_back, const int64_t* back_cnst, double rate,
                         double tcp_gamma, int paid, lmm_comm_info* out) {
   try {
     if (!s || n_route < 0 || n_back < 0 || (n_route && (!route_cnst || !route_bw || !route_lat)) ||
         (n_back && !back_cnst))
       throw std::invalid_argument("lmm_communicate: bad arguments");
-    Builder b{&s->sys};
+    Builder b{&s->sys, id};
     std::vector<lmm_plat::Link> links;
     std::vector<Id> cn;
     std::vector<int> route, back;

@@ -118,7 +118,7 @@ SIGNATURES = {
     "lmm_platform_size": (I, [ct.POINTER(PlatformParams), PI64, PI64]),
     "lmm_gen_platform_flows": (I64, [P, ct.POINTER(PlatformParams), PI64, PI64]),
     "lmm_link_new": (I64, [P, I, D, I]),
-    "lmm_communicate": (I64, [P, I, I64, PI64, PD, PD, I64, PI64, D, D, I, P]),
+    "lmm_communicate": (I64, [P, P, I, I64, PI64, PD, PD, I64, PI64, D, D, I, P]),
     "lmm_device_count": (I, []),
     "lmm_last_error": (ct.c_char_p, []),
     # include/lmm/lmm_hip.h
@@ -663,17 +663,18 @@ class System:
             raise LmmError(lib().lmm_last_error().decode())
         return Constraint(self, h)
 
-    def communicate(self, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False):
+    def communicate(self, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False, id_=None):
         """NetworkCm02Model::communicate's LMM part (lmm_communicate): route = [(Constraint, bw, lat)] in route
-        order, back = the back route's Constraints (crosstraffic).  Returns (Variable, dict(latency, lat_current,
-        sharing_penalty, bound))."""
+        order, back = the back route's Constraints (crosstraffic), id_ = the variable's opaque id (an int: the
+        action; modified_action_ids() reports it).  Returns (Variable, dict(latency, lat_current, sharing_penalty,
+        bound))."""
         n = len(route)
         rc = np.array([c.h for c, _, _ in route], dtype=np.int64)
         rb = np.array([b for _, b, _ in route], dtype=np.float64)
         rl = np.array([l for _, _, l in route], dtype=np.float64)
         bc = np.array([c.h for c in back], dtype=np.int64)
         info = CommInfo()
-        h = lib().lmm_communicate(self.h, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
+        h = lib().lmm_communicate(self.h, id_, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
                                   rl.ctypes.data_as(PD), len(bc), bc.ctypes.data_as(PI64), rate, tcp_gamma,
                                   int(paid), ct.byref(info))
         if h < 0:

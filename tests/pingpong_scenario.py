@@ -194,8 +194,7 @@ class PingDevice(DeviceBackend):
         return sys.link_new(model, bw)
 
     def communicate(self, sys, model, route, back, rate, tcp_gamma, aid):
-        v, info = sys.communicate(model, route, back, rate, tcp_gamma)
-        return v, info
+        return sys.communicate(model, route, back, rate, tcp_gamma, id_=aid)  # the action is the variable's id
 
     def _full(self, model):
         import numpy as np
