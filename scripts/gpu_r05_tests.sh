@@ -3,7 +3,7 @@
 # every -m gpu test.  Each step under its own limit; stops at the first failure.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_step.py -k pingpong tests/test_gpu_engines.py -x -v \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_step.py tests/test_gpu_engines.py -k "pingpong or rendezvous or tail_handoff or duplicate" -x -v \
   -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r05_new_tests.log 2>&1; rc=$?
 tail -n 30 gpurun_out/r05_new_tests.log
 if [ $rc -ne 0 ]; then echo "STOP new tests rc=$rc"; exit $rc; fi

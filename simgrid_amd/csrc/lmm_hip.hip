@@ -27,6 +27,7 @@
 #include "lmm_batch_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
 #include "lmm_cc_kernels.hpp"
+#include "lmm_tail_kernels.hpp"
 #include "lmm_scan.hpp"
 
 using namespace lmmdev;
@@ -34,6 +35,7 @@ using namespace lmmdev;
 constexpr unsigned kPersistProfCap = 1 << 16;  // barriers covered by lmmhip_persist_profile
 constexpr int64_t kAutoPersistVars = 1 << 18;   // LMMHIP_ENGINE_AUTO: one of the single-GPU small-system engines up to
 constexpr int64_t kAutoPersistMaxVars = 1 << 14;  // this many variables: persistent up to 2^14, frontier above
+constexpr int64_t kTailRows = 0;  // LMMHIP_TAIL_ROWS default: alive rows at which a solve's tail is handed off
 
 namespace {
 
@@ -168,6 +170,13 @@ struct lmmhip_ctx {
   // re-vote queue; the map and the largest CSC degree are rebuilt after every structural change
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
   Scr mm_rowof;  // solve_maxmin: alive row of each variable (saturation retires fixed variables' rows)
+  // tail hand-off (lmm_tail_kernels.hpp, LMMHIP_TAIL_ROWS): the child context the remaining system moves to,
+  // its scratch (flags, scans, sort pairs, the parent id of each child variable), this context's role
+  lmmhip_ctx* tail = nullptr;
+  bool cont = false;          // this context continues a handed-off solve: init from the copied state
+  int64_t tail_handoffs = 0;  // solves whose tail was handed off
+  int64_t tail_round = -1;    // the parent round of the last hand-off
+  Scr tl_cf, tl_cmap, tl_rl, tl_rlo, tl_rf, tl_rvo, tl_sk0, tl_sk1, tl_sv0, tl_sv1, tl_tmp, tl_vmap, tl_cnt;
   Scr mm_crec[3];  // solve_maxmin: packed row records (LMMHIP_CREC)
   Scr mm_rdq[2], mm_rqst, mm_useg, mm_ucnt;  // solve_maxmin: ready queue / update segments (LMMHIP_RDQ)
   bool fr_map_ok = false;
@@ -295,6 +304,10 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
   if (c->own_stream && c->own_stream != c->stream)
     (void)hipStreamSynchronize(c->own_stream);
+  if (c->tail) {  // (runs on this context's stream: destroyed first)
+    lmmhip_ctx_destroy(c->tail);
+    c->tail = nullptr;
+  }
   for (hipStream_t st : c->retired_streams) {  // a persistent launch whose rendezvous closed: its late workgroups
     (void)hipStreamSynchronize(st);           // still read the barrier words
     (void)hipStreamDestroy(st);
@@ -308,7 +321,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->tl_cf, &c->tl_cmap, &c->tl_rl, &c->tl_rlo, &c->tl_rf, &c->tl_rvo, &c->tl_sk0, &c->tl_sk1, &c->tl_sv0, &c->tl_sv1, &c->tl_tmp, &c->tl_vmap, &c->tl_cnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc})
@@ -1170,6 +1183,7 @@ int lmmhip_set_profiling(lmmhip_ctx* c, int on) {
 }
 
 static int solve_maxmin(lmmhip_ctx* c, double prec);
+static int solve_tail(lmmhip_ctx* c, double prec, int64_t nh);
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec);
 static int solve_maxmin_frontier(lmmhip_ctx* c, double prec);
 static int solve_fair(lmmhip_ctx* c, double prec);
@@ -1379,7 +1393,10 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   }
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   const int gC = grid_for(d.nC, kBlock);
-  LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
+  if (c->cont)  // a handed-off tail (lmm_tail_kernels.hpp): the constraint state came with the system
+    LAUNCH(0, -1, mm_init_cont, grid_for(d.nC, kBlock), kBlock, d);
+  else
+    LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, mm_init_vars, grid_for(d.nV, kBlock), kBlock, d);
   LAUNCH(1, -1, mm_clist, std::min(gC, 2 * c->n_cu), kBlock, d, 1);
   HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
@@ -1437,6 +1454,10 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C2 25.96-25.99 ms at 16, 26.01 at 8,
   // 26.15-26.20 at 4
   const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 16));
+  // tail hand-off (lmm_tail_kernels.hpp; LMMHIP_TAIL_ROWS, 0 = off): not from a continued solve itself, not in
+  // the profiling mode (it times this engine's launches), not with the target-ordered rows
+  const int64_t tail_rows = env_int("LMMHIP_TAIL_ROWS", kTailRows);
+  const bool tail_ok = tail_rows > 0 && !c->cont && !c->profiling && !tgt;
   bool pending = false;
   int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
   int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
@@ -1517,6 +1538,9 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         break;
       ncl = h[CTL_NCL0 + h[CTL_CB]];
       nrows = h[CTL_NROWS + h[CTL_BUF]];
+      // few rows left: the rest of the solve on the compacted remaining system (after the queued chunk)
+      if (tail_ok && nrows <= tail_rows && r >= 2)
+        return solve_tail(c, prec, nrows);
     }
     pending = true;
     slot ^= 1;
@@ -1526,6 +1550,96 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       chunk = std::min(2 * chunk, chunk_max);
   }
   return poll_ctl(c);  // (the queued tail has run: final words for the stats)
+}
+
+// Tail hand-off (lmm_tail_kernels.hpp): the rest of a max-min solve on the compacted remaining system, in a child
+// context on this context's stream.  nh: the host's bound of the rows in the alive-row buffer in use.  The kernels
+// queue behind the rounds already queued; one host round trip reads the child's sizes (and whether the solve
+// ended in the meantime).
+static int solve_tail(lmmhip_ctx* c, double prec, int64_t nh) {
+  Dev& d = c->d;
+  int64_t *cf = nullptr, *cmap = nullptr, *rl = nullptr, *rlo = nullptr, *rf = nullptr, *rvo = nullptr,
+          *cnt = nullptr;
+  int rc = scratch(c, c->tl_cf, int64_t(d.nC) + 1, &cf);
+  rc = rc ? rc : scratch(c, c->tl_cmap, int64_t(d.nC) + 1, &cmap);
+  rc = rc ? rc : scratch(c, c->tl_rl, nh + 1, &rl);
+  rc = rc ? rc : scratch(c, c->tl_rlo, nh + 1, &rlo);
+  rc = rc ? rc : scratch(c, c->tl_rf, nh + 1, &rf);
+  rc = rc ? rc : scratch(c, c->tl_rvo, nh + 1, &rvo);
+  rc = rc ? rc : scratch(c, c->tl_cnt, 4, &cnt);
+  if (rc)
+    return rc;
+  LAUNCH(6, -1, tl_cflag, grid_for(int64_t(d.nC) + 1, kBlock), kBlock, d, cf);
+  if (int rc2 = dev_scan(c, cf, cmap, int64_t(d.nC) + 1))
+    return rc2;
+  LAUNCH(6, -1, tl_rowlen, grid_for(nh + 1, kBlock), kBlock, d, nh, cf, rl, rf);
+  if (int rc2 = dev_scan(c, rl, rlo, nh + 1) | dev_scan(c, rf, rvo, nh + 1))
+    return rc2;
+  HIPCHK(hipMemcpyAsync(cnt, cmap + d.nC, sizeof(int64_t), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(cnt + 1, rlo + nh, sizeof(int64_t), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(cnt + 2, rvo + nh, sizeof(int64_t), hipMemcpyDeviceToDevice, c->stream));
+  int64_t n3[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(n3, cnt, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  if (int rc2 = poll_ctl(c))  // (synchronises: the words and the sizes)
+    return rc2;
+  if (c->h_ctl[CTL_DONE])  // the queued rounds finished the solve
+    return 0;
+  const int64_t nC2 = n3[0], nnz2 = n3[1], nV2 = n3[2];
+  const int32_t r0 = c->h_ctl[CTL_ROUNDS];  // rounds run here: the child's round 0 is this solve's round r0
+  const int32_t lastr = c->h_ctl[CTL_LASTR];
+  c->tail_handoffs += 1;
+  c->tail_round = r0;
+  if (nV2 == 0 || nC2 == 0) {  // nothing left to fix: every remaining variable drops at 0 (its value already)
+    c->h_ctl[CTL_DONE] = 1;
+    return 0;
+  }
+  if (!c->tail)
+    if (int rc2 = lmmhip_ctx_create(c->device, &c->tail))
+      return rc2;
+  lmmhip_ctx* t = c->tail;
+  t->stream = c->stream;
+  // the engine the remaining system's size calls for (AUTO; LMMHIP_TAIL_ENGINE: measurement / tests)
+  t->engine = env_int("LMMHIP_TAIL_ENGINE", LMMHIP_ENGINE_AUTO);
+  t->profiling = false;
+  FlatBufs fb;
+  if (int rc2 = alloc_flat(t, nV2, nC2, nnz2, 0, &fb))
+    return rc2;
+  uint32_t *sk0 = nullptr, *sk1 = nullptr;
+  unsigned long long *sv0 = nullptr, *sv1 = nullptr;
+  int32_t* vmap = nullptr;
+  rc = scratch(c, c->tl_sk0, nnz2, &sk0);
+  rc = rc ? rc : scratch(c, c->tl_sk1, nnz2, &sk1);
+  rc = rc ? rc : scratch(c, c->tl_sv0, nnz2, &sv0);
+  rc = rc ? rc : scratch(c, c->tl_sv1, nnz2, &sv1);
+  rc = rc ? rc : scratch(c, c->tl_vmap, nV2, &vmap);
+  if (rc)
+    return rc;
+  const Dev& td = t->d;
+  LAUNCH(6, -1, tl_rows, grid_for(nh, kBlock), kBlock, d, td, nh, cmap, cf, rlo, rvo, fb.vp, fb.csr_c, fb.csr_w,
+         fb.pen, fb.vb, fb.cvar0, vmap, sk0, sv0);
+  const int bits = nC2 > 1 ? 64 - __builtin_clzll(uint64_t(nC2 - 1)) : 1;
+  size_t tb = 0;
+  HIPCHK(sort_pairs_u32_u64(nullptr, tb, sk0, sk1, sv0, sv1, nnz2, bits, c->stream));
+  uint8_t* tmp = nullptr;
+  if (int rc2 = scratch(c, c->tl_tmp, int64_t(tb), &tmp))
+    return rc2;
+  HIPCHK(sort_pairs_u32_u64(tmp, tb, sk0, sk1, sv0, sv1, nnz2, bits, c->stream));
+  LAUNCH(6, -1, tl_csc, grid_for(std::max<int64_t>(nnz2, 1), kBlock), kBlock, nnz2, nC2, sk1, sv1, fb.csr_w,
+         fb.csc_v, fb.csc_w, fb.cp);
+  LAUNCH(6, -1, tl_cnsts, grid_for(d.nC, kBlock), kBlock, d, td, cmap, cf, fb.cb, fb.cf);
+  if (int rc2 = finish_flat(t, nV2, nC2, nnz2))  // per-element usage, CSR rows, duplicates, launch shape
+    return rc2;
+  t->cont = true;
+  const int rct = lmmhip_solve(t, LMMHIP_KIND_MAXMIN, prec);
+  t->cont = false;
+  if (rct)
+    return rct;
+  LAUNCH(6, -1, tl_scatter, grid_for(nV2, kBlock), kBlock, d, t->d, vmap, r0);
+  const int32_t tr = t->h_ctl[CTL_ROUNDS];
+  c->h_ctl[CTL_ROUNDS] = r0 + tr;
+  c->h_ctl[CTL_LASTR] = tr > 0 ? r0 + t->h_ctl[CTL_LASTR] : lastr;
+  c->h_ctl[CTL_DONE] = 1;
+  return 0;
 }
 
 // Frontier engine (lmm_frontier_kernels.hpp): three launches per round, work proportional to the touched
@@ -1576,7 +1690,10 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
-  LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
+  if (c->cont)  // a handed-off tail: the constraint state came with the system (32-bit keys from the ratios)
+    LAUNCH(0, -1, mm_init_cont, grid_for(d.nC, kBlock), kBlock, d);
+  else
+    LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
   if (d.nnz > 0)
     HIPCHK(hipMemsetAsync(d.vslot, 0xFF, sizeof(uint32_t) * size_t(d.nnz), c->stream));  // kNoVoter
@@ -1652,6 +1769,8 @@ static int engine_of(const lmmhip_ctx* c) {
   // the profiling mode times every phase launch: a multi-launch engine
   if (c->profiling)
     return eng == LMMHIP_ENGINE_FRONTIER ? LMMHIP_ENGINE_FRONTIER : LMMHIP_ENGINE_ROUNDS;
+  if (c->cont && eng == LMMHIP_ENGINE_PERSISTENT)
+    return LMMHIP_ENGINE_FRONTIER;
   if (eng != LMMHIP_ENGINE_AUTO)
     return eng;
   // AUTO (measured): one launch per solve where the host round-trips and launches of the
@@ -1660,7 +1779,7 @@ static int engine_of(const lmmhip_ctx* c) {
   // grids keep 32 waves per CU in flight instead of 16
   // round 4: the frontier engine between the two (C4, 1e5 LV08 flows: 3.54 ms against 4.34 persistent and
   // 4.48 rounds), the round engine above (C2: 25.8 against 28.2 frontier)
-  if (int64_t(c->d.nV) <= kAutoPersistMaxVars)
+  if (int64_t(c->d.nV) <= kAutoPersistMaxVars && !c->cont)  // (a handed-off tail: its init is a launch of its own)
     return LMMHIP_ENGINE_PERSISTENT;
   return int64_t(c->d.nV) <= kAutoPersistVars ? LMMHIP_ENGINE_FRONTIER : LMMHIP_ENGINE_ROUNDS;
 }
@@ -2172,6 +2291,16 @@ int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_
     t[i] = h[i];
   *nbar = kPBlkCap;
   *nblk = c->persist_grid;
+  return 0;
+}
+
+int lmmhip_tail_handoffs(lmmhip_ctx* c, int64_t* n, int64_t* round) {
+  if (!c)
+    return fail(LMMHIP_E_ARG, "null context");
+  if (n)
+    *n = c->tail_handoffs;
+  if (round)
+    *round = c->tail_round;
   return 0;
 }
 

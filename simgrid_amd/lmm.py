@@ -153,6 +153,7 @@ SIGNATURES = {
     "lmmhip_ctx_use_own_stream": (I, [P]),
     "lmmhip_ctx_set_engine": (I, [P, I]),
     "lmmhip_engine_fallbacks": (I, [P, PI64]),
+    "lmmhip_tail_handoffs": (I, [P, PI64, PI64]),
     "lmmhip_persist_profile": (I, [P, I, PI64, I64, PI64]),
     "lmmhip_persist_profile_blocks": (I, [P, PI64, I64, PI64, PI64]),
     "lmmhip_fb_shard_owner": (I, [P, I64, ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD,
@@ -497,6 +498,12 @@ class System:
         launch per solve), ENGINE_ROUNDS (one launch per phase per round), ENGINE_FRONTIER (one launch per
         phase per round, work proportional to what changed) or ENGINE_AUTO (default)."""
         _check_hip(lib().lmmhip_ctx_set_engine(self.device_ctx(), int(engine)))
+
+    def tail_handoffs(self):
+        """(solves whose tail was handed off to a compacted child system, round of the last hand-off)."""
+        n, r = I64(), I64()
+        _check_hip(lib().lmmhip_tail_handoffs(self.device_ctx(), ct.byref(n), ct.byref(r)))
+        return n.value, r.value
 
     def engine_fallbacks(self):
         """Persistent solves of this system's context re-run by the multi-launch engine after a grid-barrier

@@ -1,5 +1,6 @@
-// TEST SUPPORT ONLY (tests/test_gpu_engines.py::test_persistent_rendezvous_deadline): a kernel that holds part
-// of the chip for a given wall-clock time, so that a persistent solve queued on another stream right after it
+// TEST SUPPORT ONLY (tests/test_gpu_engines.py::test_persistent_rendezvous_deadline_falls_back_fast): a kernel
+// that holds part of the chip for a given wall-clock time, launched by another process (tests/c/occupy_run.py:
+// its hardware queue is its own, so the hold overlaps the test's persistent solve), so that the solve's grid
 // cannot become co-resident.  Built into tests/c/libocc.so by __graft_entry__.build().
 #include <hip/hip_runtime.h>
 
@@ -36,6 +37,7 @@ int occ_launch(void* stream, int blocks, double seconds, int* host, int* dev) {
   hipLaunchKernelGGL(occ_spin, dim3(blocks), dim3(1024), 0, static_cast<hipStream_t>(stream), ticks, dev);
   return int(hipGetLastError());
 }
+int occ_sync(void) { return int(hipDeviceSynchronize()); }
 int occ_cus(void) {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev))
