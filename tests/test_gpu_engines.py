@@ -269,12 +269,14 @@ def test_persistent_rendezvous_deadline_falls_back_fast():
         assert line.startswith("RUNNING"), line
         t0 = time.time()
         t = time.perf_counter()
-        s.solve()
+        s.device_solve()  # (the system is unchanged: System::solve would not run the solver again)
         wall = time.perf_counter() - t
+        s.fetch()
         vals, fb = s.values_of(ids), s.engine_fallbacks()
         t = time.perf_counter()
-        s.solve()  # cooldown: the round engine directly
+        s.device_solve()  # cooldown: the round engine directly
         wall2 = time.perf_counter() - t
+        s.fetch()
         vals2, fb2 = s.values_of(ids), s.engine_fallbacks()
         held = time.time() - t0 < 1.5 and p.poll() is None
         assert p.wait(timeout=60) == 0
@@ -339,7 +341,8 @@ def test_tail_handoff_bit_identical(name, tail, child, monkeypatch):
     nv = s.last_stats()["n_var"]
     monkeypatch.setenv("LMMHIP_TAIL_ROWS", str(nv if tail == "early" else max(1, nv // 2)))
     monkeypatch.setenv("LMMHIP_TAIL_ENGINE", child)
-    s.solve()
+    s.device_solve()
+    s.fetch()
     xt, rt = s.values_of(ids), s.last_stats()["rounds"]
     n, at = s.tail_handoffs()
     if tail == "early":
