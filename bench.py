@@ -49,6 +49,38 @@ def solve_traffic(workload):
     return int(t["solve_counter_bytes_fetch_x2"]), int(t["solve_counter_bytes_raw"]), os.path.relpath(p, ROOT)
 
 
+def request_roofline(workload, ms):
+    """The request-rate roofline: memory-side requests per solve (rocprofv3 TCC_EA0_RDREQ_sum +
+    TCC_EA0_WRREQ_sum over the solve's kernels, scripts/profile.sh PARTS=req, scripts/parse_rocprof.py) over the
+    solve's time, against the best rate the calibration kernels (scripts/ubench_gather.hip: random 8-B gathers,
+    random fp64 atomics, random byte stores on 8-80 MB tables) reached under the same counters on this chip."""
+    for k in (9, 8, 7, 6, 5):
+        p = os.path.join(ROOT, "profiles", f"r0{k}_requests_{workload}.json")
+        if os.path.exists(p):
+            break
+    else:
+        return None
+    with open(p) as f:
+        t = json.load(f)
+    per = float(t["solve_requests"])
+    ach = per / (ms * 1e-3)
+    rates = {k: float(v["requests_per_s"]) for k, v in (t.get("calibration") or {}).items()
+             if v.get("requests_per_s")}
+    best = max(rates, key=rates.get) if rates else None
+    top = sorted(((k, e) for k, e in t["kernels"].items() if e.get("requests_per_s")),
+                 key=lambda kv: -(kv[1]["TCC_EA0_RDREQ_sum"] + kv[1]["TCC_EA0_WRREQ_sum"]))[:4]
+    return {"unit": "requests/s", "per_solve": round(per), "rdreq_per_solve": round(float(t["solve_rdreq"])),
+            "wrreq_per_solve": round(float(t["solve_wrreq"])), "atomic_per_solve": round(float(t["solve_atomic"])),
+            "achieved": round(ach, 1), "ceiling": round(rates[best], 1) if best else None, "ceiling_kernel": best,
+            "frac": round(ach / rates[best], 4) if best else None,
+            "calibration_rates": {k: round(v, 1) for k, v in rates.items()},
+            "per_kernel": {k: {"requests_per_launch": round(e["TCC_EA0_RDREQ_sum_per_launch"] +
+                                                            e["TCC_EA0_WRREQ_sum_per_launch"]),
+                               "requests_per_s": round(e["requests_per_s"], 1), "avg_us": round(e["avg_ns"] / 1e3, 2)}
+                           for k, e in top},
+            "source": os.path.relpath(p, ROOT)}
+
+
 def roofline_obj(alg_bytes, ms, workload, note, gpus=1):
     """Solve-level roofline: the algorithmic bytes of one solve (all `gpus` ranks' parts)
     over the solve's time, against `gpus` x the HBM peak.  The PMC traffic summaries are single-GPU runs:
@@ -225,6 +257,8 @@ def main():
     solve_alg = 56 * nnz + 24 * nV + 32 * nC
     roofline = roofline_obj(solve_alg * world, ms_per_step, "c2" if args.variant == "plain" else "c2_stress",
                             "SURVEY.md §8(d) lmm_solve: 56 nnz + 24 V + 32 C bytes per solve (x ranks)", gpus=world)
+    if world == 1 and args.variant == "plain":
+        roofline["requests"] = request_roofline("c2", ms_per_step)
     # secondary: the dominant kernel's own per-launch byte model (kernel_bytes) over its HIP-event time
     roofline["dominant_kernel"] = {"name": dom, "avg_us": round(d["avg_us"], 2), "launches": d["launches"],
                                    "alg_bytes_per_launch": int(d["alg_bytes"] / max(1, d["launches"])),

@@ -78,6 +78,89 @@ def workload_traffic(w):
                 kernels=kernels)
 
 
+REQ_CTRS = ("TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_ATOMIC_sum")
+
+
+def load_count(path):
+    """Per kernel (full name): [summed counter value, dispatches] of a one-counter rocprofv3 pass (a count, no
+    unit scaling)."""
+    d = collections.defaultdict(lambda: [0.0, 0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d[r["Kernel_Name"]][0] += float(r["Counter_Value"])
+            d[r["Kernel_Name"]][1] += 1
+    return d
+
+
+def trace_avg_ns(path):
+    """short kernel name -> (average duration ns, calls) from a --kernel-trace --stats summary."""
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            out[short(r["Name"])] = (float(r["AverageNs"]), int(r["Calls"]))
+    return out
+
+
+def workload_requests(w, tag):
+    """Memory-side requests (L2 -> fabric: TCC_EA0_RDREQ / WRREQ, and the atomic part of WRREQ) per kernel launch
+    and per solve of workload w, with the kernels' average durations from the same tag's kernel trace."""
+    paths = {c: os.path.join(OUT, f"rp_{c}_{w}", "run_counter_collection.csv") for c in REQ_CTRS}
+    if not all(os.path.exists(p) for p in paths.values()):
+        return None
+    ctr = {c: load_count(p) for c, p in paths.items()}
+    kernels = {}
+    for c, d in ctr.items():
+        for name, (v, n) in d.items():
+            e = kernels.setdefault(short(name), {"launches": 0})
+            e[c] = e.get(c, 0.0) + v
+            e["launches"] = max(e["launches"], n)
+    solves = kernels.get(SOLVE_MARK[w], {}).get("launches", 0)
+    if solves == 0:
+        raise SystemExit(f"{w}: no {SOLVE_MARK[w]} launch in the request-counter run")
+    tr = os.path.join(ROOT, "profiles", f"{tag}_kernel_stats{'' if w == 'c2' else '_' + w}.csv")
+    dur = trace_avg_ns(tr) if os.path.exists(tr) else {}
+    tot = {c: 0.0 for c in REQ_CTRS}
+    for k, e in kernels.items():
+        n = max(e["launches"], 1)
+        for c in REQ_CTRS:
+            e[c + "_per_launch"] = e.get(c, 0.0) / n
+            if solve_kernel(k):
+                tot[c] += e.get(c, 0.0) / solves
+        if k in dur:
+            e["avg_ns"] = dur[k][0]
+            req = e.get("TCC_EA0_RDREQ_sum", 0.0) / n + e.get("TCC_EA0_WRREQ_sum", 0.0) / n
+            e["requests_per_s"] = req / (dur[k][0] * 1e-9) if dur[k][0] > 0 else None
+    return dict(workload=w, solves=solves, solve_marker=SOLVE_MARK[w], kernel_trace=os.path.relpath(tr, ROOT),
+                solve_rdreq=tot["TCC_EA0_RDREQ_sum"], solve_wrreq=tot["TCC_EA0_WRREQ_sum"],
+                solve_atomic=tot["TCC_EA0_ATOMIC_sum"],
+                solve_requests=tot["TCC_EA0_RDREQ_sum"] + tot["TCC_EA0_WRREQ_sum"], kernels=kernels)
+
+
+def calibration_requests():
+    """Request ceilings of the calibration kernels (scripts/ubench_gather.hip): requests per second of each kernel
+    (counter pass / its average duration in the kernel trace of the same program)."""
+    paths = {c: os.path.join(OUT, f"rp_cal_{c}", "run_counter_collection.csv") for c in REQ_CTRS}
+    tr = os.path.join(OUT, "rp_trace_cal", "run_kernel_stats.csv")
+    if not all(os.path.exists(p) for p in paths.values()) or not os.path.exists(tr):
+        return None
+    dur = trace_avg_ns(tr)
+    out = {}
+    for c, p in paths.items():
+        for name, (v, n) in load_count(p).items():
+            k = short(name)
+            if "<" in name:  # gather<double> / gather<float> ...: keep the element type
+                k = name.split("(")[0].replace("void ", "")
+            e = out.setdefault(k, {"dispatches": n})
+            e[c + "_per_dispatch"] = v / max(n, 1)
+    for k, e in out.items():
+        d = dur.get(short(k))
+        if d:
+            e["avg_ns"] = d[0]
+            e["requests_per_s"] = (e.get("TCC_EA0_RDREQ_sum_per_dispatch", 0) + e.get("TCC_EA0_WRREQ_sum_per_dispatch", 0)) \
+                / (d[0] * 1e-9)
+    return out
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "latest"
     prof = os.path.join(ROOT, "profiles")
@@ -97,6 +180,16 @@ def main():
         for k, e in sorted(t["kernels"].items(), key=lambda kv: -(kv[1]["fetch_bytes"] + kv[1]["write_bytes"]))[:8]:
             print(f"   {k:24s} launches {e['launches']:5d}  fetch/launch {e['fetch_bytes_per_launch'] / 1e6:9.2f} MB"
                   f"  write/launch {e['write_bytes_per_launch'] / 1e6:9.2f} MB")
+    for w in ("c2",):
+        t = workload_requests(w, tag)
+        if t is None:
+            continue
+        cal = calibration_requests()
+        t["calibration"] = cal
+        with open(os.path.join(prof, f"{tag}_requests_{w}.json"), "w") as f:
+            json.dump(t, f, indent=1)
+        print(f"{w}: requests per solve {t['solve_requests']:.4g} (rd {t['solve_rdreq']:.4g}, wr {t['solve_wrreq']:.4g}, "
+              f"atomic {t['solve_atomic']:.4g})")
     cf = os.path.join(OUT, "rp_cal_FETCH_SIZE", "run_counter_collection.csv")
     cw = os.path.join(OUT, "rp_cal_WRITE_SIZE", "run_counter_collection.csv")
     if os.path.exists(cf) and os.path.exists(cw):

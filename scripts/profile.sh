@@ -2,7 +2,7 @@
 # rocprofv3 evidence for bench.py (run on the GPU box via gpurun).  Counter passes are separate from
 # the kernel-trace passes, one counter per pass, as MI355X_MICROARCH.md prescribes (FETCH_SIZE and
 # WRITE_SIZE do not fit in one pass).  Output: gpurun_out/rp_*/ (CSV), summarised into profiles/ by
-# scripts/parse_rocprof.py.  usage: PARTS="trace c3 c4 c5 pmc cal" scripts/profile.sh
+# scripts/parse_rocprof.py.  usage: PARTS="trace c3 c4 c5 pmc req cal" scripts/profile.sh
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -39,6 +39,16 @@ if has pmc; then
       run gpurun_out/rp_${ctr}_$w.log 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_${ctr}_$w -o run \
         -- python3 bench.py $(wl_args $w 2)
     done
+  done
+fi
+if has req; then  # request counts (the request-rate roofline): one counter per pass, C2 and calibration
+  run gpurun_out/rp_trace_cal.log 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_cal \
+    -o run -- ./scripts/ubench_gather
+  for ctr in TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum; do
+    run gpurun_out/rp_${ctr}_c2.log 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_${ctr}_c2 -o run \
+      -- python3 bench.py $(wl_args c2 2)
+    run gpurun_out/rp_cal_$ctr.log 200 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_cal_$ctr -o run \
+      -- ./scripts/ubench_gather
   done
 fi
 if has cal; then  # calibration on known byte counts (scripts/ubench_gather.hip: 320 MB int32 stream, gathers)
