@@ -260,7 +260,10 @@ def test_persistent_rendezvous_deadline_falls_back_fast():
     s = L.System(False)
     ids = build(s)
     s.set_engine(L.System.ENGINE_PERSISTENT)
-    s.solve()
+    s.set_resident(False)  # (host flatten: prepare / device_solve / fetch re-solve the unchanged system)
+    s.prepare()
+    s.device_solve()
+    s.fetch()
     assert s.engine_fallbacks() == 0 and s.values_of(ids).tobytes() == ref.tobytes()
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "occupy_run.py")
     p = subprocess.Popen([sys.executable, script, "0", "2.0"], stdout=subprocess.PIPE, text=True)
@@ -337,6 +340,7 @@ def test_tail_handoff_bit_identical(name, tail, child, monkeypatch):
     s = L.System(False)
     ids = TAIL_CASES[name](s)
     s.set_engine(L.System.ENGINE_ROUNDS)
+    s.set_resident(False)
     s.prepare()
     nv = s.last_stats()["n_var"]
     monkeypatch.setenv("LMMHIP_TAIL_ROWS", str(nv if tail == "early" else max(1, nv // 2)))
