@@ -99,6 +99,18 @@ template <class T> __device__ __forceinline__ void st_rlx(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A ready candidate listed by the update (round engine, LMMHIP_SATENT): what the saturation needs of the
+// constraint besides its readiness — its ratio (the level its variables are fixed at) and its CSC range — so
+// the saturation reads them with the entry instead of gathering them after it.
+struct alignas(16) SatEnt {
+  double ratio;
+  int32_t c;
+  uint32_t beg, end;
+  int32_t dup;
+  int32_t pad[2];
+};
+static_assert(sizeof(SatEnt) == 32, "SatEnt is two 16-B loads");
+
 struct Dev {
   int32_t nV, nC;
   int64_t nnz;
@@ -194,6 +206,7 @@ struct Dev {
   int32_t* rdq[2];   // round engine, short rows (LMMHIP_RDQ): constraints the vote made ready, by round parity
   int32_t* rqst;     // [nC] the round a constraint was last queued for (one entry per constraint and round)
   int32_t* useg;     // [blocks x kUSeg] the update's ready candidates for the next round, a segment per workgroup
+  struct SatEnt* uent;  // (LMMHIP_SATENT) the same candidates as records: ratio and CSC range with the id
   int32_t* ucnt;     // [blocks] their counts
   uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words

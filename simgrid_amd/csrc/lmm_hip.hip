@@ -35,6 +35,7 @@ using namespace lmmdev;
 constexpr unsigned kPersistProfCap = 1 << 16;  // barriers covered by lmmhip_persist_profile
 constexpr int64_t kAutoPersistVars = 1 << 18;   // LMMHIP_ENGINE_AUTO: one of the single-GPU small-system engines up to
 constexpr int64_t kAutoPersistMaxVars = 1 << 14;  // this many variables: persistent up to 2^14, frontier above
+constexpr int kSatEntDefault = 0;  // LMMHIP_SATENT default (the update's ready candidates as records)
 constexpr int64_t kTailRows = 0;  // LMMHIP_TAIL_ROWS default: alive rows at which a solve's tail is handed off
 
 namespace {
@@ -97,6 +98,7 @@ struct lmmhip_ctx {
   int engine = LMMHIP_ENGINE_AUTO;
   int sat_waves = 1;  // waves per ready constraint in mm_saturate (mean 64-element CSC chunks, 1/2/4)
   bool vote_diag = std::getenv("LMMHIP_VOTE_DIAG") != nullptr;  // profiling: diagnostic vote launches
+  bool vote_bits = true;  // short-row vote: changed-constraint bitmap in LDS (LMMHIP_VOTE_BITS=0: the stamps' path)
   unsigned* pbar = nullptr;
   bool persist_prof = false;    // record barrier timestamps in the persistent launch
   long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
@@ -179,6 +181,7 @@ struct lmmhip_ctx {
   Scr tl_cf, tl_cmap, tl_rl, tl_rlo, tl_rf, tl_rvo, tl_sk0, tl_sk1, tl_sv0, tl_sv1, tl_tmp, tl_vmap, tl_cnt;
   Scr mm_crec[3];  // solve_maxmin: packed row records (LMMHIP_CREC)
   Scr mm_rdq[2], mm_rqst, mm_useg, mm_ucnt;  // solve_maxmin: ready queue / update segments (LMMHIP_RDQ)
+  Scr mm_uent;  // solve_maxmin: the update segments as records (LMMHIP_SATENT)
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
@@ -321,7 +324,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->tl_cf, &c->tl_cmap, &c->tl_rl, &c->tl_rlo, &c->tl_rf, &c->tl_rvo, &c->tl_sk0, &c->tl_sk1, &c->tl_sv0, &c->tl_sv1, &c->tl_tmp, &c->tl_vmap, &c->tl_cnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->mm_uent, &c->tl_cf, &c->tl_cmap, &c->tl_rl, &c->tl_rlo, &c->tl_rf, &c->tl_rvo, &c->tl_sk0, &c->tl_sk1, &c->tl_sv0, &c->tl_sv1, &c->tl_tmp, &c->tl_vmap, &c->tl_cnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc})
@@ -1300,7 +1303,7 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
   switch (G) {
   case 4:
   case 8:  // short rows: one lane per row (more gathers in flight per wave)
-    if (int64_t(d.nC) <= int64_t(kBitWords) * 64) {
+    if (int64_t(d.nC) <= int64_t(kBitWords) * 64 && c->vote_bits) {
       if (c->profiling && c->vote_diag) {  // measurement: bitmap load alone, filter alone (slot 7)
         LAUNCH(7, r + 1000000, (mm_vote_lane<kVBlock, true, 2>), c->n_cu, kVBlock, d, int(r));
         LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
@@ -1344,6 +1347,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
       d.rdq[0] = d.rdq[1] = nullptr;
       d.rqst = d.useg = d.ucnt = nullptr;
+      d.uent = nullptr;
     }
   } rowof_off{d};
   // packed row records for the re-votes (vote_row: the row's variable and CSR range from one 8-B record and
@@ -1363,6 +1367,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // 25.07-25.22 vs 25.34-25.39 ms, stress 28.29 vs 28.46, same box; LMMHIP_RDQ=0: the mm_ready pass)
   d.rdq[0] = d.rdq[1] = nullptr;
   d.rqst = d.useg = d.ucnt = nullptr;
+  d.uent = nullptr;
   const int64_t gU_rdq = grid_for(d.nC, kBlock);  // (<= kMaxBlocks)
   const int64_t per_blk = int64_t(kBlock) * ((int64_t(d.nC) + gU_rdq * kBlock - 1) / (gU_rdq * kBlock));
   if (d.crec[0] && env_int("LMMHIP_RDQ", 1) && per_blk <= kUSeg && env_int("LMMHIP_UPD_BLOCKS", c->tune_upd) == 0) {
@@ -1379,6 +1384,15 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     d.rqst = st;
     d.useg = sg;
     d.ucnt = uc;
+    // the candidates as records (ratio + CSC range with the id: the saturation's readiness test overlaps its
+    // first element loads) — LMMHIP_SATENT, A/B knob
+    d.uent = nullptr;
+    if (env_int("LMMHIP_SATENT", kSatEntDefault)) {
+      SatEnt* ue = nullptr;
+      if (int rc = scratch(c, c->mm_uent, gU_rdq * kUSeg, &ue))
+        return rc;
+      d.uent = ue;
+    }
   }
   // the saturation retires the rows of the variables it fixes (row map kept by init / cmp_write; not with
   // the target-ordered regroups, whose unpack would have to maintain it too).  Opt-in (LMMHIP_RETIRE=1):
@@ -1391,6 +1405,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       return rc;
     d.rowof = ro;
   }
+  c->vote_bits = env_int("LMMHIP_VOTE_BITS", 1) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   const int gC = grid_for(d.nC, kBlock);
   if (c->cont)  // a handed-off tail (lmm_tail_kernels.hpp): the constraint state came with the system
@@ -1473,6 +1488,16 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         LAUNCH(2, r, mm_vote_tgt<kBlock>, gv, kBlock, d, int(r));
       } else if (int rc = launch_vote(c, r, nrows))
         return rc;
+      if (d.rdq[0] && d.uent) {  // the update's candidates as records (LMMHIP_SATENT)
+        if (sat_k == 1)
+          LAUNCH(4, r, (mm_saturate_q<1, true>), capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
+        else if (sat_k == 2)
+          LAUNCH(4, r, (mm_saturate_q<2, true>), capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        else
+          LAUNCH(4, r, (mm_saturate_q<4, true>), capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        LAUNCH(5, r, (mm_update<true, true>), gUq, kBlock, d, int(r), prec);
+        continue;
+      }
       if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
         if (sat_k == 1)
           LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);

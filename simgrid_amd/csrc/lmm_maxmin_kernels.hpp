@@ -1012,8 +1012,13 @@ constexpr int kSatU = 4;
 // retire (multi-launch engine, round 4): the buffer's row targets; each claimed variable's alive row (rowof) is
 // marked kRetired, so the next vote's filter skips it instead of queueing a re-vote that only finds the
 // variable fixed (~6.4e4 rows per C2 round).
-__device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
-                                               int round, int lane, int* pre, bool dup, int32_t* retire = nullptr) {
+// kChk (ready candidates listed as records, LMMHIP_SATENT): the constraint's key `kc` and count `nv` were loaded by
+// the caller but not yet tested; the test is made here, after the chunk's element loads are issued (so their
+// latency overlaps), and before any store — a constraint that is no longer ready returns false untouched.
+template <bool kChk = false>
+__device__ __forceinline__ bool saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
+                                               int round, int lane, int* pre, bool dup, int32_t* retire = nullptr,
+                                               unsigned kc = 0, int nv = 0) {
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
   int32_t lv = -1, ro = 0;
@@ -1027,6 +1032,10 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     const unsigned long long row = s.csc_row[j];
     rb = uint32_t(row);
     re = uint32_t(row >> 32);
+  }
+  if (kChk && !(kc != kDeadKey && nv == 0))  // wave-uniform: not ready after this round's vote
+    return false;
+  if (j < ce) {
     if (retire)
       ro = s.rowof[lv];  // (issued with the state's load)
     if (s.vstate[lv] != 0)
@@ -1113,6 +1122,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     }
   }
   __builtin_amdgcn_wave_barrier();
+  return true;
 }
 
 // Ready test + saturation, block-cooperative.  In pass p, wave w of workgroup b tests the 64 constraints of
@@ -1294,7 +1304,8 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 // them, mm_saturate's prefix and binary search over their counts) then the vote's queue; K waves per entry;
 // an entry is saturated when it is still alive with nothing voting elsewhere (every vote of the round is in).
 // Block 0 empties the other parity's vote queue, which the next round's vote fills.
-template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
+template <int K, bool kEnt = false>
+__global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1349,6 +1360,21 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
       for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
         if (lo + step < ublocks && pre[lo + step] <= i)
           lo += step;
+      if (kEnt) {  // the record: ratio and CSC range with the id; readiness tested inside, after the first loads
+        const SatEnt e = s.uent[int64_t(lo) * kUSeg + (i - pre[lo])];
+        const unsigned kc = s.key[e.c];
+        const int nv = s.nvote[e.c];
+        bool ok = e.beg == e.end && kc != kDeadKey && nv == 0;  // (an empty column: nothing to fix)
+        for (uint32_t base = e.beg + uint32_t(k) * kWave; base < e.end; base += K * kWave)  // wave-uniform
+          if (!(ok = saturate_chunk<true>(s, e.c, e.ratio, base, e.end, round, lane, wpre[w], e.dup != 0, retire, kc,
+                                          nv)))
+            break;
+        if (ok && k == 0 && lane == 0) {
+          s.ctouch[e.c] = 2;  // c leaves the light table: mm_update (the owner of key / chg) retires it
+          s.ctl[CTL_LASTR] = round;
+        }
+        continue;
+      }
       c = s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
     } else {
       c = q[i - total];
@@ -1371,7 +1397,10 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
 // K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups (key and touch
 // flag, then — touched constraints only — record, flags, scale, votes) is issued before any of them is
 // used, so a wave keeps K times the memory requests in flight.
-template <int K, bool kRdq = false>
+// kEnt (LMMHIP_SATENT): the ready candidates are written as records (SatEnt: ratio, CSC range, duplicate flag)
+// straight into the workgroup's segment of s.uent; their CSC range and flag are loaded with the record of every
+// touched constraint (coalesced in identity order).
+template <int K, bool kRdq = false, bool kEnt = false>
 __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
                                              bool* touch, int* ucnt_sh = nullptr, int32_t* ulist = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -1385,12 +1414,16 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
   unsigned long long qx[K], qy[K], qz[K];
   double rem[K], use[K], bnd[K];
   int32_t ce[K], nv[K];
+  uint32_t cpb[K], cpe[K];
+  int32_t cdp[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int64_t c = base0 + k * stride + lane;
     qx[k] = qy[k] = qz[k] = 0;
     rem[k] = use[k] = bnd[k] = 0.0;
     ce[k] = nv[k] = 0;
+    cpb[k] = cpe[k] = 0;
+    cdp[k] = 0;
     if (okey[k] != kDeadKey && tf[k] == 1) {  // an untouched constraint keeps its record as it is
       const CstRec* rec = s.cst + c;
       qx[k] = rec->drem;
@@ -1401,6 +1434,11 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       bnd[k] = rec->bound;
       ce[k] = s.cexp[c];
       nv[k] = s.nvote[c];
+      if (kEnt) {
+        cpb[k] = s.cnst_ptr[c];
+        cpe[k] = s.cnst_ptr[c + 1];
+        cdp[k] = s.cdup[c];
+      }
     }
   }
   int alive = 0;
@@ -1477,7 +1515,19 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
           changed = nk != okey[k];
           alive++;
           if (kRdq && nvn == 0) {  // its last elements voting elsewhere left with fixed variables: ready next
-            ulist[atomicAdd(ucnt_sh, 1)] = int32_t(c);  // round (the stamp keeps the vote from queueing it too)
+            const int slot = atomicAdd(ucnt_sh, 1);  // round (the stamp keeps the vote from queueing it too)
+            if (kEnt) {
+              SatEnt e;
+              e.ratio = r;
+              e.c = int32_t(c);
+              e.beg = cpb[k];
+              e.end = cpe[k];
+              e.dup = cdp[k];
+              e.pad[0] = e.pad[1] = 0;
+              s.uent[int64_t(blockIdx.x) * kUSeg + slot] = e;
+            } else {
+              ulist[slot] = int32_t(c);
+            }
             s.rqst[c] = round + 1;
           }
         }
@@ -1492,13 +1542,14 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
 
 // balive[block] = constraints of the block's range still in the light table (read by mm_done; plain
 // stores, no global atomic).
-template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+template <bool kRdq = false, bool kEnt = false>
+__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_ROUNDS] += 1;
   __shared__ int alive_cnt, ucnt_sh;
-  __shared__ int32_t ulist[kRdq ? kUSeg : 1];
+  __shared__ int32_t ulist[kRdq && !kEnt ? kUSeg : 1];
   if (threadIdx.x == 0)
     alive_cnt = ucnt_sh = 0;
   __syncthreads();
@@ -1507,7 +1558,7 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
        base += 2 * stride)  // wave-uniform; two groups of 64 constraints per step, loads in flight together
-    alive += update_groups<2, kRdq>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
+    alive += update_groups<2, kRdq, kEnt>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
@@ -1515,7 +1566,7 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
     s.balive[blockIdx.x] = alive_cnt;
   if (kRdq) {  // the workgroup's ready candidates for the next round into its segment
     const int n = ucnt_sh;
-    for (int i = threadIdx.x; i < n; i += kBlock)
+    for (int i = threadIdx.x; i < n && !kEnt; i += kBlock)
       s.useg[int64_t(blockIdx.x) * kUSeg + i] = ulist[i];
     if (threadIdx.x == 0)
       s.ucnt[blockIdx.x] = n;
