@@ -181,12 +181,18 @@ def test_target_ordered_vote_bit_identical(stress, monkeypatch):
     # (LMMHIP_TGT, LMMHIP_RETIRE, LMMHIP_CREC, LMMHIP_RDQ): the row retirement by the saturation, the packed row
     # records and the ready constraints listed by the update and the vote (no mm_ready pass) must not change a
     # byte either
-    for tgt, retire, crec, rdq in (("1", "0", "0", "0"), ("0", "0", "0", "0"), ("0", "1", "1", "0"),
-                                   ("0", "0", "1", "0"), ("0", "0", "1", "1"), ("0", "1", "1", "1")):
+    # (+ LMMHIP_SATENT: the update's ready candidates as records; LMMHIP_VOTE_BITS=0: the stamps' filter)
+    for tgt, retire, crec, rdq, ent, bits in (("1", "0", "0", "0", "0", "1"), ("0", "0", "0", "0", "0", "1"),
+                                              ("0", "1", "1", "0", "0", "1"), ("0", "0", "1", "0", "0", "1"),
+                                              ("0", "0", "1", "1", "0", "1"), ("0", "1", "1", "1", "0", "1"),
+                                              ("0", "0", "1", "1", "1", "1"), ("0", "1", "1", "1", "1", "1"),
+                                              ("0", "0", "1", "1", "1", "0")):
         monkeypatch.setenv("LMMHIP_TGT", tgt)
         monkeypatch.setenv("LMMHIP_RETIRE", retire)
         monkeypatch.setenv("LMMHIP_CREC", crec)
         monkeypatch.setenv("LMMHIP_RDQ", rdq)
+        monkeypatch.setenv("LMMHIP_SATENT", ent)
+        monkeypatch.setenv("LMMHIP_VOTE_BITS", bits)
         out.append(_values(_synthetic(100000, 1000000, 1, stress), L.System.ENGINE_ROUNDS))
     for o in out[1:]:
         assert out[0][1] == o[1]
