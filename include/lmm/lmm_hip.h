@@ -110,6 +110,14 @@ int lmmhip_res_values(lmmhip_ctx* ctx, int64_t n, double* values, uint8_t* reset
 /* Same, into context-owned pinned host buffers (valid until the next call / lmmhip_ctx_destroy): the
  * D2H runs at full PCIe rate and the caller scatters from them without another copy. */
 int lmmhip_res_values_pinned(lmmhip_ctx* ctx, int64_t n, const double** values, const uint8_t** reset);
+/* Same values, fetched in `nslices` slices the caller can scatter while the next ones are still in flight
+ * (System::fetch_resident): ONE array in context-owned pinned memory, where a slot the solve leaves alone holds
+ * the bit pattern LMMHIP_VAL_KEEP (a signalling NaN no arithmetic produces) instead of a separate reset flag.
+ * Returns once everything is queued; lmmhip_res_values_wait(ctx, i) blocks until slice i (slots
+ * [i * ceil(n / nslices), ...)) has landed.  Valid until the next fetch / lmmhip_ctx_destroy. */
+#define LMMHIP_VAL_KEEP 0x7FF4C0FFEE5107E5ull
+int lmmhip_res_values_sliced(lmmhip_ctx* ctx, int64_t n, int nslices, const double** values);
+int lmmhip_res_values_wait(lmmhip_ctx* ctx, int slice);
 /* Number of lmmhip_res_flatten calls served by the refresh path (same constraint list and precision,
  * no element record / slab change since the last flatten, and no constraint bound crossing the part
  * test (maxmin.cpp:523-525) in a way that changes the member set: only the dense penalties and bounds

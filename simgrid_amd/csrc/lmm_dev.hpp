@@ -220,6 +220,9 @@ __device__ __forceinline__ bool rbounded(int32_t cv) { return cv < 0; }
 
 constexpr int kStatRounds = 4096;  // rounds covered by the profiling counters
 constexpr int32_t kUnvoted = -1;   // row target: not evaluated yet
+// A signalling NaN (quiet bit clear, distinctive payload): no fp64 arithmetic returns it, so it can mark "leave this
+// slot alone" inside an array of values (rs_values_mark, lmmhip_res_values_sliced).
+constexpr unsigned long long kValKeep = 0x7FF4C0FFEE5107E5ull;  // (= LMMHIP_VAL_KEEP, include/lmm/lmm_hip.h)
 constexpr int32_t kRetired = -2;   // row target: variable fixed or dropped (skip until compaction)
 
 __device__ __forceinline__ double dinf() { return __builtin_huge_val(); }

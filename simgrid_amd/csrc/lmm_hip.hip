@@ -77,6 +77,7 @@ struct lmmhip_ctx {
   std::vector<void*> allocs;  // owned device allocations
   int32_t* h_ctl = nullptr;   // pinned mirror of the control words (+ 2 slots: pipelined polls of solve_maxmin)
   hipEvent_t ev_poll[2] = {nullptr, nullptr};  // completion of the pipelined control-word copies
+  std::vector<hipEvent_t> ev_slice;  // lmmhip_res_values_sliced: completion of each slice's copy
   bool uploaded = false;
   bool profiling = false;
   int group = 8;  // lanes per row in mm_vote (power of two >= mean row length, <= 64)
@@ -346,6 +347,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   for (hipEvent_t ev : c->ev_poll)
     if (ev)
       (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : c->ev_slice)
+    (void)hipEventDestroy(ev);
   if (c->vstat)
     (void)hipFree(c->vstat);
   if (c->pbar)
@@ -1125,6 +1128,58 @@ int lmmhip_res_values_pinned(lmmhip_ctx* c, int64_t n, const double** values, co
   HIPCHK(hipStreamSynchronize(c->stream));
   *values = c->pin_vals;
   *reset = c->pin_rst;
+  return 0;
+}
+
+int lmmhip_res_values_sliced(lmmhip_ctx* c, int64_t n, int nslices, const double** values) {
+  if (!c || !c->uploaded || !c->res_flat)
+    return fail(LMMHIP_E_STATE, "no resident flatten to read values from");
+  if (n != c->res_flat_nv || !values || nslices < 1 || nslices > 256)
+    return fail(LMMHIP_E_ARG, "values: n must be the last resident flatten's slot count, 1 <= nslices <= 256");
+  HIPCHK(hipSetDevice(c->device));
+  if (n > c->pin_cap) {
+    if (c->pin_vals)
+      HIPCHK(hipHostFree(c->pin_vals));
+    if (c->pin_rst)
+      HIPCHK(hipHostFree(c->pin_rst));
+    c->pin_vals = nullptr;
+    c->pin_rst = nullptr;
+    c->pin_cap = 0;
+    const int64_t cap = std::max(n, c->pin_cap + c->pin_cap / 4);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_vals), size_t(cap) * sizeof(double), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_rst), size_t(cap), hipHostMallocDefault));
+    c->pin_cap = cap;
+  }
+  while (int(c->ev_slice.size()) < nslices) {
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->ev_slice.push_back(ev);
+  }
+  double* vout = nullptr;
+  if (int rc = scratch(c, c->rs_vout, n, &vout))
+    return rc;
+  if (n) {
+    const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
+    const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
+    RS_LAUNCH(rs_values_mark, n, n, vm, dv, static_cast<const uint8_t*>(c->rs_vrst.p), c->d.x,
+              reinterpret_cast<unsigned long long*>(vout));
+  }
+  const int64_t per = (n + nslices - 1) / nslices;
+  for (int i = 0; i < nslices; i++) {
+    const int64_t lo = std::min(n, i * per), hi = std::min(n, lo + per);
+    if (hi > lo)
+      HIPCHK(hipMemcpyAsync(c->pin_vals + lo, vout + lo, size_t(hi - lo) * sizeof(double), hipMemcpyDeviceToHost,
+                            c->stream));
+    HIPCHK(hipEventRecord(c->ev_slice[size_t(i)], c->stream));
+  }
+  *values = c->pin_vals;
+  return 0;
+}
+
+int lmmhip_res_values_wait(lmmhip_ctx* c, int slice) {
+  if (!c || slice < 0 || slice >= int(c->ev_slice.size()))
+    return fail(LMMHIP_E_ARG, "no such slice");
+  HIPCHK(hipEventSynchronize(c->ev_slice[size_t(slice)]));
   return 0;
 }
 

@@ -516,6 +516,19 @@ __global__ void __launch_bounds__(kBlock) rs_ptr32(int64_t n, const int64_t* __r
     out[i] = uint32_t(in[i]);
 }
 
+// The sliced fetch (lmmhip_res_values_sliced): ONE array, per variable slot the value the host writes back (as
+// rs_values: the solved value of a member, 1.0 / 0 for a reset non-member) and, for the slots the host must leave
+// alone (vrst 0), kValKeep — a signalling-NaN payload no arithmetic produces — instead of a separate flag array.
+__global__ void __launch_bounds__(kBlock)
+    rs_values_mark(int64_t nv, const int64_t* __restrict__ vm, const int64_t* __restrict__ dv,
+                   const uint8_t* __restrict__ vrst, const double* __restrict__ x, unsigned long long* out) {
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < nv; v += int64_t(gridDim.x) * kBlock) {
+    const uint8_t r = vrst[v];
+    const double val = vm[v] ? x[dv[v]] : r == 3 ? 1.0 : 0.0;
+    out[v] = r ? (unsigned long long)__double_as_longlong(val) : kValKeep;
+  }
+}
+
 // Per variable slot after the solve: the solved value of a member, 0 for the others (only slots with
 // vrst set are written back by the host); rst_out (optional) receives a copy of the reset flags.
 __global__ void __launch_bounds__(kBlock)

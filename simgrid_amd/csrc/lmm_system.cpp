@@ -12,6 +12,7 @@
 #include "lmm_system.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <chrono>
 #include <cmath>
@@ -1068,31 +1069,42 @@ void System::prepare_resident() {
 void System::fetch_resident() {
   auto t0 = std::chrono::steady_clock::now();
   const size_t n = vars_.size();
-  const double* vals = nullptr;
-  const uint8_t* rst = nullptr;
-  int rc = lmmhip_res_values_pinned(ctx(), int64_t(n), &vals, &rst);
-  if (rc)
-    fatal(std::string("resident fetch failed: ") + lmmhip_last_error());
   double* out = values_.data();
-  // two streams over pinned memory, one over the value column; large systems in a few slices on host threads
-  // (C2: 1e7 slots, 6-9 ms on one core, memory-bound per core)
-  auto scatter = [&](size_t lo, size_t hi) {
-    for (size_t v = lo; v < hi; v++)
-      if (rst[v])
-        out[v] = vals[v];
-  };
+  // Large systems: the values arrive in slices (lmmhip_res_values_sliced: one array, LMMHIP_VAL_KEEP marks the
+  // slots to leave alone) and host threads scatter each slice as soon as it has landed, while the next ones are
+  // still crossing PCIe (C2: 1e7 slots, 80 MB).  Small ones: one copy, one thread.
   const size_t nt = n >= (size_t(1) << 20) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  const int ns = nt > 1 ? int(4 * nt) : 1;
+  const double* vals = nullptr;
+  if (lmmhip_res_values_sliced(ctx(), int64_t(n), ns, &vals))
+    fatal(std::string("resident fetch failed: ") + lmmhip_last_error());
+  const size_t per = (n + size_t(ns) - 1) / size_t(ns);
+  const uint64_t* bits = reinterpret_cast<const uint64_t*>(vals);
+  std::atomic<int> err{0};
+  auto work = [&](size_t t) {
+    for (size_t i = t; i < size_t(ns); i += nt) {
+      if (lmmhip_res_values_wait(ctx(), int(i))) {
+        err = 1;
+        return;
+      }
+      const size_t lo = std::min(n, i * per), hi = std::min(n, lo + per);
+      for (size_t v = lo; v < hi; v++)
+        if (bits[v] != LMMHIP_VAL_KEEP)
+          out[v] = vals[v];
+    }
+  };
   if (nt <= 1) {
-    scatter(0, n);
+    work(0);
   } else {
     std::vector<std::thread> pool;
-    const size_t per = (n + nt - 1) / nt;
     for (size_t t = 1; t < nt; t++)
-      pool.emplace_back(scatter, std::min(n, t * per), std::min(n, (t + 1) * per));
-    scatter(0, std::min(n, per));
+      pool.emplace_back(work, t);
+    work(0);
     for (auto& th : pool)
       th.join();
   }
+  if (err)
+    fatal(std::string("resident fetch failed: ") + lmmhip_last_error());
   res_prepared_ = false;
   stats_.fetch_ms = ms_since(t0);
   finish_solve();

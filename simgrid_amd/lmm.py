@@ -134,6 +134,8 @@ SIGNATURES = {
     "lmmhip_res_values": (I, [P, I64, PD, ct.POINTER(ct.c_uint8)]),
     "lmmhip_res_flatten_fair": (I, [P, I64, ct.POINTER(ct.c_int32), PI64]),
     "lmmhip_res_values_pinned": (I, [P, I64, ct.POINTER(P), ct.POINTER(P)]),
+    "lmmhip_res_values_sliced": (I, [P, I64, I, ct.POINTER(P)]),
+    "lmmhip_res_values_wait": (I, [P, I]),
     "lmmhip_res_refreshes": (I, [P, PI64]),
     "lmmhip_res_cross_refreshes": (I, [P, PI64]),
     "lmmhip_flat_download": (I, [P, PI64, P, P, P, P, P, P, P, P, P, P]),
