@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <thread>
 #include <chrono>
 #include <cmath>
@@ -1074,7 +1075,8 @@ void System::fetch_resident() {
   // slots to leave alone) and host threads scatter each slice as soon as it has landed, while the next ones are
   // still crossing PCIe (C2: 1e7 slots, 80 MB).  Small ones: one copy, one thread.
   const size_t nt = n >= (size_t(1) << 20) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
-  const int ns = nt > 1 ? int(4 * nt) : 1;
+  const char* sl = std::getenv("LMM_FETCH_SLICES");  // measurement knob: slices per fetch (1: one copy, then scatter)
+  const int ns = sl && *sl ? std::max(1, std::min(256, std::atoi(sl))) : nt > 1 ? int(4 * nt) : 1;
   const double* vals = nullptr;
   if (lmmhip_res_values_sliced(ctx(), int64_t(n), ns, &vals))
     fatal(std::string("resident fetch failed: ") + lmmhip_last_error());
