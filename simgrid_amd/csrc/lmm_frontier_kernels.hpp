@@ -467,7 +467,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 // (fr_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
 constexpr int kFS = 1024;
 
-template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round) {
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ SatLds<kFS, kFS> L;
@@ -481,7 +481,7 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
     nch = int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave);
     if (s.vstat)
       atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 5, 1);
-    if (nch > kFrBigCh) {  // rare (fat-tree core links): spread over the grid by fr_sat_big
+    if (nch > bigch) {  // rare (fat-tree core links): spread over the grid by fr_sat_big
       s.ready[atomicAdd(&s.ctl[CTL_NREADY], 1)] = int32_t(c);
       rdy = false;
       nch = 0;
@@ -526,7 +526,7 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
 
 // The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
 // constraint over the whole grid, wave k taking chunks k, k + kFrBigWaves, ...
-__global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round) {
+__global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round, int bigw) {
   if (s.ctl[CTL_DONE])
     return;
   const int nb = s.ctl[CTL_NREADY];
@@ -538,13 +538,13 @@ __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  for (int64_t g = wave; g < int64_t(nb) * kFrBigWaves; g += nwaves) {
-    const int32_t c = s.ready[g / kFrBigWaves];
-    const int k = int(g % kFrBigWaves);
+  for (int64_t g = wave; g < int64_t(nb) * bigw; g += nwaves) {
+    const int32_t c = s.ready[g / bigw];
+    const int k = int(g % bigw);
     const double r = ld_rlx(&s.cst[c].ratio);
     const uint32_t ce = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
-    for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += kFrBigWaves * kWave)
+    for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
       fr_sat_chunk(s, c, r, base, ce, round, lane, wpre[w], dup);
     if (k == 0 && lane == 0)
       s.ctouch[c] = 2;

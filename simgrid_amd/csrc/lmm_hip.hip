@@ -1756,7 +1756,11 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
     HIPCHK(hipStreamSynchronize(c->stream));
     c->fr_map_ok = true;
   }
-  const bool big = c->fr_maxdeg > kFrBigCh * kWave;
+  // constraints of more CSC chunks than this saturate in fr_sat_big, kFrBigWaves waves each over the whole grid
+  // (LMMHIP_FR_BIGCH, A/B knob: fat-tree core links' chunk chains in C4)
+  const int bigch = std::max(1, env_int("LMMHIP_FR_BIGCH", kFrBigCh));
+  const bool big = c->fr_maxdeg > bigch * kWave;
+  const int bigw = std::max(1, env_int("LMMHIP_FR_BIGW", kFrBigWaves));  // waves per big constraint (A/B knob)
   // measurement knobs (defaults = the measured best): the re-vote reads the floors with the keys; the
   // saturation's workgroup size and chunk body (the round engine's saturate_chunk)
   const bool mf_early = env_int("LMMHIP_FR_MFEARLY", 0) != 0;
@@ -1807,15 +1811,15 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
         LAUNCH(2, r, fr_vote<false>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       }
       if (sat_b == 256 && sat_old)
-        LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r));
+        LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
       else if (sat_b == 256)
-        LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r));
+        LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
       else if (sat_old)
-        LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r));
+        LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r), bigch);
       else
-        LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r));
+        LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
       if (big)
-        LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r));
+        LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r), bigw);
       LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec);
     }
     LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
