@@ -160,6 +160,11 @@ struct lmmhip_ctx {
   bool res_struct_host = true;
   int32_t* res_dirty = nullptr;
   int64_t res_refreshes = 0, res_cross_refreshes = 0;
+  // refresh path: the variables the delta batches touched since the last flatten (-1: too many), and whether rs_c2c
+  // (CSR -> CSC position map, written by the device flatten's transpose) matches the uploaded structure
+  Scr rs_vlist, rs_c2c;
+  int64_t res_vl_n = 0;
+  bool res_c2c_ok = false;
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
@@ -328,7 +333,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
   for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->mm_uent, &c->tl_cf, &c->tl_cmap, &c->tl_rl, &c->tl_rlo, &c->tl_rf, &c->tl_rvo, &c->tl_sk0, &c->tl_sk1, &c->tl_sv0, &c->tl_sv1, &c->tl_tmp, &c->tl_vmap, &c->tl_cnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
-                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc})
+                             &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc, &c->rs_vlist, &c->rs_c2c})
     if (b->p)
       (void)hipFree(b->p);
   for (lmmhip_ctx::Scr& b : c->rs_stage)
@@ -515,6 +520,7 @@ static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, bool 
   c->fb_perm_ok = false;
   c->fb_renum_ok = false;
   c->fr_map_ok = false;
+  c->res_c2c_ok = false;  // (a resident flatten sets it again once finish_flat returns)
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
   c->group = mean <= 4 ? 4 : mean <= 8 ? 8 : mean <= 16 ? 16 : mean <= 32 ? 32 : 64;
   const double cmean = nC > 0 ? double(nnz) / double(nC) : 1.0;  // mean constraint degree
@@ -852,6 +858,26 @@ int lmmhip_res_apply(lmmhip_ctx* c, int64_t n_elem_total, int64_t n_var_total, i
     if (rc)
       return rc;
     RS_LAUNCH(rs_apply_v, nv, nv, did, deb, dn, dp, db, r, c->res_dirty);
+    // the touched variables, for the refresh path (up to 1/8 of the slots: beyond that a full pass is as cheap)
+    if (c->res_vl_n >= 0 && c->res_vl_n + nv <= std::max<int64_t>(4096, n_var_total / 8)) {
+      int32_t* vl = nullptr;
+      if (c->rs_vlist.bytes < size_t(c->res_vl_n + nv) * sizeof(int32_t)) {  // grow, keeping the list
+        lmmhip_ctx::Scr old = c->rs_vlist;
+        c->rs_vlist = lmmhip_ctx::Scr{};
+        if (int rc = scratch(c, c->rs_vlist, std::max<int64_t>(4096, 2 * (c->res_vl_n + nv)), &vl))
+          return rc;
+        if (old.p && c->res_vl_n > 0)
+          HIPCHK(hipMemcpyAsync(vl, old.p, size_t(c->res_vl_n) * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (old.p)
+          HIPCHK(hipFree(old.p));
+      }
+      vl = static_cast<int32_t*>(c->rs_vlist.p);
+      HIPCHK(hipMemcpyAsync(vl + c->res_vl_n, did, size_t(nv) * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+      c->res_vl_n += nv;
+    } else {
+      c->res_vl_n = -1;  // too many: the refresh path rewrites every member
+    }
   }
   if (nc) {
     const int32_t* did;
@@ -919,9 +945,18 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
       Dev& d = c->d;
       const int64_t* vm = static_cast<const int64_t*>(c->rs_vm.p);
       const int64_t* dv = static_cast<const int64_t*>(c->rs_dv.p);
-      RS_LAUNCH(rs_refresh_v, nvs, nvs, r, vm, dv, const_cast<double*>(d.pen), const_cast<double*>(d.vbound));
-      if ((flags & kResPenalty) && d.nnz > 0)
-        RS_LAUNCH(mm_elem_usage, d.nnz, d, 0);
+      if (c->res_vl_n >= 0 && c->res_c2c_ok && env_int("LMMHIP_RES_VLIST", 1)) {  // the touched variables only
+        const int64_t n = c->res_vl_n;
+        if (n > 0)
+          RS_LAUNCH(rs_refresh_vl, n, n, static_cast<const int32_t*>(c->rs_vlist.p), r, vm, dv,
+                    const_cast<double*>(d.pen), const_cast<double*>(d.vbound), d.var_ptr,
+                    static_cast<const int32_t*>(c->rs_c2c.p), d.csc_w, d.csc_u, d.csc_p, int(flags & kResPenalty));
+      } else {
+        RS_LAUNCH(rs_refresh_v, nvs, nvs, r, vm, dv, const_cast<double*>(d.pen), const_cast<double*>(d.vbound));
+        if ((flags & kResPenalty) && d.nnz > 0)
+          RS_LAUNCH(mm_elem_usage, d.nnz, d, 0);
+      }
+      c->res_vl_n = 0;
       HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
       HIPCHK(hipMemsetAsync(c->res_dirty + 3, 0, sizeof(int32_t), c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
@@ -1047,8 +1082,11 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
     if ((rc = scratch(c, c->rs_tmp, int64_t(tb), &t)))
       return rc;
     HIPCHK(sort_pairs_i32(t, tb, fb.csr_c, skey, kidx, sval, nnz, bits, c->stream));
+    int32_t* c2c = nullptr;
+    if (!fair && (rc = scratch(c, c->rs_c2c, nnz, &c2c)))
+      return rc;
     RS_LAUNCH(rs_csc, nnz, nnz, sval, wrow, rowpen, fb.csc_v, fb.csc_w, c->d.csc_u, c->d.csc_p,
-              c->d.csc_row);
+              c->d.csc_row, c2c);
     if (!fair)
       RS_LAUNCH(rs_cptr_sorted, nnz, nnz, nC, skey, fb.cp);
   }
@@ -1058,6 +1096,8 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   c->res_last_list.assign(cnst_list, cnst_list + nl);
   c->res_last_prec = precision;
   c->res_struct_host = false;
+  c->res_c2c_ok = !fair;
+  c->res_vl_n = 0;
   if (c->res_dirty) {
     HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->res_dirty + 3, 0, sizeof(int32_t), c->stream));

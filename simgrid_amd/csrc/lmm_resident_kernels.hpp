@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(kBlock)
 __global__ void __launch_bounds__(kBlock)
     rs_csc(int64_t nnz, const int32_t* __restrict__ sk, const WRow* __restrict__ wrow,
            const RowPen* __restrict__ rowpen, int32_t* csc_v, double* csc_w, double* csc_u, double* csc_p,
-           unsigned long long* csc_row) {
+           unsigned long long* csc_row, int32_t* c2c) {
   // kCscU elements per thread per step, their two dependent gathers (record, then row) in flight together
   constexpr int kCscU = 4;
   const int64_t stride = int64_t(gridDim.x) * kBlock;
@@ -507,6 +507,35 @@ __global__ void __launch_bounds__(kBlock)
       csc_u[j] = e[u].w / rp[u].pen;
       csc_p[j] = rp[u].pen;
       csc_row[j] = (unsigned long long)rp[u].rb | ((unsigned long long)rp[u].re << 32);
+      if (c2c)  // the inverse map, CSR element -> CSC position (the refresh path's per-variable updates)
+        c2c[k[u]] = int32_t(j);
+    }
+  }
+}
+
+// Refresh path with a list of the variables the delta batches since the last flatten touched (lmmhip_res_apply):
+// their dense penalty and bound, and — penalties moved — the usage w / penalty and penalty of each of their CSC
+// elements, through the CSR -> CSC map rs_csc kept (the same division as mm_elem_usage: identical bits).  Work
+// proportional to the changed variables instead of to the whole system.
+__global__ void __launch_bounds__(kBlock)
+    rs_refresh_vl(int64_t n, const int32_t* __restrict__ list, ResDev r, const int64_t* __restrict__ vm,
+                  const int64_t* __restrict__ dv, double* pen, double* vbound, const uint32_t* __restrict__ var_ptr,
+                  const int32_t* __restrict__ c2c, const double* __restrict__ csc_w, double* csc_u, double* csc_p,
+                  int usage) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const int32_t v = list[i];
+    if (!vm[v])
+      continue;
+    const int64_t d = dv[v];
+    const double p = r.v_pen[v];
+    pen[d] = p;
+    vbound[d] = r.v_bound[v];
+    if (!usage)
+      continue;
+    for (uint32_t k = var_ptr[d]; k < var_ptr[d + 1]; k++) {
+      const int32_t j = c2c[k];
+      csc_u[j] = csc_w[j] / p;
+      csc_p[j] = p;
     }
   }
 }
