@@ -92,13 +92,23 @@ def load_count(path):
     return d
 
 
-def trace_avg_ns(path):
-    """short kernel name -> (average duration ns, calls) from a --kernel-trace --stats summary."""
-    out = {}
+def trace_avg_ns(path, key=None):
+    """kernel name (short(), or `key`) -> (average duration ns, calls) from a --kernel-trace --stats summary;
+    instances that map to one name are merged, weighted by their calls."""
+    key = key or short
+    acc = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            out[short(r["Name"])] = (float(r["AverageNs"]), int(r["Calls"]))
-    return out
+            k = key(r["Name"])
+            ns, n = acc.get(k, (0.0, 0))
+            acc[k] = (ns + float(r["TotalDurationNs"]), n + int(r["Calls"]))
+    return {k: (ns / max(n, 1), n) for k, (ns, n) in acc.items()}
+
+
+def cal_key(name):
+    """Calibration kernels keep their template argument (gather<double> vs gather<float>)."""
+    n = name.split("(")[0].replace("void ", "").strip()
+    return n
 
 
 def workload_requests(w, tag):
@@ -143,17 +153,14 @@ def calibration_requests():
     tr = os.path.join(OUT, "rp_trace_cal", "run_kernel_stats.csv")
     if not all(os.path.exists(p) for p in paths.values()) or not os.path.exists(tr):
         return None
-    dur = trace_avg_ns(tr)
+    dur = trace_avg_ns(tr, cal_key)
     out = {}
     for c, p in paths.items():
         for name, (v, n) in load_count(p).items():
-            k = short(name)
-            if "<" in name:  # gather<double> / gather<float> ...: keep the element type
-                k = name.split("(")[0].replace("void ", "")
-            e = out.setdefault(k, {"dispatches": n})
+            e = out.setdefault(cal_key(name), {"dispatches": n})
             e[c + "_per_dispatch"] = v / max(n, 1)
     for k, e in out.items():
-        d = dur.get(short(k))
+        d = dur.get(k)
         if d:
             e["avg_ns"] = d[0]
             e["requests_per_s"] = (e.get("TCC_EA0_RDREQ_sum_per_dispatch", 0) + e.get("TCC_EA0_WRREQ_sum_per_dispatch", 0)) \
