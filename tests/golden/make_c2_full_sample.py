@@ -14,6 +14,7 @@ light-table rescan is O(rounds x constraints), maxmin.cpp:663-680).  The fixture
   * `oracle_rounds`, `oracle_seconds`: the oracle's sequential round count and solve time.
 
 Run from the repo root (CPU only, ~30 GB of host memory at peak):  python tests/golden/make_c2_full_sample.py
+(--stress: the stress variant, tests/golden/c2_stress_full_sample.npz)
 
 Round 4 changed the flattened system's constraint rule (System::flatten_maxmin: every listed constraint a
 member lies on is flattened, whatever its bound; the ~1000 zero-bound constraints of C2 start dead in the
@@ -36,6 +37,13 @@ NC, NV, K, SEED = 1_000_000, 10_000_000, 8, 1
 NSAMPLE = 100_000
 SAMPLE_SEED = 20261017
 OUT = os.path.join(ROOT, "tests", "golden", "c2_full_sample.npz")
+# --stress: the C2 stress variant (bench.py --variant stress: 5 % FATPIPE constraints, 10 % bounded variables,
+# penalties {1, 2, 4}) into c2_stress_full_sample.npz (round 5)
+STRESS_KW = dict(penalty_mix=1, bounded_permille=100, fatpipe_permille=50)
+GEN_KW = {}
+if "--stress" in sys.argv:
+    GEN_KW = STRESS_KW
+    OUT = os.path.join(ROOT, "tests", "golden", "c2_stress_full_sample.npz")
 
 
 def flat_sha256(f):
@@ -112,7 +120,7 @@ def main():
     O.set_precision(1e-5)
     t0 = time.time()
     ps = L.System(False)
-    pv = ps.gen_synthetic(NC, NV, K, seed=SEED)
+    pv = ps.gen_synthetic(NC, NV, K, seed=SEED, **GEN_KW)
     f = M.export_flat(ps)
     assert len(f.penalty) == NV and np.array_equal(f.var_ids, pv), "flat order must be generation order"
     sha = flat_sha256(f)
@@ -120,7 +128,7 @@ def main():
     del ps
 
     os_ = O.System(False)
-    vs = os_.gen_synthetic(NC, NV, K, seed=SEED)
+    vs = os_.gen_synthetic(NC, NV, K, seed=SEED, **GEN_KW)
     t1 = time.time()
     secs = os_.timed_solve()
     rounds = os_.last_rounds
