@@ -356,6 +356,8 @@ __global__ void __launch_bounds__(kBlock) fbr_unperm(Dev s, const double* __rest
 // fb_var_inc.
 // Shared constraints shorter than `longmin` elements take their increments in fbk_update_seq itself (fb_chain_pull);
 // only the long ones, whose chains are the round's critical path, get them precomputed here.
+// (streammin <= longmin, LMMHIP_FB_STREAM: shared constraints from this length on get their increments here too, and
+// their wave streams them in fbk_update_seq — fb_chain — instead of pulling mu itself)
 __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int all, uint32_t longmin) {  // all: round 0, every variable listed
   if (s.ctl[CTL_DONE])
     return;
@@ -843,7 +845,7 @@ __device__ void fb_long_chain(const Dev& s, int32_t c, double prec, double* sh) 
 // workgroup each (fb_long_chain, from fbk_acc's increments in fbd); the others one wave per listed constraint:
 // shorter shared ones through fb_chain_pull, FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0
 // erases the constraint (:129).
-__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin) {
+__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin, uint32_t streammin) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
@@ -878,6 +880,8 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uin
       rem = fb_fat_update(s, c, rem, s.xmin[c], prec, &u);
       if (lane == 0)
         s.use[c] = u;
+    } else if (ce - cb >= streammin) {  // increments written by fbk_acc (LMMHIP_FB_STREAM)
+      rem = fb_chain(s.fbd, cb, ce, rem, prec, d, lane);
     } else {
       rem = fb_chain_pull(s, cb, ce, rem, prec, d, lane);
     }

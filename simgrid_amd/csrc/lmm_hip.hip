@@ -123,6 +123,7 @@ struct lmmhip_ctx {
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
   int64_t fb_round = 0;
   uint32_t fb_longmin = 0;  // solve_fair: shared constraints with >= this many elements use fbk_acc's increments
+  uint32_t fb_streammin = 1u << 30;  // solve_fair: ... and from this length on their waves stream them (fb_chain)
   double fb_prec = 0;
   bool fb_shard = false;
   FbOwner fbo{};                   // sharded solve: the owned constraints (lmmhip_fb_shard_owner)
@@ -2114,7 +2115,7 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
       LAUNCH(3, r, fbo_put_mu, gV, kBlock, d, c->fbo);
       break;
     }
-    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(r == 0), c->fb_longmin);
+    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(r == 0), std::min(c->fb_longmin, c->fb_streammin));
     LAUNCH(4, r, fbk_accc, gC, kBlock, d);
     break;
   case 2:
@@ -2125,7 +2126,7 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
     }
     // one context: element by element in the CSC order, bit-identical to the reference
     LAUNCH(5, r, fbk_update_seq, kLongBlocks + grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec,
-           c->fb_longmin);
+           c->fb_longmin, std::min(c->fb_longmin, c->fb_streammin));
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d, int(r > 0));  // (vstb is packed in rounds > 0)
     c->fb_round++;
     break;
@@ -2244,6 +2245,9 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   // (fb_chain_pull).  Pulling in round 0 and streaming fbk_acc's listed-variable rewrites afterwards measured
   // 3 % slower on C5 (9.68 vs 9.42 ms, same box): the increments' gathers move, they do not go away.
   c->fb_longmin = uint32_t(std::max(0, env_int("LMMHIP_FB_LONG", 16384)));
+  // shared constraints of at least this many elements (below longmin) stream fbk_acc's increments in their wave
+  // instead of gathering mu in the chain (LMMHIP_FB_STREAM, A/B knob; default: none)
+  c->fb_streammin = uint32_t(std::max(0, env_int("LMMHIP_FB_STREAM", 1 << 30)));
   if (c->fbd_cap < c->d.nnz) {  // increments in CSC order (fbk_acc -> fbk_update_seq)
     if (int rc = dalloc(c, &c->d.fbd, c->d.nnz))
       return rc;

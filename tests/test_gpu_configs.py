@@ -147,9 +147,11 @@ def c5_1e6_oracle():
 
 # LMMHIP_FB_LONG: shared constraints with at least this many elements chain increments precomputed by fbk_acc,
 # shorter ones compute them inside the chain (fb_chain_pull); the C5 1e6 system's longest holds ~1.6e4
-@pytest.mark.parametrize("longmin", ["default", "0", "4096", "1000000000"])
+@pytest.mark.parametrize("longmin", ["default", "0", "4096", "1000000000", "stream256", "stream4096"])
 def test_c5_1e6_flows_vs_oracle(c5_1e6_oracle, longmin, monkeypatch):
-    if longmin != "default":
+    if longmin.startswith("stream"):  # (LMMHIP_FB_STREAM: shorter shared constraints stream fbk_acc's increments)
+        monkeypatch.setenv("LMMHIP_FB_STREAM", longmin[6:])
+    elif longmin != "default":
         monkeypatch.setenv("LMMHIP_FB_LONG", longmin)
     p, y = c5_1e6_oracle
     s = L.System(False, L.System.FAIR_BOTTLENECK)
