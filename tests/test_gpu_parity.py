@@ -327,21 +327,27 @@ def test_c_client_drives_a_solve():
 
 @pytest.mark.slow
 @pytest.mark.timeout(600)
-def test_synthetic_full_size_vs_oracle_sample():
+@pytest.mark.parametrize("variant", ["plain", "stress"])
+def test_synthetic_full_size_vs_oracle_sample(variant):
     """C2 at FULL size (1e6 x 1e7 x 8, seed 1) against the oracle's own solve of the same system, made once in
-    the build container (tests/golden/make_c2_full_sample.py; ~45 min of the O(rounds x constraints) reference
-    loop, maxmin.cpp:560-680): a fixed random sample of 1e5 variables within K.ABS_TOL / K.REL_TOL, and the
-    saturated-constraint set (maxmin.cpp print()'s test over every constraint) identical bit for bit."""
+    the build container (tests/golden/make_c2_full_sample.py; the O(rounds x constraints) reference loop,
+    maxmin.cpp:560-680): a fixed random sample of 1e5 variables within K.ABS_TOL / K.REL_TOL, and the
+    saturated-constraint set (maxmin.cpp print()'s test over every constraint) identical bit for bit.
+    `stress`: the bench's --variant stress system (5 % FATPIPE constraints, 10 % bounded variables, penalties
+    {1, 2, 4}; make_c2_full_sample.py --stress)."""
     import os
 
     from simgrid_amd import multi as M
+    from tests.golden.make_c2_full_sample import STRESS_KW, flat_sha256, saturated_bits
 
-    path = os.path.join(os.path.dirname(__file__), "golden", "c2_full_sample.npz")
+    name = "c2_full_sample.npz" if variant == "plain" else "c2_stress_full_sample.npz"
+    path = os.path.join(os.path.dirname(__file__), "golden", name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not generated (tests/golden/make_c2_full_sample.py)")
     fx = np.load(path)
     s = L.System(False)
-    vids = s.gen_synthetic(1_000_000, 10_000_000, 8, seed=1)
+    vids = s.gen_synthetic(1_000_000, 10_000_000, 8, seed=1, **(STRESS_KW if variant == "stress" else {}))
     f = M.export_flat(s)
-    from tests.golden.make_c2_full_sample import flat_sha256, saturated_bits
     assert flat_sha256(f) == str(fx["csr_sha256"]), "not the system the oracle solved"
     assert np.array_equal(f.var_ids, vids)
     s.solve()
