@@ -475,19 +475,34 @@ def link_new(sys, model, bw, fatpipe=False):
     return c
 
 
+def wifi_link_new(sys, model):
+    """NetworkWifiLink's constraint (network_cm02.cpp:383-392): a NetworkCm02Link of bandwidth 1 / bandwidth
+    factor, hence bound bandwidth factor * (1 / bandwidth factor); shared."""
+    bf = net_factors(model)[1]
+    return sys.constraint_new(None, bf * (1.0 / bf))
+
+
 def communicate(sys, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False):
     """NetworkCm02Model::communicate (network_cm02.cpp:165-274), its LMM part, on an oracle System:
-    route = [(constraint, bw, lat)] in route order (route_to sums the latencies), back = the back route's
-    constraints (crosstraffic, weight 0.05).  Returns (variable, dict(latency, lat_current, sharing_penalty,
-    bound)); the variable has penalty 0 while the latency is unpaid (1.0 without latency), or with `paid`
-    the sharing penalty update_actions_state restores (network_cm02.cpp:105-146)."""
-    lat_factor, _, weight_s = net_factors(model)
+    route = [(constraint, bw, lat)] in route order (route_to sums the latencies) — a WIFI access point as
+    (constraint, bw, lat, (src_rate, dst_rate)), the stations' NetworkWifiLink::get_host_rate (-1: not
+    associated), whose own bandwidth 1 / bandwidth factor and latency 0 replace bw / lat —, back = the back
+    route's constraints (crosstraffic, weight 0.05).  Returns (variable, dict(latency, lat_current,
+    sharing_penalty, bound)); the variable has penalty 0 while the latency is unpaid (1.0 without latency), or
+    with `paid` the sharing penalty update_actions_state restores (network_cm02.cpp:105-146)."""
+    lat_factor, bf, weight_s = net_factors(model)
+    links = []
+    for r in route:
+        if len(r) > 3:  # WIFI: LinkImpl::get_bandwidth of the NetworkWifiLink, latency 0 (network_cm02.cpp:386)
+            links.append((r[0], 1.0 / bf, 0.0, r[3]))
+        else:
+            links.append((r[0], r[1], r[2], None))
     lat = 0.0
-    for _, _, l in route:
+    for _, _, l, _ in links:
         lat += l
     sharing_penalty = lat  # action->sharing_penalty_ = latency (network_cm02.cpp:188)
     if weight_s > 0:      # std::accumulate over the route (network_cm02.cpp:196-201)
-        for _, bw, _ in route:
+        for _, bw, _, _ in links:
             sharing_penalty = sharing_penalty + weight_s / bw
     lat_current = lat
     latency = lat * lat_factor  # latency_ *= get_latency_factor(size) (network_cm02.cpp:208-209)
@@ -495,11 +510,23 @@ def communicate(sys, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid
         bound = tcp_gamma / (2.0 * lat_current) if lat_current > 0 else -1.0
     else:
         bound = min(rate, tcp_gamma / (2.0 * lat_current)) if lat_current > 0 else rate
+    for _, _, _, rates in links:  # the assertions of network_cm02.cpp:242-255
+        if rates is not None:
+            if len(back):
+                raise ValueError("Cross-traffic is not yet supported when using WIFI")
+            if rates[0] == -1 and rates[1] == -1:
+                raise ValueError("Some Stations are not associated to any Access Point")
     pen = (sharing_penalty if paid else 0.0) if latency > 0 else 1.0
-    v = sys.variable_new(None, pen, -1.0, len(route) + len(back))
+    v = sys.variable_new(None, pen, -1.0, len(links) + len(back))
     sys.update_variable_bound(v, bound)
-    for c, _, _ in route:
-        sys.expand(c, v, 1.0)
+    for c, _, _, rates in links:  # network_cm02.cpp:239-264
+        if rates is None:
+            w = 1.0
+        elif rates[0] != -1:  # (src and dst on one access point: the source's rate, :249-251)
+            w = 1.0 / rates[0]
+        else:
+            w = 1.0 / rates[1]
+        sys.expand(c, v, w)
     for c in back:
         sys.expand(c, v, 0.05)
     return v, dict(latency=latency, lat_current=lat_current, sharing_penalty=sharing_penalty, bound=bound)

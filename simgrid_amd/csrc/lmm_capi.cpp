@@ -494,9 +494,21 @@ int64_t lmm_link_new(lmm_sys* s, int model, double bw, int fatpipe) {
   }
 }
 
-int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
-                        const double* route_lat, int64_t n_back, const int64_t* back_cnst, double rate,
-                        double tcp_gamma, int paid, lmm_comm_info* out) {
+int64_t lmm_wifi_link_new(lmm_sys* s, int model) {
+  try {
+    if (!s)
+      throw std::invalid_argument("null system");
+    Builder b{&s->sys};
+    return lmm_plat::wifi_link_constraint(b, model);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst,
+                           const double* route_bw, const double* route_lat, const double* route_rates, int64_t n_back,
+                           const int64_t* back_cnst, double rate, double tcp_gamma, int paid, lmm_comm_info* out) {
   try {
     if (!s || n_route < 0 || n_back < 0 || (n_route && (!route_cnst || !route_bw || !route_lat)) ||
         (n_back && !back_cnst))
@@ -509,10 +521,17 @@ int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const 
     for (int64_t i = 0; i < n_route; i++) {
       if (!cnst_ok(s, route_cnst[i]))
         throw std::invalid_argument("lmm_communicate: bad route constraint");
-      links.push_back({route_bw[i], route_lat[i], false});
+      lmm_plat::Link k{route_bw[i], route_lat[i], false};
+      if (route_rates && (route_rates[2 * i] != 0.0 || route_rates[2 * i + 1] != 0.0)) {
+        k.wifi = true;  // a WIFI access point: its own bandwidth (1 / bandwidth factor) and latency (0)
+        k.lat = 0.0;
+        k.src_rate = route_rates[2 * i];
+        k.dst_rate = route_rates[2 * i + 1];
+      }
+      links.push_back(k);
       cn.push_back(Id(route_cnst[i]));
       route.push_back(int(i));
-      lat += route_lat[i];
+      lat += k.lat;
     }
     for (int64_t i = 0; i < n_back; i++) {
       if (!cnst_ok(s, back_cnst[i]))
@@ -533,6 +552,13 @@ int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const 
     g_err = ex.what();
     return -1;
   }
+}
+
+int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
+                        const double* route_lat, int64_t n_back, const int64_t* back_cnst, double rate,
+                        double tcp_gamma, int paid, lmm_comm_info* out) {
+  return lmm_communicate_ex(s, id, model, n_route, route_cnst, route_bw, route_lat, nullptr, n_back, back_cnst, rate,
+                            tcp_gamma, paid, out);
 }
 
 }  // extern "C"

@@ -83,6 +83,10 @@ Params params_from(const C& c) {
 struct Link {
   double bw, lat;
   bool fatpipe;
+  // WIFI access point (NetworkWifiLink, network_cm02.cpp:383-420): the rates of the flow's source and destination
+  // stations on it (get_host_rate: -1 = not associated); bw / lat are then the link's own (1 / bandwidth factor, 0)
+  bool wifi = false;
+  double src_rate = -1.0, dst_rate = -1.0;
 };
 
 inline std::vector<std::string> split(const std::string& s, char sep) {
@@ -514,12 +518,25 @@ typename B::Cnst link_constraint(B& b, int model, double bw, bool fatpipe) {
   return c;
 }
 
+// A WIFI access point's constraint (NetworkWifiLink, network_cm02.cpp:383-392): a shared link of bandwidth
+// 1 / bandwidth factor, so that its bound is bandwidth factor * (1 / bandwidth factor) — 1 up to that rounding;
+// a station's flow then takes 1 / rate of it per unit of rate (communicate).
+template <class B>
+typename B::Cnst wifi_link_constraint(B& b, int model) {
+  const double bf = net_factors(model).bandwidth;
+  return b.constraint_new(bf * (1.0 / bf));
+}
+
 // One communication, NetworkCm02Model::communicate (network_cm02.cpp:165-274): the action's latency (after the
 // latency factor), its sharing penalty (the route latency + weight_S / bw per route link, in route order), the
 // bound (rate < 0: TCP-gamma / (2 * route latency); else min(rate, that)), the variable — penalty 0 while the
 // latency is unpaid (1 without latency), or, `paid`, the state once it is paid (update_actions_state restores
 // the sharing penalty: network_cm02.cpp:105-146) — and its elements: each route link at 1.0, with
-// crosstraffic each back-route link at 0.05.  route / back: indices into `links` and `cn`.
+// crosstraffic each back-route link at 0.05.  route / back: indices into `links` and `cn`.  A WIFI route link
+// (network_cm02.cpp:239-260) weighs 1 / the source station's rate, or the destination's when the source is not
+// associated with that access point (neither associated: error); its bandwidth in the weight_S sum is the link's own,
+// 1 / bandwidth factor (LinkImpl::get_bandwidth of the NetworkWifiLink).  WIFI with crosstraffic (a back route) is
+// the reference's assertion "Cross-traffic is not yet supported when using WIFI": an error here too.
 struct Comm {
   double latency;          // NetworkAction::latency_ (route latency * latency factor)
   double lat_current;      // lat_current_ (route latency)
@@ -535,8 +552,21 @@ typename B::Var communicate(B& b, int model, const std::vector<Link>& links, con
   a.sharing_penalty = lat;
   a.lat_current = lat;
   if (f.weight_s > 0)
-    for (int l : route)
-      a.sharing_penalty += f.weight_s / links[size_t(l)].bw;
+    for (int l : route) {
+      const Link& k = links[size_t(l)];
+      a.sharing_penalty += f.weight_s / (k.wifi ? 1.0 / f.bandwidth : k.bw);
+    }
+  for (int l : route) {
+    const Link& k = links[size_t(l)];
+    if (!k.wifi)
+      continue;
+    if (!back.empty())
+      throw std::invalid_argument(
+          "Cross-traffic is not yet supported when using WIFI. Please use --cfg=network/crosstraffic:0");
+    if (k.src_rate == -1 && k.dst_rate == -1)
+      throw std::invalid_argument("Some Stations are not associated to any Access Point. Make sure to call "
+                                  "set_host_rate on all Stations.");
+  }
   a.latency = lat * f.latency;
   if (rate < 0)
     a.bound = a.lat_current > 0 ? tcp_gamma / (2.0 * a.lat_current) : -1.0;
@@ -544,8 +574,11 @@ typename B::Var communicate(B& b, int model, const std::vector<Link>& links, con
     a.bound = a.lat_current > 0 ? std::min(rate, tcp_gamma / (2.0 * a.lat_current)) : rate;
   const double pen = a.latency > 0 ? (paid ? a.sharing_penalty : 0.0) : 1.0;
   typename B::Var v = b.variable_new(pen, a.bound, int(route.size() + back.size()));
-  for (int l : route)
-    b.expand(cn[size_t(l)], v, 1.0);
+  for (int l : route) {
+    const Link& k = links[size_t(l)];
+    // (src and dst on one access point: the source's rate, network_cm02.cpp:249-251)
+    b.expand(cn[size_t(l)], v, !k.wifi ? 1.0 : k.src_rate != -1 ? 1.0 / k.src_rate : 1.0 / k.dst_rate);
+  }
   for (int l : back)
     b.expand(cn[size_t(l)], v, 0.05);
   if (out)

@@ -119,6 +119,8 @@ SIGNATURES = {
     "lmm_gen_platform_flows": (I64, [P, ct.POINTER(PlatformParams), PI64, PI64]),
     "lmm_link_new": (I64, [P, I, D, I]),
     "lmm_communicate": (I64, [P, P, I, I64, PI64, PD, PD, I64, PI64, D, D, I, P]),
+    "lmm_wifi_link_new": (I64, [P, I]),
+    "lmm_communicate_ex": (I64, [P, P, I, I64, PI64, PD, PD, PD, I64, PI64, D, D, I, P]),
     "lmm_device_count": (I, []),
     "lmm_last_error": (ct.c_char_p, []),
     # include/lmm/lmm_hip.h
@@ -672,20 +674,34 @@ class System:
             raise LmmError(lib().lmm_last_error().decode())
         return Constraint(self, h)
 
+    def wifi_link_new(self, model):
+        """A WIFI access point's constraint (lmm_wifi_link_new: NetworkWifiLink, bandwidth 1 / bandwidth factor)."""
+        h = lib().lmm_wifi_link_new(self.h, model)
+        if h < 0:
+            raise LmmError(lib().lmm_last_error().decode())
+        return Constraint(self, h)
+
     def communicate(self, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False, id_=None):
         """NetworkCm02Model::communicate's LMM part (lmm_communicate): route = [(Constraint, bw, lat)] in route
-        order, back = the back route's Constraints (crosstraffic), id_ = the variable's opaque id (an int: the
-        action; modified_action_ids() reports it).  Returns (Variable, dict(latency, lat_current, sharing_penalty,
-        bound))."""
+        order — a WIFI access point as (Constraint, bw, lat, (src_rate, dst_rate)), the stations' rates on it
+        (-1: not associated; lmm_communicate_ex) —, back = the back route's Constraints (crosstraffic), id_ = the
+        variable's opaque id (an int: the action; modified_action_ids() reports it).  Returns (Variable,
+        dict(latency, lat_current, sharing_penalty, bound))."""
         n = len(route)
-        rc = np.array([c.h for c, _, _ in route], dtype=np.int64)
-        rb = np.array([b for _, b, _ in route], dtype=np.float64)
-        rl = np.array([l for _, _, l in route], dtype=np.float64)
+        rc = np.array([r[0].h for r in route], dtype=np.int64)
+        rb = np.array([r[1] for r in route], dtype=np.float64)
+        rl = np.array([r[2] for r in route], dtype=np.float64)
         bc = np.array([c.h for c in back], dtype=np.int64)
         info = CommInfo()
-        h = lib().lmm_communicate(self.h, id_, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
-                                  rl.ctypes.data_as(PD), len(bc), bc.ctypes.data_as(PI64), rate, tcp_gamma,
-                                  int(paid), ct.byref(info))
+        if any(len(r) > 3 for r in route):
+            rr = np.array([r[3] if len(r) > 3 else (0.0, 0.0) for r in route], dtype=np.float64).reshape(-1)
+            h = lib().lmm_communicate_ex(self.h, id_, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
+                                         rl.ctypes.data_as(PD), rr.ctypes.data_as(PD), len(bc),
+                                         bc.ctypes.data_as(PI64), rate, tcp_gamma, int(paid), ct.byref(info))
+        else:
+            h = lib().lmm_communicate(self.h, id_, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
+                                      rl.ctypes.data_as(PD), len(bc), bc.ctypes.data_as(PI64), rate, tcp_gamma,
+                                      int(paid), ct.byref(info))
         if h < 0:
             raise LmmError(lib().lmm_last_error().decode())
         return Variable(self, h), {k: getattr(info, k) for k, _ in CommInfo._fields_}

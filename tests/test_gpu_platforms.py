@@ -43,3 +43,27 @@ def test_platform_flows_match_oracle(name, plat, model, kind, n):
     if kind == 0:
         excess, infeasible, unbottlenecked = s.check_certificate()
         assert infeasible == 0 and unbottlenecked == 0, (excess, infeasible, unbottlenecked)
+
+
+@pytest.mark.parametrize("model", [0, 1], ids=["cm02", "lv08"])
+def test_wifi_flows_device_match_oracle(model):
+    """WIFI access points (lmm_wifi_link_new / lmm_communicate_ex, network_cm02.cpp:239-260, 383-420): the HIP
+    solve of tests/test_wifi.py's two-AP system equals the oracle's, and stations alone on an AP get the closed
+    form 1 / Σ 1/r_i (the slowest station sets everyone's rate)."""
+    from tests.test_wifi import build_wifi
+
+    s, o = L.System(False), O.System(False)
+    (pv, _), (ov, _) = build_wifi(s, "product", model), build_wifi(o, "oracle", model)
+    s.solve()
+    o.solve()
+    got, want = np.array([v.get_value() for v in pv]), np.array([v.get_value() for v in ov])
+    tol = np.maximum(ABS_TOL, REL_TOL * np.abs(want))
+    assert np.all(np.abs(got - want) <= tol), (got, want)
+    assert np.all(want > 0)
+    s1 = L.System(False)
+    ap = s1.wifi_link_new(model)
+    vs = [s1.communicate(model, [(ap, 0.0, 0.0, (r, -1.0))], paid=True)[0] for r in (54e6, 54e6, 6e6)]
+    s1.solve()
+    bf = 0.97 if model == 1 else 1.0
+    for v in vs:
+        assert v.get_value() == pytest.approx(bf * (1.0 / bf) / (2 / 54e6 + 1 / 6e6), rel=1e-9)
