@@ -291,16 +291,10 @@ __global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
 
 // Rounds >= 1: the variables fr_update queued in workgroup b's segment (the CSC range of its constraints).
 // Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
-template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
-  if (s.ctl[CTL_DONE])
-    return;
-  if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-      s.ctl[CTL_DONE] = 1;
-    return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_PALIVE0 + (round & 1)] = 0;  // this round's fr_update raises it
+// fr_vote_blk: the work of (virtual) workgroup vb — also run by the persistent frontier kernel (fr_persist), whose
+// workgroups loop over the virtual ones; the queue counts are read relaxed (written in the same launch there).
+template <bool kEarly, int R>
+__device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, int64_t vb) {
   // spb (<= kFVS) consecutive segments per workgroup: on C2 ~170 queued rows, one pass, and the launch's
   // workgroups resident at once; small systems keep one segment per workgroup (more workgroups)
   const int64_t nseg = (int64_t(s.nC) + kFB - 1) / kFB;
@@ -309,8 +303,8 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
   pre[0] = 0;
 #pragma unroll
   for (int k = 0; k < kFVS; k++) {
-    const int64_t sg = int64_t(blockIdx.x) * spb + k;
-    n[k] = k < spb && sg < nseg ? s.fq_n[sg] : 0;
+    const int64_t sg = vb * spb + k;
+    n[k] = k < spb && sg < nseg ? ld_rlx(&s.fq_n[sg]) : 0;
     seg[k] = k < spb && sg < nseg ? s.cnst_ptr[sg * kFB] : 0u;
     pre[k + 1] = pre[k] + n[k];
   }
@@ -329,6 +323,19 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
       fr_diag(s, round, 7, o == FR_BOUND);
     }
   }
+}
+
+template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
+  if (s.ctl[CTL_DONE])
+    return;
+  if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      s.ctl[CTL_DONE] = 1;
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    s.ctl[CTL_PALIVE0 + (round & 1)] = 0;  // this round's fr_update raises it
+  fr_vote_blk<kEarly, R>(s, round, spb, blockIdx.x);
 }
 
 // Saturation of one 64-element CSC chunk of ready constraint c: saturate_chunk's decisions and arithmetic
@@ -467,13 +474,11 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 // (fr_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
 constexpr int kFS = 1024;
 
-template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
-  if (s.ctl[CTL_DONE])
-    return;
-  __shared__ SatLds<kFS, kFS> L;
-  constexpr int NBW = kFS / kWave;
+template <int NB, bool kOld>
+__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int64_t vb, SatLds<NB, NB>& L) {
+  constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  const int64_t c = int64_t(blockIdx.x) * kFS + threadIdx.x;
+  const int64_t c = vb * NB + threadIdx.x;
   bool rdy = false;
   int nch = 0;
   if (c < s.nC && s.key32[c] != kDead32 && s.nvote[c] == 0) {
@@ -521,11 +526,35 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
   }
   __syncthreads();
   if (ta)  // workgroup-uniform
-    fr_flush<kFS, kOld>(s, round, L);
+    fr_flush<NB, kOld>(s, round, L);
+}
+
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ SatLds<kFS, kFS> L;
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
 }
 
 // The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
 // constraint over the whole grid, wave k taking chunks k, k + kFrBigWaves, ...
+// (the grid's waves over the list: wave / nwaves; wpre = the calling wave's 64-int LDS scratch)
+__device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bigw, int nb, int64_t wave,
+                                                 int64_t nwaves, int* wpre) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int64_t g = wave; g < int64_t(nb) * bigw; g += nwaves) {
+    const int32_t c = ld_rlx(&s.ready[g / bigw]);
+    const int k = int(g % bigw);
+    const double r = ld_rlx(&s.cst[c].ratio);
+    const uint32_t ce = s.cnst_ptr[c + 1];
+    const bool dup = s.cdup[c] != 0;
+    for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
+      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup);
+    if (k == 0 && lane == 0)
+      s.ctouch[c] = 2;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round, int bigw) {
   if (s.ctl[CTL_DONE])
     return;
@@ -535,20 +564,10 @@ __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round, int bigw)
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;
   __shared__ int wpre[kBlock / kWave][kWave];
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int w = threadIdx.x / kWave;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  for (int64_t g = wave; g < int64_t(nb) * bigw; g += nwaves) {
-    const int32_t c = s.ready[g / bigw];
-    const int k = int(g % bigw);
-    const double r = ld_rlx(&s.cst[c].ratio);
-    const uint32_t ce = s.cnst_ptr[c + 1];
-    const bool dup = s.cdup[c] != 0;
-    for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
-      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre[w], dup);
-    if (k == 0 && lane == 0)
-      s.ctouch[c] = 2;
-  }
+  fr_sat_big_waves(s, round, bigw, nb, wave, nwaves, wpre[w]);
 }
 
 // Constraint update (maxmin.cpp:603-658; the arithmetic of update_groups) + slot scan.  Workgroup b owns
@@ -562,20 +581,24 @@ __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round, int bigw)
 // the stores of the new state, the queue and the cleared slots.
 constexpr int kFrScanU = 8;
 
-__global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) {
-  if (s.ctl[CTL_DONE])
-    return;
-  __shared__ int qn;
-  __shared__ int pre[kFB / kWave][kWave];
-  __shared__ uint32_t mf[kFB];
+struct FrUpdLds {
+  int qn;
+  int pre[kFB / kWave][kWave];
+  uint32_t mf[kFB];
+};
+
+__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int64_t vb, FrUpdLds& U) {
+  int& qn = U.qn;
+  auto& pre = U.pre;
+  uint32_t* mf = U.mf;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   if (threadIdx.x == 0)
     qn = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (vb == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ROUNDS] += 1;
-    s.ctl[CTL_NREADY] = 0;  // fr_sat_big's list of the next round
+    st_rlx(&s.ctl[CTL_NREADY], 0);  // fr_sat_big's list of the next round (its adds are atomics: no cached copy)
   }
-  const int64_t gbase = int64_t(blockIdx.x) * kFB + int64_t(w) * kWave;
+  const int64_t gbase = vb * kFB + int64_t(w) * kWave;
   const int64_t c = gbase + lane;
   const bool in = c < s.nC;
   const uint32_t okey = in ? s.key32[c] : kDead32;
@@ -670,7 +693,7 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
   pre[w][lane] = incl - len;
   mf[threadIdx.x] = kNoVoter;
   __syncthreads();  // (qn, pre, mf)
-  const uint32_t seg = s.cnst_ptr[int64_t(blockIdx.x) * kFB];
+  const uint32_t seg = s.cnst_ptr[vb * kFB];
   for (int f0 = 0; f0 < total; f0 += kFrScanU * kWave) {  // wave-uniform (one pass up to 512 slots)
     int ol[kFrScanU];
     uint32_t jj[kFrScanU];
@@ -741,12 +764,19 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
     s.minfl[c] = mf[threadIdx.x];
   const bool any_alive = __syncthreads_or(alive);
   if (threadIdx.x == 0) {
-    s.fq_n[blockIdx.x] = qn;
+    s.fq_n[vb] = qn;
     if (any_alive)
-      s.ctl[CTL_PALIVE0 + (round & 1)] = 1;
+      st_rlx(&s.ctl[CTL_PALIVE0 + (round & 1)], 1);
   }
   if (__syncthreads_or(tch || sat) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
+}
+
+__global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) {
+  if (s.ctl[CTL_DONE])
+    return;
+  __shared__ FrUpdLds U;
+  fr_update_blk(s, round, prec, blockIdx.x, U);
 }
 
 }  // namespace lmmdev

@@ -24,6 +24,7 @@
 #include "lmm_maxmin_kernels.hpp"
 #include "lmm_persist_kernels.hpp"
 #include "lmm_frontier_kernels.hpp"
+#include "lmm_frontier_persist.hpp"
 #include "lmm_batch_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
 #include "lmm_cc_kernels.hpp"
@@ -1766,6 +1767,79 @@ static int solve_tail(lmmhip_ctx* c, double prec, int64_t nh) {
 // Frontier engine (lmm_frontier_kernels.hpp): three launches per round, work proportional to the touched
 // constraints and the moving votes.  Slots: 2 fr_vote, 4 fr_sat (+ fr_sat_big), 5 fr_update, 6 the per-chunk
 // control-word copy; 0 / 1 init.
+// The frontier engine's rounds in one persistent launch (lmm_frontier_persist.hpp, LMMHIP_FR_PERSIST), queued
+// after round 0's vote: serialised per device with the other persistent launches (g_persist_mu), the same launch
+// rendezvous with a deadline.  *closed: the rendezvous closed — nothing of the launch ran, the caller continues
+// with the multi-launch rounds from round 0's saturation.  A grid-barrier timeout (CTL_ERR 1) is returned as
+// LMMHIP_E_HIP with CTL_ERR left at 1: the caller re-runs the whole solve.
+static int frontier_persist_launch(lmmhip_ctx* c, const Dev& d, double prec, int spb, int bigch, int bigw, bool big,
+                                   bool long_rows, bool* closed) {
+  const void* kern = long_rows ? reinterpret_cast<const void*>(&fr_persist<16>)
+                               : reinterpret_cast<const void*>(&fr_persist<8>);
+  if (!c->pbar)
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->pbar), BAR_WORDS * sizeof(unsigned)));
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kFB, 0));
+  if (per_cu < 1)
+    return fail(LMMHIP_E_HIP, "persistent frontier kernel: no workgroup fits a CU (occupancy query)");
+  const int64_t nblk = (int64_t(d.nC) + kFB - 1) / kFB;
+  // workgroups: one per CU at most (the grid barriers' cost grows with the arrivals), no more than the
+  // multi-launch grid's workgroups (LMMHIP_FRP_GRID, A/B knob)
+  int grid = int(std::min<int64_t>(std::max<int64_t>(1, nblk), c->n_cu));
+  grid = std::max(1, std::min(env_int("LMMHIP_FRP_GRID", grid), c->n_cu * per_cu));
+  const int max_rounds = int(std::min<int64_t>(int64_t(d.nV) + 2, INT32_MAX - 1));
+  long long rdv_ticks = 100000LL * env_int("LMMHIP_PERSIST_RDV_MS", 20);  // 100 MHz wall clock
+  int32_t* hflag = c->d_rdv;
+  unsigned* barw = c->pbar;
+  Dev dd = d;
+  int ibig = big ? 1 : 0;
+  void* args[] = {&dd, &barw, &prec, const_cast<int*>(&max_rounds), &spb, &bigch, &bigw, &ibig, &rdv_ticks, &hflag};
+  {
+    std::lock_guard<std::mutex> lk(g_persist_mu);
+    hipEvent_t& last = g_persist_last[c->device];
+    if (last && hipStreamWaitEvent(c->stream, last, 0) != hipSuccess) {  // (a stale event: make a new one)
+      (void)hipGetLastError();
+      (void)hipEventDestroy(last);
+      last = nullptr;
+    }
+    if (!last)
+      HIPCHK(hipEventCreateWithFlags(&last, hipEventDisableTiming));
+    HIPCHK(hipMemsetAsync(c->pbar, 0, BAR_WORDS * sizeof(unsigned), c->stream));
+    __atomic_store_n(c->h_rdv, 0, __ATOMIC_RELEASE);
+    HIPCHK(hipLaunchKernel(kern, dim3(grid), dim3(kFB), args, 0, c->stream));
+    HIPCHK(hipEventRecord(last, c->stream));
+  }
+  c->stats.kernel_launches[2] += 1;
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->ev1_done = true;
+  for (;;) {  // the launch, or its rendezvous closing (the mapped word), whichever comes first
+    const hipError_t q = hipEventQuery(c->ev1);
+    if (q == hipSuccess)
+      break;
+    if (q != hipErrorNotReady)
+      HIPCHK(q);
+    if (__atomic_load_n(c->h_rdv, __ATOMIC_ACQUIRE)) {
+      *closed = true;
+      c->ev1_done = false;
+      if (c->stream == c->own_stream) {  // (as solve_maxmin_persist_once: off the closed launch's stream)
+        hipStream_t ns = nullptr;
+        HIPCHK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+        c->retired_streams.push_back(c->own_stream);
+        c->own_stream = c->stream = ns;
+      }
+      return 0;
+    }
+    std::this_thread::yield();
+  }
+  if (int rc = poll_ctl(c))
+    return rc;
+  if (c->h_ctl[CTL_ERR] == 1)
+    return fail(LMMHIP_E_HIP, "persistent frontier kernel: a grid-barrier wait timed out");
+  if (c->h_ctl[CTL_ERR] == 2)
+    return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
+  return 0;
+}
+
 static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   Dev d = c->d;  // (a copy: the frontier's buffers stay out of the context's Dev, which the other engines use)
   if (!c->vote_diag)  // per-round diagnostic counters only on request (LMMHIP_VOTE_DIAG): they cost atomics
@@ -1839,11 +1913,41 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   for (int k = 0; k < 2; k++)
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
   const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
+  // the rounds in one persistent launch (LMMHIP_FR_PERSIST; not under profiling or the per-round diagnostics,
+  // which time / count per launch; not during a fallback's cooldown)
+  bool vote0 = false;
+  int frp = env_int("LMMHIP_FR_PERSIST", 0);
+  if (c->profiling || d.vstat || sat_old || mf_early)
+    frp = 0;
+  if (frp && c->persist_cool > 0) {
+    c->persist_cool -= 1;
+    frp = 0;
+  }
+  if (frp) {
+    LAUNCH(2, 0, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
+    LAUNCH(2, 0, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
+    vote0 = true;
+    c->h_ctl[CTL_ERR] = 0;
+    bool closed = false;
+    const int prc = frontier_persist_launch(c, d, prec, spb, bigch, bigw, big, long_rows, &closed);
+    if (!closed && (prc != LMMHIP_E_HIP || c->h_ctl[CTL_ERR] != 1))
+      return prc;
+    c->persist_fallbacks += 1;
+    c->persist_cool = env_int("LMMHIP_PERSIST_COOLDOWN", 64);
+    if (!closed) {  // a barrier timed out mid-solve: the whole solve again, multi-launch (cooldown)
+      HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+      c->ev1_done = false;
+      return solve_maxmin_frontier(c, prec);
+    }
+    // closed before any store: the multi-launch rounds below continue from round 0's saturation
+  }
   for (;;) {
     for (int k = 0; k < chunk; k++, r++) {
       if (r == 0) {
-        LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
-        LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
+        if (!vote0) {
+          LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
+          LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
+        }
       } else if (long_rows) {  // (LV08 routes: ~12 elements per row)
         LAUNCH(2, r, (fr_vote<false, 16>), (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       } else if (mf_early) {

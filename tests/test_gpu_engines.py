@@ -77,6 +77,40 @@ def test_frontier_engine_bit_identical(name):
     assert xf.tobytes() == xr.tobytes(), float(np.max(np.abs(xf - xr)))
 
 
+def _launches(s):
+    """Per-slot kernel launches of the last solve (lmmhip_stats.kernel_launches: 2 vote / persistent, 4 saturation,
+    5 update)."""
+    import ctypes as ct
+
+    st = L.LmmhipStats()
+    assert L.lib().lmmhip_get_stats(s.device_ctx(), ct.byref(st)) == 0
+    return list(st.kernel_launches)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("grid", ["auto", "7"])
+def test_frontier_persistent_bit_identical(name, grid, monkeypatch):
+    """The frontier engine's rounds in one persistent launch (lmm_frontier_persist.hpp, LMMHIP_FR_PERSIST=1; with
+    the default grid and with 7 workgroups, each then looping over many of the multi-launch grid's): the same
+    values bit for bit and the same rounds as the multi-launch frontier and round engines, and no per-round
+    saturation / update launch."""
+    monkeypatch.setenv("LMMHIP_FR_PERSIST", "1")
+    if grid != "auto":
+        monkeypatch.setenv("LMMHIP_FRP_GRID", grid)
+    s = L.System(False)
+    ids = CASES[name](s)
+    s.set_engine(L.System.ENGINE_FRONTIER)
+    s.solve()
+    xp, rp, lp = s.values_of(ids), s.last_stats()["rounds"], _launches(s)
+    assert s.engine_fallbacks() == 0
+    assert lp[4] == 0 and lp[5] == 0, lp
+    monkeypatch.delenv("LMMHIP_FR_PERSIST")
+    xf, rf = _values(CASES[name], L.System.ENGINE_FRONTIER)
+    xr, rr = _values(CASES[name], L.System.ENGINE_ROUNDS)
+    assert rp == rf == rr
+    assert xp.tobytes() == xf.tobytes() == xr.tobytes(), float(np.max(np.abs(xp - xr)))
+
+
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_engines_bit_identical(name):
     xp, rp = _values(CASES[name], L.System.ENGINE_PERSISTENT)
