@@ -40,6 +40,8 @@ enum : int {
   CTL_FBW = 24,
   // multi-launch maxmin, target-ordered rows: alive rows counted by the regroup (srt_prep -> srt_flip)
   CTL_SORTN = 30,
+  // fair bottleneck, one context: the long-chain queue head of the round's fbk_update_seq (reset by fbk_share)
+  CTL_FBLQ = 31,
   CTL_WORDS = 32
 };
 

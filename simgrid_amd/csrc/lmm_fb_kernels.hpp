@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
     s.ctl[CTL_ROUNDS] += 1;
+    s.ctl[CTL_FBLQ] = 0;  // fbk_update_seq's long-chain queue of this round
   }
   unsigned long long ne = 0, nc = 0;  // this round's listed constraints and their elements (measurement)
   for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
@@ -676,7 +677,32 @@ __global__ void __launch_bounds__(kBlock) fb_long_list(Dev s, uint32_t longmin) 
       s.fb_long[1 + atomicAdd(&s.fb_long[0], 1)] = int32_t(c);
 }
 
-constexpr int kLongBlocks = 128;  // workgroups of fbk_update_seq that take the long constraints
+constexpr int kLongBlocks = 128;  // workgroups of fbk_update_seq that take the long constraints (default)
+
+// The long list longest first (one workgroup, up to kLongSortMax entries; a longer list stays in list order):
+// the workgroups of fbk_update_seq then take the chains from a queue in that order (longest-processing-time
+// first), so no workgroup is left with two of the longest chains while others idle.  Rank of entry i = the
+// entries longer than it, or as long with a smaller constraint id: a permutation, the same for every run.
+constexpr int kLongSortMax = 4096;
+__global__ void __launch_bounds__(1024) fb_long_sort(Dev s) {
+  __shared__ int32_t ids[kLongSortMax];
+  __shared__ uint32_t len[kLongSortMax];
+  const int n = s.fb_long[0];
+  if (n > kLongSortMax)
+    return;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const int32_t c = s.fb_long[1 + i];
+    ids[i] = c;
+    len[i] = s.cnst_ptr[c + 1] - s.cnst_ptr[c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    int rank = 0;
+    for (int j = 0; j < n; j++)
+      rank += len[j] > len[i] || (len[j] == len[i] && ids[j] < ids[i]);
+    s.fb_long[1 + rank] = ids[i];
+  }
+}
 
 // Block-wide (kBlock threads) exclusive scan of an int64 per thread; *tot = the block total.
 __device__ __forceinline__ long long fb_block_scan64(long long v, long long* ws, long long* tot) {
@@ -845,14 +871,29 @@ __device__ void fb_long_chain(const Dev& s, int32_t c, double prec, double* sh) 
 // workgroup each (fb_long_chain, from fbk_acc's increments in fbd); the others one wave per listed constraint:
 // shorter shared ones through fb_chain_pull, FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0
 // erases the constraint (:129).
-__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin, uint32_t streammin) {
+// nlb: the workgroups that take the long chains; dyn: they take them from the queue CTL_FBLQ (the list sorted
+// longest first by fb_long_sort) instead of the static stride i = b, b + nlb, ...
+__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin, uint32_t streammin,
+                                                         int nlb, int dyn) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
-  if (blockIdx.x < kLongBlocks) {
+  __shared__ int qi;
+  if (int(blockIdx.x) < nlb) {
     const int nl = s.fb_long[0];
-    for (int i = blockIdx.x; i < nl; i += kLongBlocks) {  // block-uniform
+    for (int i = blockIdx.x;;) {  // block-uniform
+      if (dyn) {
+        __syncthreads();  // (qi's last reader is done)
+        if (threadIdx.x == 0)
+          qi = atomicAdd(&s.ctl[CTL_FBLQ], 1);
+        __syncthreads();
+        i = qi;
+      }
+      if (i >= nl)
+        break;
       const int32_t c = s.fb_long[1 + i];
+      if (!dyn)
+        i += nlb;
       if (s.ratio[c] != 0.0) {
         if (threadIdx.x == 0)
           s.erased[c] = 0;
@@ -864,8 +905,8 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uin
   }
   const int lane = threadIdx.x & (kWave - 1);
   double* d = dl[threadIdx.x / kWave];
-  for (int64_t c = (int64_t(blockIdx.x - kLongBlocks) * kBlock + threadIdx.x) / kWave; c < s.nC;
-       c += int64_t(gridDim.x - kLongBlocks) * (kBlock / kWave)) {  // wave-uniform
+  for (int64_t c = (int64_t(blockIdx.x - nlb) * kBlock + threadIdx.x) / kWave; c < s.nC;
+       c += int64_t(gridDim.x - nlb) * (kBlock / kWave)) {  // wave-uniform
     const bool fat = s.cflags[c] & 1;
     const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
     if (!fat && ce - cb >= longmin)  // a long constraint: its workgroup writes everything

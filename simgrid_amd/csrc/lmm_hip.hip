@@ -124,6 +124,8 @@ struct lmmhip_ctx {
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
   int64_t fb_round = 0;
   uint32_t fb_longmin = 0;  // solve_fair: shared constraints with >= this many elements use fbk_acc's increments
+  int fb_nlb = 128;          // solve_fair: fbk_update_seq workgroups for the long chains
+  int fb_lpt = 0;            // solve_fair: long chains longest first from a queue (fb_long_sort)
   uint32_t fb_streammin = 1u << 30;  // solve_fair: ... and from this length on their waves stream them (fb_chain)
   double fb_prec = 0;
   bool fb_shard = false;
@@ -2229,8 +2231,8 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
       break;
     }
     // one context: element by element in the CSC order, bit-identical to the reference
-    LAUNCH(5, r, fbk_update_seq, kLongBlocks + grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec,
-           c->fb_longmin, std::min(c->fb_longmin, c->fb_streammin));
+    LAUNCH(5, r, fbk_update_seq, c->fb_nlb + grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec,
+           c->fb_longmin, std::min(c->fb_longmin, c->fb_streammin), c->fb_nlb, c->fb_lpt);
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d, int(r > 0));  // (vstb is packed in rounds > 0)
     c->fb_round++;
     break;
@@ -2363,6 +2365,13 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   hipLaunchKernelGGL(fb_long_list, dim3(grid_for(c->d.nC, kBlock)), dim3(kBlock), 0, c->stream, c->d,
                      c->fb_longmin);
   HIPCHK(hipGetLastError());
+  // the long chains longest first, taken from a queue (LMMHIP_FB_LPT, A/B knob), by LMMHIP_FB_LONGWG workgroups
+  c->fb_lpt = env_int("LMMHIP_FB_LPT", 0) != 0 ? 1 : 0;
+  c->fb_nlb = std::max(1, env_int("LMMHIP_FB_LONGWG", kLongBlocks));
+  if (c->fb_lpt) {
+    hipLaunchKernelGGL(fb_long_sort, dim3(1), dim3(1024), 0, c->stream, c->d);
+    HIPCHK(hipGetLastError());
+  }
   c->d.xnb = c->xnb_own;
   c->d.xmin = c->xmin_own;
   if (int rc = fb_perm(c))
