@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the vote filter's packed words (LMMHIP_PKF): bit identity, then the C2 / C2-stress A/B on one box.
+# Round 5: the vote filter's packed words (LMMHIP_PKF, removed after this measurement: DESIGN.md §6 "Round 5"): bit identity, then the C2 / C2-stress A/B on one box.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_engines.py -k "target_ordered" -x -v -p no:cacheprovider \
