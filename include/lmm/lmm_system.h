@@ -190,7 +190,7 @@ int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const 
  * (0, 0) for an ordinary link.  A WIFI link weighs 1 / source rate (1 / destination rate when the source is not
  * associated, network_cm02.cpp:239-260), and its own bandwidth (1 / bf) and latency (0) are used, whatever
  * route_bw / route_lat hold for it.  Errors (-1, lmm_last_error) as the reference's assertions: a back route
- * (crosstraffic) with a WIFI link, or neither station associated. */
+ * (crosstraffic) with a WIFI link, or neither station associated; and a rate that is neither > 0 nor -1. */
 int64_t lmm_wifi_link_new(lmm_sys* s, int model);
 int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst,
                            const double* route_bw, const double* route_lat, const double* route_rates, int64_t n_back,

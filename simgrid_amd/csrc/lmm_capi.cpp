@@ -523,6 +523,9 @@ int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, con
         throw std::invalid_argument("lmm_communicate: bad route constraint");
       lmm_plat::Link k{route_bw[i], route_lat[i], false};
       if (route_rates && (route_rates[2 * i] != 0.0 || route_rates[2 * i + 1] != 0.0)) {
+        for (int e = 0; e < 2; e++)  // a station's rate on the access point, or -1 (not associated)
+          if (!(route_rates[2 * i + e] > 0.0 || route_rates[2 * i + e] == -1.0))
+            throw std::invalid_argument("lmm_communicate: a WIFI rate must be > 0 or -1 (not associated)");
         k.wifi = true;  // a WIFI access point: its own bandwidth (1 / bandwidth factor) and latency (0)
         k.lat = 0.0;
         k.src_rate = route_rates[2 * i];

@@ -86,6 +86,9 @@ def test_wifi_weights_and_errors():
             comm([(ap, 0.0, 0.0, (6e6, -1.0))], back=[wl])
         with pytest.raises(err, match="not associated"):
             comm([(ap, 0.0, 0.0, (-1.0, -1.0))])
+        if backend == "product":  # (a rate of 0 would weigh 1 / 0: refused)
+            with pytest.raises(err, match="WIFI rate"):
+                comm([(ap, 0.0, 0.0, (0.0, 6e6))])
 
 
 def test_wifi_oracle_closed_form():
