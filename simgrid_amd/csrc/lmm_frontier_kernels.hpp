@@ -293,8 +293,10 @@ __global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
 // Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
 // fr_vote_blk: the work of (virtual) workgroup vb — also run by the persistent frontier kernel (fr_persist), whose
 // workgroups loop over the virtual ones; the queue counts are read relaxed (written in the same launch there).
-template <bool kEarly, int R>
-__device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, int64_t vb) {
+// kP: called by the persistent kernel (fr_persist), where the counts were written in the same launch: read relaxed
+// (the multi-launch kernel's plain loads may come from the scalar cache, which a launch boundary keeps coherent).
+template <bool kEarly, int R, bool kP = false>
+__device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, int vb) {
   // spb (<= kFVS) consecutive segments per workgroup: on C2 ~170 queued rows, one pass, and the launch's
   // workgroups resident at once; small systems keep one segment per workgroup (more workgroups)
   const int64_t nseg = (int64_t(s.nC) + kFB - 1) / kFB;
@@ -303,8 +305,8 @@ __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, in
   pre[0] = 0;
 #pragma unroll
   for (int k = 0; k < kFVS; k++) {
-    const int64_t sg = vb * spb + k;
-    n[k] = k < spb && sg < nseg ? ld_rlx(&s.fq_n[sg]) : 0;
+    const int64_t sg = int64_t(vb) * spb + k;
+    n[k] = k < spb && sg < nseg ? (kP ? ld_rlx(&s.fq_n[sg]) : s.fq_n[sg]) : 0;
     seg[k] = k < spb && sg < nseg ? s.cnst_ptr[sg * kFB] : 0u;
     pre[k + 1] = pre[k] + n[k];
   }
@@ -475,10 +477,10 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 constexpr int kFS = 1024;
 
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int64_t vb, SatLds<NB, NB>& L) {
+__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  const int64_t c = vb * NB + threadIdx.x;
+  const int64_t c = int64_t(vb) * NB + threadIdx.x;
   bool rdy = false;
   int nch = 0;
   if (c < s.nC && s.key32[c] != kDead32 && s.nvote[c] == 0) {
@@ -539,11 +541,12 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
 // The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
 // constraint over the whole grid, wave k taking chunks k, k + kFrBigWaves, ...
 // (the grid's waves over the list: wave / nwaves; wpre = the calling wave's 64-int LDS scratch)
+template <bool kP = false>
 __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bigw, int nb, int64_t wave,
                                                  int64_t nwaves, int* wpre) {
   const int lane = threadIdx.x & (kWave - 1);
   for (int64_t g = wave; g < int64_t(nb) * bigw; g += nwaves) {
-    const int32_t c = ld_rlx(&s.ready[g / bigw]);
+    const int32_t c = kP ? ld_rlx(&s.ready[g / bigw]) : s.ready[g / bigw];
     const int k = int(g % bigw);
     const double r = ld_rlx(&s.cst[c].ratio);
     const uint32_t ce = s.cnst_ptr[c + 1];
@@ -587,7 +590,10 @@ struct FrUpdLds {
   uint32_t mf[kFB];
 };
 
-__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int64_t vb, FrUpdLds& U) {
+// kP: called by fr_persist (the control words another workgroup reads or adds to in the same launch: relaxed
+// atomic stores; the multi-launch kernel keeps its plain stores).
+template <bool kP = false>
+__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int vb, FrUpdLds& U) {
   int& qn = U.qn;
   auto& pre = U.pre;
   uint32_t* mf = U.mf;
@@ -596,9 +602,12 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
     qn = 0;
   if (vb == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ROUNDS] += 1;
-    st_rlx(&s.ctl[CTL_NREADY], 0);  // fr_sat_big's list of the next round (its adds are atomics: no cached copy)
+    if (kP)
+      st_rlx(&s.ctl[CTL_NREADY], 0);  // fr_sat_big's list of the next round (its adds are atomics: no cached copy)
+    else
+      s.ctl[CTL_NREADY] = 0;
   }
-  const int64_t gbase = vb * kFB + int64_t(w) * kWave;
+  const int64_t gbase = int64_t(vb) * kFB + int64_t(w) * kWave;
   const int64_t c = gbase + lane;
   const bool in = c < s.nC;
   const uint32_t okey = in ? s.key32[c] : kDead32;
@@ -693,7 +702,7 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   pre[w][lane] = incl - len;
   mf[threadIdx.x] = kNoVoter;
   __syncthreads();  // (qn, pre, mf)
-  const uint32_t seg = s.cnst_ptr[vb * kFB];
+  const uint32_t seg = s.cnst_ptr[int64_t(vb) * kFB];
   for (int f0 = 0; f0 < total; f0 += kFrScanU * kWave) {  // wave-uniform (one pass up to 512 slots)
     int ol[kFrScanU];
     uint32_t jj[kFrScanU];
@@ -765,8 +774,12 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   const bool any_alive = __syncthreads_or(alive);
   if (threadIdx.x == 0) {
     s.fq_n[vb] = qn;
-    if (any_alive)
-      st_rlx(&s.ctl[CTL_PALIVE0 + (round & 1)], 1);
+    if (any_alive) {
+      if (kP)
+        st_rlx(&s.ctl[CTL_PALIVE0 + (round & 1)], 1);
+      else
+        s.ctl[CTL_PALIVE0 + (round & 1)] = 1;
+    }
   }
   if (__syncthreads_or(tch || sat) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint

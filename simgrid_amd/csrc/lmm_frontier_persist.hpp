@@ -42,12 +42,12 @@ __global__ void __launch_bounds__(kFB) fr_persist(Dev s, unsigned* barw, double 
       if (lead)
         st_rlx(&s.ctl[CTL_PALIVE0 + (r & 1)], 0);  // this round's update raises it (last read a barrier ago)
       for (int64_t vb = blockIdx.x; vb < nvote; vb += gridDim.x)  // workgroup-uniform
-        fr_vote_blk<false, R>(s, r, spb, vb);
+        fr_vote_blk<false, R, true>(s, r, spb, int(vb));
       if (!grid_sync(b, ++gen))
         return;
     }
     for (int64_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
-      fr_sat_blk<kFB, false>(s, r, bigch, vb, L.sat);
+      fr_sat_blk<kFB, false>(s, r, bigch, int(vb), L.sat);
       __syncthreads();
     }
     if (!grid_sync(b, ++gen))
@@ -58,13 +58,13 @@ __global__ void __launch_bounds__(kFB) fr_persist(Dev s, unsigned* barw, double 
         if (lead)
           s.ctl[CTL_LASTR] = r;
         const int64_t wave = (int64_t(blockIdx.x) * kFB + threadIdx.x) / kWave;
-        fr_sat_big_waves(s, r, bigw, nb, wave, int64_t(gridDim.x) * (kFB / kWave), L.wpre[threadIdx.x / kWave]);
+        fr_sat_big_waves<true>(s, r, bigw, nb, wave, int64_t(gridDim.x) * (kFB / kWave), L.wpre[threadIdx.x / kWave]);
         if (!grid_sync(b, ++gen))
           return;
       }
     }
     for (int64_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {  // (virtual workgroup 0 resets CTL_NREADY)
-      fr_update_blk(s, r, prec, vb, L.upd);
+      fr_update_blk<true>(s, r, prec, int(vb), L.upd);
       __syncthreads();
     }
     if (!grid_sync(b, ++gen))
