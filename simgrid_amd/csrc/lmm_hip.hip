@@ -1528,7 +1528,9 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
   // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
   // Both decide and switch buffers on the device (ctl CTL_BUF / CTL_CB): no host round trip.
-  const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 32);
+  // (round 5, re-swept on the final code, same box: every 48 rounds 24.94-25.08 ms against 25.10-25.21 at 32, 25.49-25.56
+  // at 16, 25.11-25.21 at 64, 25.30-25.34 at 96; stress 28.29-28.37 vs 28.42-28.44)
+  const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 48);
   const int cmp_pct = env_int("LMMHIP_COMPACT_PCT", 75);
   const int cl_every = env_int("LMMHIP_CLIST_EVERY", 8);
   // Short rows, LMMHIP_TGT=1 (measured and off by default): target-ordered alive rows
@@ -1566,8 +1568,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   int chunk = 2, slot = 0;
   // rounds queued per poll: the host learns of termination one chunk late, so up to 2 x chunk_max no-op
   // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C2 25.96-25.99 ms at 16, 26.01 at 8,
-  // 26.15-26.20 at 4
-  const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 16));
+  // 26.15-26.20 at 4; round 5, with compactions every 48 rounds: 25.03-25.06 at 32 against 25.07-25.08 at 16
+  const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 32));
   // tail hand-off (lmm_tail_kernels.hpp; LMMHIP_TAIL_ROWS, 0 = off): not from a continued solve itself, not in
   // the profiling mode (it times this engine's launches), not with the target-ordered rows
   const int64_t tail_rows = env_int("LMMHIP_TAIL_ROWS", kTailRows);
