@@ -12,6 +12,32 @@ line() {  # line <tag> <env...> -- <bench args>
   if [ $rc -ne 0 ]; then echo "STOP $tag rc=$rc"; tail -n 20 gpurun_out/kn_$tag.log; exit $rc; fi
   python3 -c "import json; d=json.loads(open('gpurun_out/kn_$tag.json').read().strip().splitlines()[-1]); print('$tag', d['ms_per_step'])"
 }
+if [ "$1" = "4" ]; then
+for pass in a b; do
+line base4_$pass LMMHIP_X=0 --
+line sb768_$pass LMMHIP_SAT_BLOCKS=768 --
+line sb1024_$pass LMMHIP_SAT_BLOCKS=1024 --
+line sb1280_$pass LMMHIP_SAT_BLOCKS=1280 --
+line sb1536_$pass LMMHIP_SAT_BLOCKS=1536 --
+line st_base4_$pass LMMHIP_X=0 -- --variant stress
+line st_sb1024_$pass LMMHIP_SAT_BLOCKS=1024 -- --variant stress
+line st_sb768_$pass LMMHIP_SAT_BLOCKS=768 -- --variant stress
+done
+echo done
+exit 0
+fi
+if [ "$1" = "3" ]; then
+for pass in a b; do
+line base3_$pass LMMHIP_X=0 --
+line sb512_$pass LMMHIP_SAT_BLOCKS=512 --
+line sb1024_$pass LMMHIP_SAT_BLOCKS=1024 --
+line sb2048_$pass LMMHIP_SAT_BLOCKS=2048 --
+line cmp40_$pass LMMHIP_COMPACT_EVERY=40 --
+line cmp56_$pass LMMHIP_COMPACT_EVERY=56 --
+done
+echo done
+exit 0
+fi
 if [ "$1" = "2" ]; then
 for pass in a b; do
 line base_$pass LMMHIP_X=0 --

@@ -1517,7 +1517,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // Launch-width caps (tuning knobs, environment; 0 = uncapped): fewer blocks cut the fixed per-round
   // cost of the grid-stride round kernels once the alive set is small.
   const int cap_upd = env_int("LMMHIP_UPD_BLOCKS", c->tune_upd);
-  const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat);
+  // the saturation's grid capped at 4 workgroups per CU (round 5, same box: C2 24.73-24.90 ms against 25.04-25.16
+  // uncapped, i.e. up to kMaxBlocks = 2048; 768: 24.79-25.03, 1280: 24.76-24.81, 1536: 24.83-25.00, 512: 25.42-25.73;
+  // stress 27.99-28.05 vs 28.29-28.36): every workgroup first rebuilds the prefix of the update's segment counts,
+  // and half as many of them still give each ready constraint its waves
+  const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat > 0 ? c->tune_sat : 4 * c->n_cu);
   auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
   const int gUq = int(gU_rdq);          // (ready-queue mode: at most kUSeg constraints per workgroup)
