@@ -12,6 +12,30 @@ line() {  # line <tag> <env...> -- <bench args>
   if [ $rc -ne 0 ]; then echo "STOP $tag rc=$rc"; tail -n 20 gpurun_out/kn_$tag.log; exit $rc; fi
   python3 -c "import json; d=json.loads(open('gpurun_out/kn_$tag.json').read().strip().splitlines()[-1]); print('$tag', d['ms_per_step'])"
 }
+if [ "$1" = "6" ]; then
+for pass in a b; do
+line u6base_$pass LMMHIP_UPDQ_BLOCKS=1024 --
+line u6s1280_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=1280 --
+line u6s1536_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=1536 --
+line u6s2048_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=2048 --
+line st_u6s1280_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=1280 -- --variant stress
+line st_u6s1536_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=1536 -- --variant stress
+done
+echo done
+exit 0
+fi
+if [ "$1" = "5" ]; then
+for pass in a b; do
+line base5_$pass LMMHIP_X=0 --
+line uq1024_$pass LMMHIP_UPDQ_BLOCKS=1024 --
+line uq1024s768_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=768 --
+line uq1024s1280_$pass LMMHIP_UPDQ_BLOCKS=1024 LMMHIP_SAT_BLOCKS=1280 --
+line st_base5_$pass LMMHIP_X=0 -- --variant stress
+line st_uq1024_$pass LMMHIP_UPDQ_BLOCKS=1024 -- --variant stress
+done
+echo done
+exit 0
+fi
 if [ "$1" = "4" ]; then
 for pass in a b; do
 line base4_$pass LMMHIP_X=0 --

@@ -1467,7 +1467,13 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   d.rdq[0] = d.rdq[1] = nullptr;
   d.rqst = d.useg = d.ucnt = nullptr;
   d.uent = nullptr;
-  const int64_t gU_rdq = grid_for(d.nC, kBlock);  // (<= kMaxBlocks)
+  // (<= kMaxBlocks) Update workgroups: 4 per CU, each with a longer segment, so that the saturation's prefix over
+  // the segment counts is shorter — but enough of them to keep every segment within kUSeg (LMMHIP_UPDQ_BLOCKS).
+  // Round 5, same box: C2 24.52-24.54 ms against 24.84-24.85 with one per 256 constraints (2,048 at C2), stress
+  // 27.86-27.94 vs 28.14; with the saturation cap at 5 per CU below, 24.41-24.45 (stress 27.75-27.77)
+  const int64_t gU_need = (int64_t(d.nC) + kUSeg - 1) / kUSeg;
+  const int64_t gU_rdq = std::max<int64_t>(1, std::min<int64_t>(grid_for(d.nC, kBlock),
+      std::max<int64_t>(gU_need, env_int("LMMHIP_UPDQ_BLOCKS", 4 * c->n_cu))));
   const int64_t per_blk = int64_t(kBlock) * ((int64_t(d.nC) + gU_rdq * kBlock - 1) / (gU_rdq * kBlock));
   if (d.crec[0] && env_int("LMMHIP_RDQ", 1) && per_blk <= kUSeg && env_int("LMMHIP_UPD_BLOCKS", c->tune_upd) == 0) {
     int32_t *q0 = nullptr, *q1 = nullptr, *st = nullptr, *sg = nullptr, *uc = nullptr;
@@ -1521,7 +1527,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // uncapped, i.e. up to kMaxBlocks = 2048; 768: 24.79-25.03, 1280: 24.76-24.81, 1536: 24.83-25.00, 512: 25.42-25.73;
   // stress 27.99-28.05 vs 28.29-28.36): every workgroup first rebuilds the prefix of the update's segment counts,
   // and half as many of them still give each ready constraint its waves
-  const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat > 0 ? c->tune_sat : 4 * c->n_cu);
+  // (with 4 update workgroups per CU: 5 per CU, 24.41-24.45 ms against 24.52-24.54 at 4 and 24.52-24.60 at 6 / 8)
+  const int cap_sat = env_int("LMMHIP_SAT_BLOCKS", c->tune_sat > 0 ? c->tune_sat : 5 * c->n_cu);
   auto capped = [](int g, int cap) { return cap > 0 && g > cap ? cap : g; };
   const int gU = capped(gC, cap_upd);  // mm_update: thread per constraint, identity order
   const int gUq = int(gU_rdq);          // (ready-queue mode: at most kUSeg constraints per workgroup)
