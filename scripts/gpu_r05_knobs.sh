@@ -12,6 +12,18 @@ line() {  # line <tag> <env...> -- <bench args>
   if [ $rc -ne 0 ]; then echo "STOP $tag rc=$rc"; tail -n 20 gpurun_out/kn_$tag.log; exit $rc; fi
   python3 -c "import json; d=json.loads(open('gpurun_out/kn_$tag.json').read().strip().splitlines()[-1]); print('$tag', d['ms_per_step'])"
 }
+if [ "$1" = "7" ]; then  # (a build with kUSeg = 2048)
+for pass in a b; do
+line u7_1024_$pass LMMHIP_UPDQ_BLOCKS=1024 --
+line u7_768_$pass LMMHIP_UPDQ_BLOCKS=768 --
+line u7_512_$pass LMMHIP_UPDQ_BLOCKS=512 --
+line u7_512s1024_$pass LMMHIP_UPDQ_BLOCKS=512 LMMHIP_SAT_BLOCKS=1024 --
+line st_u7_1024_$pass LMMHIP_UPDQ_BLOCKS=1024 -- --variant stress
+line st_u7_512_$pass LMMHIP_UPDQ_BLOCKS=512 -- --variant stress
+done
+echo done
+exit 0
+fi
 if [ "$1" = "6" ]; then
 for pass in a b; do
 line u6base_$pass LMMHIP_UPDQ_BLOCKS=1024 --
