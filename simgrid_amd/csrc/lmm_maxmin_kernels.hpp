@@ -1007,7 +1007,10 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
 // atomic request per element; scripts/ubench_atomic.hip).  Decrements to c itself are skipped: c
 // leaves the light table (every alive variable on it is fixed, usage -> 0, maxmin.cpp:608-615).
 // c's ratio is left in place (the other waves of c read it; the dead key hides it from later readers).
-constexpr int kSatU = 4;
+#ifndef LMM_KSATU
+#define LMM_KSATU 4  // (build knob, measurement)
+#endif
+constexpr int kSatU = LMM_KSATU;
 
 // retire (multi-launch engine, round 4): the buffer's row targets; each claimed variable's alive row (rowof) is
 // marked kRetired, so the next vote's filter skips it instead of queueing a re-vote that only finds the
