@@ -1545,6 +1545,13 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
 
 // balive[block] = constraints of the block's range still in the light table (read by mm_done; plain
 // stores, no global atomic).
+// groups of 64 constraints per wave step, their loads in flight together (build knob, measurement).  Round 5, same
+// box, two passes (scripts/gpu_r05_updk.sh, profiles/r05_ab_c2_updk.json): 4 -> C2 24.35-24.36 ms against
+// 24.40-24.42 with 2 and 24.54-24.58 with 1 (at C2 a thread of the 1,024 update workgroups owns ~4 constraints:
+// with 4 groups every load of the round's update is issued at once)
+#ifndef LMM_UPD_K
+#define LMM_UPD_K 4
+#endif
 template <bool kRdq = false, bool kEnt = false>
 __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
@@ -1560,8 +1567,8 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   bool any_touch = false;
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
-       base += 2 * stride)  // wave-uniform; two groups of 64 constraints per step, loads in flight together
-    alive += update_groups<2, kRdq, kEnt>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
+       base += LMM_UPD_K * stride)  // wave-uniform; LMM_UPD_K groups of 64 constraints per step, loads in flight together
+    alive += update_groups<LMM_UPD_K, kRdq, kEnt>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
