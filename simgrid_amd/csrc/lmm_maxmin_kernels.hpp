@@ -612,15 +612,25 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 constexpr int kQW = 2 * kWave;  // per-wave queue capacity
 constexpr int kDiagSlot = kMaxBlocks - 4;  // vstat block slots kDiagSlot.. hold the vote diagnostics (kDiag)
 
-template <bool kBits, int R, int F, int kDiag, bool kRec = false, bool kRdq = false>
-__device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
-                                          const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
-                                          const uint16_t* __restrict__ key) {
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave, nw = blockDim.x / kWave;
+// The wave's row range [wlo, whi) of the workgroup's rows [lo, hi).
+__device__ __forceinline__ void vote_wave_range(int64_t lo, int64_t hi, int64_t& wlo, int64_t& whi) {
+  const int w = threadIdx.x / kWave, nw = blockDim.x / kWave;
   const int64_t ngr = (hi - lo + kWave - 1) / kWave;
   const int64_t gpw = (ngr + nw - 1) / nw;
-  const int64_t wlo = lo + int64_t(w) * gpw * kWave;
-  const int64_t whi = wlo + gpw * kWave < hi ? wlo + gpw * kWave : hi;
+  wlo = lo + int64_t(w) * gpw * kWave;
+  whi = wlo + gpw * kWave < hi ? wlo + gpw * kWave : hi;
+}
+
+// kPre: the targets and floors of the wave's first filter step were loaded by the caller (tt0 / sk0, issued before
+// the bitmap copy, so that their latency overlaps it).
+template <bool kBits, int R, int F, int kDiag, bool kRec = false, bool kRdq = false, bool kPre = false>
+__device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
+                                          const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
+                                          const uint16_t* __restrict__ key, const int* tt0 = nullptr,
+                                          const unsigned* sk0 = nullptr) {
+  const int lane = threadIdx.x & (kWave - 1);
+  int64_t wlo, whi;
+  vote_wave_range(lo, hi, wlo, whi);
   const int32_t* __restrict__ rtgt = s.rtgt[buf];
   const uint16_t* __restrict__ skey = s.skey[buf];
   const uint16_t prev = uint16_t(round - 1);
@@ -630,11 +640,19 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   for (int64_t base = wlo; base < whi; base += int64_t(F) * kWave) {  // wave-uniform
     int tt[F];
     unsigned sk[F];
+    if (kPre && base == wlo) {  // wave-uniform
 #pragma unroll
-    for (int u = 0; u < F; u++) {
-      const int64_t row = base + u * kWave + lane;
-      tt[u] = row < whi ? rtgt[row] : kRetired;
-      sk[u] = row < whi ? unsigned(skey[row]) : 1u;
+      for (int u = 0; u < F; u++) {
+        tt[u] = tt0[u];
+        sk[u] = sk0[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < F; u++) {
+        const int64_t row = base + u * kWave + lane;
+        tt[u] = row < whi ? rtgt[row] : kRetired;
+        sk[u] = row < whi ? unsigned(skey[row]) : 1u;
+      }
     }
     bool ch[F];
 #pragma unroll
@@ -767,6 +785,11 @@ __global__ void __launch_bounds__(kBlock) mm_vote_diagcount(Dev s, int round) {
 // Multi-launch engine, short rows (mean length <= 8): one 1024-thread workgroup per CU (the bitmap takes up
 // to kBitWords * 8 B of LDS), one contiguous chunk of rows per workgroup.
 constexpr int kVBlock = 1024;
+// LMM_VOTE_PRE: the first filter step's loads issued before the bitmap copy (build knob, measurement).  Round 5, same
+// box: 24.313 / 24.390 ms against 24.340 / 24.309 without (neutral: the copy is not the vote's critical path); off.
+#ifndef LMM_VOTE_PRE
+#define LMM_VOTE_PRE 0
+#endif
 template <int B, bool kBits, int kDiag = 0, bool kRec = false, bool kRdq = false>
 __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (s.ctl[CTL_DONE])
@@ -777,6 +800,23 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
   if (threadIdx.x == 0)
     st_rows = st_elems = 0;
+  const int64_t nrows = s.ctl[CTL_NROWS + buf];
+  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;  // rows per workgroup
+  const int64_t lo = int64_t(blockIdx.x) * per;
+  const int64_t hi = lo + per < nrows ? lo + per : nrows;
+  constexpr bool kPre = LMM_VOTE_PRE != 0 && kBits && kDiag == 0;
+  int tt0[kPre ? kFilt : 1];
+  unsigned sk0[kPre ? kFilt : 1];
+  if (kPre) {  // the wave's first filter step, in flight during the bitmap copy
+    int64_t wlo, whi;
+    vote_wave_range(lo, hi, wlo, whi);
+#pragma unroll
+    for (int u = 0; u < (kPre ? kFilt : 1); u++) {
+      const int64_t row = wlo + u * kWave + (threadIdx.x & (kWave - 1));
+      tt0[u] = row < whi ? s.rtgt[buf][row] : kRetired;
+      sk0[u] = row < whi ? unsigned(s.skey[buf][row]) : 1u;
+    }
+  }
   if (kBits)
     load_bits<B, LMM_BITS_STAGGER != 0, LMM_BITS_UNROLL>(s, bits);
   __syncthreads();
@@ -791,13 +831,9 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
       s.ctl[CTL_WORDS - 1] = 1;
     return;
   }
-  const int64_t nrows = s.ctl[CTL_NROWS + buf];
-  const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;  // rows per workgroup
-  const int64_t lo = int64_t(blockIdx.x) * per;
-  const int64_t hi = lo + per < nrows ? lo + per : nrows;
   if (lo < hi)
-    vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
-                                                   &st_rows, &st_elems, s.key);
+    vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
+                                                         &st_rows, &st_elems, s.key, tt0, sk0);
   if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
@@ -1241,6 +1277,15 @@ template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int3
   if (k == 0 && lane == 0)  // c leaves the light table: mm_update (the owner of key / chg) retires it
     s.ctouch[c] = 2;
 }
+// (the same with the constraint's ratio, CSC range and duplicate flag already loaded)
+template <int K> __device__ __forceinline__ void saturate_one_pre(const Dev& s, int32_t c, int k, int round, int lane,
+                                                                  int* pre, int32_t* retire, double r, uint32_t cb,
+                                                                  uint32_t ce, bool dup) {
+  for (uint32_t base = cb + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
+    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup, retire);
+  if (k == 0 && lane == 0)
+    s.ctouch[c] = 2;
+}
 
 // K waves per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
 // counts in LDS (parallel: 8 segments per thread, wave shuffles, one LDS exchange) and maps its waves
@@ -1307,6 +1352,12 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 // them, mm_saturate's prefix and binary search over their counts) then the vote's queue; K waves per entry;
 // an entry is saturated when it is still alive with nothing voting elsewhere (every vote of the round is in).
 // Block 0 empties the other parity's vote queue, which the next round's vote fills.
+// LMM_SATQ_SPEC: a candidate's ratio, CSC range and duplicate flag loaded with its key and vote count (build knob).
+// Round 5, same box, two passes (scripts/gpu_r05_spec2.sh, profiles/r05_ab_c2_spec2.json): C2 24.285-24.293 ms
+// against 24.309-24.340 without — small, but in both passes; kept.
+#ifndef LMM_SATQ_SPEC
+#define LMM_SATQ_SPEC 1
+#endif
 template <int K, bool kEnt = false>
 __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
   if (s.ctl[CTL_DONE])
@@ -1382,11 +1433,26 @@ __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ub
     } else {
       c = q[i - total];
     }
+#if LMM_SATQ_SPEC
+    // the constraint's ratio, CSC range and duplicate flag loaded with its key and count (one dependent level less;
+    // a candidate that is not ready discards them)
+    const unsigned kc = s.key[c];
+    const int nv = s.nvote[c];
+    const double r = ld_rlx(&s.cst[c].ratio);
+    const uint32_t cb = s.cnst_ptr[c], cend = s.cnst_ptr[c + 1];
+    const bool dup = s.cdup[c] != 0;
+    if (kc == kDeadKey || nv != 0)
+      continue;
+    if (k == 0 && lane == 0)
+      s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
+    saturate_one_pre<K>(s, c, k, round, lane, wpre[w], retire, r, cb, cend, dup);
+#else
     if (s.key[c] == kDeadKey || s.nvote[c] != 0)
       continue;
     if (k == 0 && lane == 0)
       s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
     saturate_one<K>(s, c, k, round, lane, wpre[w], retire);
+#endif
   }
 }
 
