@@ -13,17 +13,19 @@ if [ $rc -ne 0 ]; then echo "STOP smoke rc=$rc"; exit $rc; fi
 timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_default.json 2> gpurun_out/bench_default.log; rc=$?
 tail -1 gpurun_out/bench_default.json | cut -c1-300
 if [ $rc -ne 0 ]; then echo "STOP bench rc=$rc"; tail -n 20 gpurun_out/bench_default.log; exit $rc; fi
-# the saturation grid cap re-swept on the K=4 update (env knob; 5 per CU = 1280 is the default)
+# the end-of-solve chunk knobs around the default (5 % of the variables, 4 rounds per chunk)
+# (earlier in the round: the saturation grid cap LMMHIP_SAT_BLOCKS 1024 / 1536 re-swept here, default stayed)
 line() {  # line <tag> <env...>
   local tag=$1; shift
   env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dropin-steps 0 \
-    > gpurun_out/sc_$tag.json 2> gpurun_out/sc_$tag.log; local rc=$?
-  if [ $rc -ne 0 ]; then echo "STOP $tag rc=$rc"; tail -n 20 gpurun_out/sc_$tag.log; exit $rc; fi
-  python3 -c "import json; d=json.loads(open('gpurun_out/sc_$tag.json').read().strip().splitlines()[-1]); print('$tag', d['ms_per_step'])"
+    > gpurun_out/se_$tag.json 2> gpurun_out/se_$tag.log; local rc=$?
+  if [ $rc -ne 0 ]; then echo "STOP $tag rc=$rc"; tail -n 20 gpurun_out/se_$tag.log; exit $rc; fi
+  python3 -c "import json; d=json.loads(open('gpurun_out/se_$tag.json').read().strip().splitlines()[-1]); print('$tag', d['ms_per_step'])"
 }
 for pass in a b; do
   line base_$pass LMMHIP_X=0
-  line s1024_$pass LMMHIP_SAT_BLOCKS=1024
-  line s1536_$pass LMMHIP_SAT_BLOCKS=1536
+  line t2_$pass LMMHIP_CHUNK_TAIL=2
+  line p10_$pass LMMHIP_CHUNK_TAIL_PCT=10
+  line p2_$pass LMMHIP_CHUNK_TAIL_PCT=2
 done
 echo done

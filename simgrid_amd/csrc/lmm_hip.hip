@@ -1581,6 +1581,17 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C2 25.96-25.99 ms at 16, 26.01 at 8,
   // 26.15-26.20 at 4; round 5, with compactions every 48 rounds: 25.03-25.06 at 32 against 25.07-25.08 at 16
   const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 32));
+  // Near the end of the solve, short chunks: the rounds queued after the last one are no-op launches of the full
+  // grids (~32 of them after C2's last round with 32-round chunks, rocprofv3 trace of round 5), so once the alive rows
+  // (host view: refreshed at each compaction) fall to LMMHIP_CHUNK_TAIL_PCT % of the variables (default 5), or below
+  // LMMHIP_CHUNK_TAIL_ROWS / the alive-constraint list below LMMHIP_CHUNK_TAIL_CNST (A/B knobs), a chunk is at most
+  // LMMHIP_CHUNK_TAIL rounds (default 4).  Round 5, same box, two passes (scripts/gpu_r05_ctail.sh,
+  // profiles/r05_ab_c2_ctail.json): C2 23.90-23.95 ms at 5e5 rows (5 %) / 4 rounds against 24.10-24.12 without;
+  // 1e6 / 8 and 2e6 / 8 23.92-23.94, 1e6 / 4 23.95-24.07; the constraint-list thresholds (2e4, 1e5) 24.06-24.11.
+  const int64_t ctail_rows = env_int("LMMHIP_CHUNK_TAIL_ROWS",
+                                     int(int64_t(d.nV) * std::max(0, env_int("LMMHIP_CHUNK_TAIL_PCT", 5)) / 100));
+  const int64_t ctail_cnst = env_int("LMMHIP_CHUNK_TAIL_CNST", 0);
+  const int ctail = std::max(1, env_int("LMMHIP_CHUNK_TAIL", 4));
   // tail hand-off (lmm_tail_kernels.hpp; LMMHIP_TAIL_ROWS, 0 = off): not from a continued solve itself, not in
   // the profiling mode (it times this engine's launches), not with the target-ordered rows
   const int64_t tail_rows = env_int("LMMHIP_TAIL_ROWS", kTailRows);
@@ -1685,6 +1696,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
     if (chunk < chunk_max)
       chunk = std::min(2 * chunk, chunk_max);
+    if ((nrows <= ctail_rows || ncl <= ctail_cnst) && chunk > ctail)
+      chunk = ctail;
   }
   return poll_ctl(c);  // (the queued tail has run: final words for the stats)
 }
