@@ -219,11 +219,6 @@ int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
  * engine directly.  Persistent launches of one process are serialised per device, so two Systems never starve
  * each other. */
 int lmmhip_engine_fallbacks(lmmhip_ctx* ctx, int64_t* n);
-/* Tail hand-off of the multi-launch max-min engine (LMMHIP_TAIL_ROWS: alive rows at a termination poll at or
- * below which the rest of the solve runs on the compacted remaining system in a child context, with the engine
- * its size calls for; lmm_tail_kernels.hpp): solves of this context handed off so far, and the
- * round of the last hand-off (-1: none).  Results are bit-identical with and without it. */
-int lmmhip_tail_handoffs(lmmhip_ctx* ctx, int64_t* n, int64_t* round);
 /* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the
  * wall-clock time (100 MHz) of the last workgroup's arrival and of workgroup 0's exit.  With t != NULL,
  * copies the last solve's records: t[2i] = last arrival at barrier i, t[2i+1] = exit (barrier 0 = the
@@ -330,6 +325,11 @@ int lmmhip_actions_lazy_download(lmmhip_ctx* ctx, double* last_update, double* l
 int lmmhip_device_count(void);
 
 const char* lmmhip_last_error(void);
+
+/* Build provenance: the first 16 hex digits of a SHA-256 over the sources this library was compiled from
+ * (simgrid_amd/csrc, include/lmm; simgrid_amd/build_id.py defines the hash, csrc/Makefile compiles it in).
+ * smoke() compares it with the hash of the tree it runs from. */
+const char* lmmhip_build_id(void);
 
 #ifdef __cplusplus
 }

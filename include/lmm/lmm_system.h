@@ -185,16 +185,20 @@ int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const 
                         double tcp_gamma, int paid, lmm_comm_info* out);
 /* WIFI access points (NetworkWifiLink, network_cm02.cpp:383-420).  lmm_wifi_link_new: the access point's
  * constraint, a shared link of bandwidth 1 / bandwidth factor (bound bf * (1 / bf)).  lmm_communicate_ex is
- * lmm_communicate with route_rates (NULL: no WIFI link on the route): 2 doubles per route link, the source and
+ * lmm_communicate with `crosstraffic` (the network/crosstraffic configuration: nonzero = on, whether or not the
+ * back route holds links; lmm_communicate passes n_back > 0) and route_rates (NULL: no WIFI link on the route): 2
+ * doubles per route link, the source and
  * destination stations' rates on that access point (NetworkWifiLink::get_host_rate, -1 = not associated), or
  * (0, 0) for an ordinary link.  A WIFI link weighs 1 / source rate (1 / destination rate when the source is not
  * associated, network_cm02.cpp:239-260), and its own bandwidth (1 / bf) and latency (0) are used, whatever
- * route_bw / route_lat hold for it.  Errors (-1, lmm_last_error) as the reference's assertions: a back route
- * (crosstraffic) with a WIFI link, or neither station associated; and a rate that is neither > 0 nor -1. */
+ * route_bw / route_lat hold for it.  Errors (-1, lmm_last_error) as the reference's assertions: crosstraffic on
+ * with a WIFI link on the route (network_cm02.cpp:242), or neither station associated; and a rate that is neither
+ * > 0 nor -1. */
 int64_t lmm_wifi_link_new(lmm_sys* s, int model);
 int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst,
                            const double* route_bw, const double* route_lat, const double* route_rates, int64_t n_back,
-                           const int64_t* back_cnst, double rate, double tcp_gamma, int paid, lmm_comm_info* out);
+                           const int64_t* back_cnst, int crosstraffic, double rate, double tcp_gamma, int paid,
+                           lmm_comm_info* out);
 
 int lmm_device_count(void);
 const char* lmm_last_error(void);

@@ -482,14 +482,18 @@ def wifi_link_new(sys, model):
     return sys.constraint_new(None, bf * (1.0 / bf))
 
 
-def communicate(sys, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False):
+def communicate(sys, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False, crosstraffic=None):
     """NetworkCm02Model::communicate (network_cm02.cpp:165-274), its LMM part, on an oracle System:
     route = [(constraint, bw, lat)] in route order (route_to sums the latencies) — a WIFI access point as
     (constraint, bw, lat, (src_rate, dst_rate)), the stations' NetworkWifiLink::get_host_rate (-1: not
     associated), whose own bandwidth 1 / bandwidth factor and latency 0 replace bw / lat —, back = the back
     route's constraints (crosstraffic, weight 0.05).  Returns (variable, dict(latency, lat_current,
     sharing_penalty, bound)); the variable has penalty 0 while the latency is unpaid (1.0 without latency), or
-    with `paid` the sharing penalty update_actions_state restores (network_cm02.cpp:105-146)."""
+    with `paid` the sharing penalty update_actions_state restores (network_cm02.cpp:105-146).  crosstraffic: the
+    network/crosstraffic configuration (None: on iff `back` has links; the WIFI assertion of :242 tests the
+    configuration, not the back route)."""
+    if crosstraffic is None:
+        crosstraffic = bool(len(back))
     lat_factor, bf, weight_s = net_factors(model)
     links = []
     for r in route:
@@ -512,7 +516,7 @@ def communicate(sys, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid
         bound = min(rate, tcp_gamma / (2.0 * lat_current)) if lat_current > 0 else rate
     for _, _, _, rates in links:  # the assertions of network_cm02.cpp:242-255
         if rates is not None:
-            if len(back):
+            if crosstraffic:
                 raise ValueError("Cross-traffic is not yet supported when using WIFI")
             if rates[0] == -1 and rates[1] == -1:
                 raise ValueError("Some Stations are not associated to any Access Point")

@@ -508,7 +508,8 @@ int64_t lmm_wifi_link_new(lmm_sys* s, int model) {
 
 int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst,
                            const double* route_bw, const double* route_lat, const double* route_rates, int64_t n_back,
-                           const int64_t* back_cnst, double rate, double tcp_gamma, int paid, lmm_comm_info* out) {
+                           const int64_t* back_cnst, int crosstraffic, double rate, double tcp_gamma, int paid,
+                           lmm_comm_info* out) {
   try {
     if (!s || n_route < 0 || n_back < 0 || (n_route && (!route_cnst || !route_bw || !route_lat)) ||
         (n_back && !back_cnst))
@@ -543,7 +544,8 @@ int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, con
       back.push_back(int(n_route + i));
     }
     lmm_plat::Comm a;
-    const Id v = lmm_plat::communicate(b, model, links, cn, route, back, lat, rate, tcp_gamma, paid != 0, &a);
+    const Id v = lmm_plat::communicate(b, model, links, cn, route, back, lat, rate, tcp_gamma, paid != 0,
+                                       crosstraffic != 0, &a);
     if (out) {
       out->latency = a.latency;
       out->lat_current = a.lat_current;
@@ -560,8 +562,8 @@ int64_t lmm_communicate_ex(lmm_sys* s, void* id, int model, int64_t n_route, con
 int64_t lmm_communicate(lmm_sys* s, void* id, int model, int64_t n_route, const int64_t* route_cnst, const double* route_bw,
                         const double* route_lat, int64_t n_back, const int64_t* back_cnst, double rate,
                         double tcp_gamma, int paid, lmm_comm_info* out) {
-  return lmm_communicate_ex(s, id, model, n_route, route_cnst, route_bw, route_lat, nullptr, n_back, back_cnst, rate,
-                            tcp_gamma, paid, out);
+  return lmm_communicate_ex(s, id, model, n_route, route_cnst, route_bw, route_lat, nullptr, n_back, back_cnst,
+                            n_back > 0, rate, tcp_gamma, paid, out);
 }
 
 }  // extern "C"

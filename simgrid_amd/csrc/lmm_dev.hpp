@@ -38,10 +38,6 @@ enum : int {
   // fair bottleneck: the reference's work summed over the rounds, three uint64 words:
   // elements of the listed constraints, listed variables, listed constraints (words 24..29)
   CTL_FBW = 24,
-  // multi-launch maxmin, target-ordered rows: alive rows counted by the regroup (srt_prep -> srt_flip)
-  CTL_SORTN = 30,
-  // fair bottleneck, one context: the long-chain queue head of the round's fbk_update_seq (reset by fbk_share)
-  CTL_FBLQ = 31,
   CTL_WORDS = 32
 };
 
@@ -101,18 +97,6 @@ template <class T> __device__ __forceinline__ void st_rlx(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// A ready candidate listed by the update (round engine, LMMHIP_SATENT): what the saturation needs of the
-// constraint besides its readiness — its ratio (the level its variables are fixed at) and its CSC range — so
-// the saturation reads them with the entry instead of gathering them after it.
-struct alignas(16) SatEnt {
-  double ratio;
-  int32_t c;
-  uint32_t beg, end;
-  int32_t dup;
-  int32_t pad[2];
-};
-static_assert(sizeof(SatEnt) == 32, "SatEnt is two 16-B loads");
-
 struct Dev {
   int32_t nV, nC;
   int64_t nnz;
@@ -167,7 +151,6 @@ struct Dev {
   const int32_t* ccol[3];
   int32_t* rtgt[3];  // per row: constraint the variable votes for; kUnvoted / kRetired
   uint16_t* skey[3];  // per row: min key over the row's OTHER constraints at its last vote (0 if bounded)
-  uint32_t* rend[3];  // target-ordered buffers 1 / 2: end of the row's CSR range (crow holds its start)
   int32_t* bsum;    // compaction scratch: per-block rows / elems (2 x blocks)
   // fair bottleneck: CSC chunks (lmm_fb_kernels.hpp) and the per-constraint exchange buffers
   int32_t nch;               // number of chunks
@@ -186,12 +169,6 @@ struct Dev {
   int32_t* vperm;            // [nV] position of each variable in the locality order
   int32_t* csc_vp;           // [nnz] csc_v through vperm
   double* mu_p;              // [nV] mu (vtmp) in the locality order
-  // multi-launch maxmin, target-ordered rows (mm_vote_tgt): regroup scratch — sort keys (the
-  // voted constraint / 16) and packed values (variable id, floor, low target bits), radix-sorted by hipCUB
-  uint32_t* sk_in;
-  uint32_t* sk_out;
-  unsigned long long* sv_in;
-  unsigned long long* sv_out;
   uint64_t* flagbits;  // [nC/64 + 2] measurement only: targets of the rows the filter queued (kDiag)
   // frontier engine (lmm_frontier_kernels.hpp): votes registered at their target constraint
   const int2* csr_cs;        // [nnz] per CSR element: its constraint and its CSC position (one 8-B pair)
@@ -202,13 +179,9 @@ struct Dev {
   unsigned long long* fq_a;  // [nnz] re-vote queue, one segment per fr_update workgroup: variable | target << 32
   unsigned long long* fq_b;  // [nnz]   and the variable's CSR row (begin | end << 32)
   int32_t* fq_n;             // [nC / kFB + 1] queued variables per segment
-  // multi-launch engine (round 4): the alive row of each variable in the buffer in use (maintained by
-  // mm_init_vars and cmp_write), so that mm_saturate retires the rows of the variables it fixes (null: off)
-  int32_t* rowof;
   int32_t* rdq[2];   // round engine, short rows (LMMHIP_RDQ): constraints the vote made ready, by round parity
   int32_t* rqst;     // [nC] the round a constraint was last queued for (one entry per constraint and round)
   int32_t* useg;     // [blocks x kUSeg] the update's ready candidates for the next round, a segment per workgroup
-  struct SatEnt* uent;  // (LMMHIP_SATENT) the same candidates as records: ratio and CSC range with the id
   int32_t* ucnt;     // [blocks] their counts
   uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words

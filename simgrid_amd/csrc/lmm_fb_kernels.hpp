@@ -141,7 +141,6 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
     s.ctl[CTL_ROUNDS] += 1;
-    s.ctl[CTL_FBLQ] = 0;  // fbk_update_seq's long-chain queue of this round
   }
   unsigned long long ne = 0, nc = 0;  // this round's listed constraints and their elements (measurement)
   for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {
@@ -304,50 +303,6 @@ __global__ void __launch_bounds__(kBlock) fbp_csc(Dev s) {
     s.csc_vp[j] = s.vperm[s.csc_v[j]];
 }
 
-// Renumbered variables (one context, round 4): the solve runs on a copy of the CSR whose rows are in the
-// locality order of fb_perm (new id n = vperm[old], order[n] = old), so every per-variable pass — the row
-// minima of fb_var_inc, the listed tests of fbk_count, the delisting stores of fbk_unlist — gets the locality
-// the chains' mu gathers already had; the CSC keeps the reference's element order with csc_v -> csc_vp.  The
-// values are the same bytes (every variable's arithmetic is its own); fbr_unperm writes them back in order.
-__global__ void __launch_bounds__(kBlock) fbr_len(Dev s, const int32_t* __restrict__ order, uint32_t* plen) {
-  for (int64_t n = int64_t(blockIdx.x) * kBlock + threadIdx.x; n <= s.nV; n += int64_t(gridDim.x) * kBlock) {
-    if (n == s.nV) {
-      plen[n] = 0;
-      continue;
-    }
-    const int32_t v = order[n];
-    plen[n] = s.var_ptr[v + 1] - s.var_ptr[v];
-  }
-}
-
-__global__ void __launch_bounds__(kBlock) fbr_rows(Dev s, const int32_t* __restrict__ order,
-                                                   const uint32_t* __restrict__ pvp, int32_t* pc, double* pw) {
-  for (int64_t n = int64_t(blockIdx.x) * kBlock + threadIdx.x; n < s.nV; n += int64_t(gridDim.x) * kBlock) {
-    const int32_t v = order[n];
-    const uint32_t b = s.var_ptr[v], e = s.var_ptr[v + 1], o = pvp[n];
-    for (uint32_t j = b; j < e; j++) {
-      pc[o + (j - b)] = s.csr_c[j];
-      pw[o + (j - b)] = s.csr_w[j];
-    }
-  }
-}
-
-// Per solve (penalties and bounds may move between solves): the per-variable inputs in the new order.
-__global__ void __launch_bounds__(kBlock) fbr_vars(Dev s, const int32_t* __restrict__ order, double* ppen,
-                                                   double* pvb) {
-  for (int64_t n = int64_t(blockIdx.x) * kBlock + threadIdx.x; n < s.nV; n += int64_t(gridDim.x) * kBlock) {
-    const int32_t v = order[n];
-    ppen[n] = s.pen[v];
-    pvb[n] = s.vbound[v];
-  }
-}
-
-// After the solve: x[old] = px[vperm[old]] (s: the context's own arrays).
-__global__ void __launch_bounds__(kBlock) fbr_unperm(Dev s, const double* __restrict__ px) {
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock)
-    s.x[v] = px[s.vperm[v]];
-}
-
 // :107-127 — per chunk of a listed constraint.  FATPIPE: min of w*mu over ALL its elements (the stale mu of
 // variables that already left the list included) -> pacc.  Shared: the increments w * mu in CSC order into
 // fbd (element-parallel, all gathers of the round spread over the chip), which fbk_update_seq then chains
@@ -357,8 +312,6 @@ __global__ void __launch_bounds__(kBlock) fbr_unperm(Dev s, const double* __rest
 // fb_var_inc.
 // Shared constraints shorter than `longmin` elements take their increments in fbk_update_seq itself (fb_chain_pull);
 // only the long ones, whose chains are the round's critical path, get them precomputed here.
-// (streammin <= longmin, LMMHIP_FB_STREAM: shared constraints from this length on get their increments here too, and
-// their wave streams them in fbk_update_seq — fb_chain — instead of pulling mu itself)
 __global__ void __launch_bounds__(kBlock) fbk_acc(Dev s, int all, uint32_t longmin) {  // all: round 0, every variable listed
   if (s.ctl[CTL_DONE])
     return;
@@ -679,31 +632,6 @@ __global__ void __launch_bounds__(kBlock) fb_long_list(Dev s, uint32_t longmin) 
 
 constexpr int kLongBlocks = 128;  // workgroups of fbk_update_seq that take the long constraints (default)
 
-// The long list longest first (one workgroup, up to kLongSortMax entries; a longer list stays in list order):
-// the workgroups of fbk_update_seq then take the chains from a queue in that order (longest-processing-time
-// first), so no workgroup is left with two of the longest chains while others idle.  Rank of entry i = the
-// entries longer than it, or as long with a smaller constraint id: a permutation, the same for every run.
-constexpr int kLongSortMax = 4096;
-__global__ void __launch_bounds__(1024) fb_long_sort(Dev s) {
-  __shared__ int32_t ids[kLongSortMax];
-  __shared__ uint32_t len[kLongSortMax];
-  const int n = s.fb_long[0];
-  if (n > kLongSortMax)
-    return;
-  for (int i = threadIdx.x; i < n; i += 1024) {
-    const int32_t c = s.fb_long[1 + i];
-    ids[i] = c;
-    len[i] = s.cnst_ptr[c + 1] - s.cnst_ptr[c];
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += 1024) {
-    int rank = 0;
-    for (int j = 0; j < n; j++)
-      rank += len[j] > len[i] || (len[j] == len[i] && ids[j] < ids[i]);
-    s.fb_long[1 + rank] = ids[i];
-  }
-}
-
 // Block-wide (kBlock threads) exclusive scan of an int64 per thread; *tot = the block total.
 __device__ __forceinline__ long long fb_block_scan64(long long v, long long* ws, long long* tot) {
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -871,29 +799,16 @@ __device__ void fb_long_chain(const Dev& s, int32_t c, double prec, double* sh) 
 // workgroup each (fb_long_chain, from fbk_acc's increments in fbd); the others one wave per listed constraint:
 // shorter shared ones through fb_chain_pull, FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0
 // erases the constraint (:129).
-// nlb: the workgroups that take the long chains; dyn: they take them from the queue CTL_FBLQ (the list sorted
-// longest first by fb_long_sort) instead of the static stride i = b, b + nlb, ...
-__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin, uint32_t streammin,
-                                                         int nlb, int dyn) {
+// nlb: the workgroups that take the long chains (list entries b, b + nlb, ...).  Round 5 measured taking them
+// longest first from a queue (LMMHIP_FB_LPT): 8.38 vs 8.35-8.37 ms on C5, removed in round 6.
+__global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin, int nlb) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ __attribute__((aligned(16))) double dl[kBlock / kWave][kSeqP * kWave];
-  __shared__ int qi;
   if (int(blockIdx.x) < nlb) {
     const int nl = s.fb_long[0];
-    for (int i = blockIdx.x;;) {  // block-uniform
-      if (dyn) {
-        __syncthreads();  // (qi's last reader is done)
-        if (threadIdx.x == 0)
-          qi = atomicAdd(&s.ctl[CTL_FBLQ], 1);
-        __syncthreads();
-        i = qi;
-      }
-      if (i >= nl)
-        break;
+    for (int i = blockIdx.x; i < nl; i += nlb) {  // block-uniform
       const int32_t c = s.fb_long[1 + i];
-      if (!dyn)
-        i += nlb;
       if (s.ratio[c] != 0.0) {
         if (threadIdx.x == 0)
           s.erased[c] = 0;
@@ -921,8 +836,6 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uin
       rem = fb_fat_update(s, c, rem, s.xmin[c], prec, &u);
       if (lane == 0)
         s.use[c] = u;
-    } else if (ce - cb >= streammin) {  // increments written by fbk_acc (LMMHIP_FB_STREAM)
-      rem = fb_chain(s.fbd, cb, ce, rem, prec, d, lane);
     } else {
       rem = fb_chain_pull(s, cb, ce, rem, prec, d, lane);
     }

@@ -24,11 +24,9 @@
 #include "lmm_maxmin_kernels.hpp"
 #include "lmm_persist_kernels.hpp"
 #include "lmm_frontier_kernels.hpp"
-#include "lmm_frontier_persist.hpp"
 #include "lmm_batch_kernels.hpp"
 #include "lmm_resident_kernels.hpp"
 #include "lmm_cc_kernels.hpp"
-#include "lmm_tail_kernels.hpp"
 #include "lmm_scan.hpp"
 
 using namespace lmmdev;
@@ -36,8 +34,6 @@ using namespace lmmdev;
 constexpr unsigned kPersistProfCap = 1 << 16;  // barriers covered by lmmhip_persist_profile
 constexpr int64_t kAutoPersistVars = 1 << 18;   // LMMHIP_ENGINE_AUTO: one of the single-GPU small-system engines up to
 constexpr int64_t kAutoPersistMaxVars = 1 << 14;  // this many variables: persistent up to 2^14, frontier above
-constexpr int kSatEntDefault = 0;  // LMMHIP_SATENT default (the update's ready candidates as records)
-constexpr int64_t kTailRows = 0;  // LMMHIP_TAIL_ROWS default: alive rows at which a solve's tail is handed off
 
 namespace {
 
@@ -125,8 +121,6 @@ struct lmmhip_ctx {
   int64_t fb_round = 0;
   uint32_t fb_longmin = 0;  // solve_fair: shared constraints with >= this many elements use fbk_acc's increments
   int fb_nlb = 128;          // solve_fair: fbk_update_seq workgroups for the long chains
-  int fb_lpt = 0;            // solve_fair: long chains longest first from a queue (fb_long_sort)
-  uint32_t fb_streammin = 1u << 30;  // solve_fair: ... and from this length on their waves stream them (fb_chain)
   double fb_prec = 0;
   bool fb_shard = false;
   FbOwner fbo{};                   // sharded solve: the owned constraints (lmmhip_fb_shard_owner)
@@ -151,8 +145,8 @@ struct lmmhip_ctx {
   FlatBufs fb_last{};
   int tune_upd = 0, tune_sat = 0;
   double* pin_vals = nullptr;  // pinned host staging of lmmhip_res_values_pinned
-  uint8_t* pin_rst = nullptr;
-  int64_t pin_cap = 0;  // launch-width caps of the round kernels (0 = none)
+  uint8_t* pin_rst = nullptr;  // (lmmhip_res_values_pinned only: the sliced fetch marks kept slots in the values)
+  int64_t pin_cap = 0, pin_rst_cap = 0;  // capacities of pin_vals / pin_rst (elements)
   int64_t fcap[4] = {0, 0, 0, 0};               // capacities of the flat-system buffers (nV, nC, nnz, nch)
   int64_t res_flat_nv = 0;                      // variable slots covered by that flatten
   // refresh path of lmmhip_res_flatten: the last flatten's list and precision, host-side structural
@@ -168,30 +162,19 @@ struct lmmhip_ctx {
   // (CSR -> CSC position map, written by the device flatten's transpose) matches the uploaded structure
   Scr rs_vlist, rs_c2c;
   int64_t res_vl_n = 0;
+  bool res_pen_dirty = false;  // lmmhip_update_vars wrote penalties behind the mirror's back: recompute csc_u / csc_p
   bool res_c2c_ok = false;
   int res_flat_kind = LMMHIP_KIND_MAXMIN;  // solver the last resident flatten built for
   Scr sat_out, tv_out;  // lmmhip_get_saturated / lmmhip_get_touched_vars staging
   Scr cc_par, cc_flag, cc_rank, cc_out;  // lmmhip_components
-  Scr tg_kin, tg_kout, tg_vin, tg_vout, tg_tmp;  // multi-launch engine: regroup of target-ordered rows
   Scr fb_longl;                                   // solve_fair: the long shared constraints (fb_long_list)
   Scr fbp_k0, fbp_k1, fbp_v0, fbp_v1, fbp_tmp, fbp_perm, fbp_cscvp, fbp_mu;  // solve_fair: locality order (fb_perm)
   bool fb_perm_ok = false;                        // the order matches the uploaded system
-  Scr fbr_vp, fbr_c, fbr_w, fbr_pen, fbr_vb, fbr_x;  // solve_fair: the renumbered CSR copy (fb_renum)
-  bool fb_renum_ok = false;
   // frontier engine (lmm_frontier_kernels.hpp): CSR -> CSC map of the uploaded structure, vote slots, floors,
   // re-vote queue; the map and the largest CSC degree are rebuilt after every structural change
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
-  Scr mm_rowof;  // solve_maxmin: alive row of each variable (saturation retires fixed variables' rows)
-  // tail hand-off (lmm_tail_kernels.hpp, LMMHIP_TAIL_ROWS): the child context the remaining system moves to,
-  // its scratch (flags, scans, sort pairs, the parent id of each child variable), this context's role
-  lmmhip_ctx* tail = nullptr;
-  bool cont = false;          // this context continues a handed-off solve: init from the copied state
-  int64_t tail_handoffs = 0;  // solves whose tail was handed off
-  int64_t tail_round = -1;    // the parent round of the last hand-off
-  Scr tl_cf, tl_cmap, tl_rl, tl_rlo, tl_rf, tl_rvo, tl_sk0, tl_sk1, tl_sv0, tl_sv1, tl_tmp, tl_vmap, tl_cnt;
   Scr mm_crec[3];  // solve_maxmin: packed row records (LMMHIP_CREC)
   Scr mm_rdq[2], mm_rqst, mm_useg, mm_ucnt;  // solve_maxmin: ready queue / update segments (LMMHIP_RDQ)
-  Scr mm_uent;  // solve_maxmin: the update segments as records (LMMHIP_SATENT)
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
@@ -317,10 +300,6 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
   if (c->own_stream && c->own_stream != c->stream)
     (void)hipStreamSynchronize(c->own_stream);
-  if (c->tail) {  // (runs on this context's stream: destroyed first)
-    lmmhip_ctx_destroy(c->tail);
-    c->tail = nullptr;
-  }
   for (hipStream_t st : c->retired_streams) {  // a persistent launch whose rendezvous closed: its late workgroups
     (void)hipStreamSynchronize(st);           // still read the barrier words
     (void)hipStreamDestroy(st);
@@ -334,7 +313,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->tg_kin, &c->tg_kout, &c->tg_vin, &c->tg_vout, &c->tg_tmp, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fbr_vp, &c->fbr_c, &c->fbr_w, &c->fbr_pen, &c->fbr_vb, &c->fbr_x, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_rowof, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->mm_uent, &c->tl_cf, &c->tl_cmap, &c->tl_rl, &c->tl_rlo, &c->tl_rf, &c->tl_rvo, &c->tl_sk0, &c->tl_sk1, &c->tl_sv0, &c->tl_sv1, &c->tl_tmp, &c->tl_vmap, &c->tl_cnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc, &c->rs_vlist, &c->rs_c2c})
@@ -428,9 +407,6 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
     rc |= dalloc(c, &d.rtgt[b], nV);
     rc |= dalloc(c, &d.skey[b], nV);
   }
-  d.rend[0] = nullptr;
-  rc |= dalloc(c, &d.rend[1], nV);
-  rc |= dalloc(c, &d.rend[2], nV);
   rc |= dalloc(c, &d.chg, nC);
   rc |= dalloc(c, &d.chgbits, (nC + 127) / 128 * 2 + 2);
   rc |= dalloc(c, &d.flagbits, (nC + 127) / 128 * 2 + 2);
@@ -522,7 +498,6 @@ static int alloc_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, int64_
 static int finish_flat(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, bool elem_done = false) {
   Dev& d = c->d;
   c->fb_perm_ok = false;
-  c->fb_renum_ok = false;
   c->fr_map_ok = false;
   c->res_c2c_ok = false;  // (a resident flatten sets it again once finish_flat returns)
   const double mean = nV > 0 ? double(nnz) / double(nV) : 1.0;
@@ -684,6 +659,12 @@ int lmmhip_update_vars(lmmhip_ctx* c, const double* penalty, const double* var_b
   if (var_bound && c->d.nV)
     HIPCHK(
         hipMemcpyAsync((void*)c->d.vbound, var_bound, sizeof(double) * c->d.nV, hipMemcpyHostToDevice, c->stream));
+  // the dense penalties / bounds (and csc_u / csc_p) no longer match the resident records for variables the delta
+  // list does not name: the next resident refresh must rewrite every member
+  if (penalty || var_bound)
+    c->res_vl_n = -1;
+  if (penalty)
+    c->res_pen_dirty = true;
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -957,10 +938,11 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
                     static_cast<const int32_t*>(c->rs_c2c.p), d.csc_w, d.csc_u, d.csc_p, int(flags & kResPenalty));
       } else {
         RS_LAUNCH(rs_refresh_v, nvs, nvs, r, vm, dv, const_cast<double*>(d.pen), const_cast<double*>(d.vbound));
-        if ((flags & kResPenalty) && d.nnz > 0)
+        if (((flags & kResPenalty) || c->res_pen_dirty) && d.nnz > 0)
           RS_LAUNCH(mm_elem_usage, d.nnz, d, 0);
       }
       c->res_vl_n = 0;
+      c->res_pen_dirty = false;
       HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
       HIPCHK(hipMemsetAsync(c->res_dirty + 3, 0, sizeof(int32_t), c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
@@ -1102,6 +1084,7 @@ static int res_flatten(lmmhip_ctx* c, bool fair, int64_t n_list, const int32_t* 
   c->res_struct_host = false;
   c->res_c2c_ok = !fair;
   c->res_vl_n = 0;
+  c->res_pen_dirty = false;
   if (c->res_dirty) {
     HIPCHK(hipMemsetAsync(c->res_dirty, 0, sizeof(int32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->res_dirty + 3, 0, sizeof(int32_t), c->stream));
@@ -1139,25 +1122,42 @@ int lmmhip_res_cross_refreshes(lmmhip_ctx* c, int64_t* n) {
   return 0;
 }
 
+}  // extern "C"
+
+// Pinned host staging of the value fetch, grown with 1/4 headroom (the headroom was computed after the
+// capacity had been reset); the reset flags only for lmmhip_res_values_pinned.
+static int pin_grow(lmmhip_ctx* c, int64_t n, bool with_rst) {
+  if (n > c->pin_cap) {
+    const int64_t cap = std::max(n, c->pin_cap + c->pin_cap / 4);
+    if (c->pin_vals)
+      HIPCHK(hipHostFree(c->pin_vals));
+    c->pin_vals = nullptr;
+    c->pin_cap = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_vals), size_t(cap) * sizeof(double), hipHostMallocDefault));
+    c->pin_cap = cap;
+  }
+  if (with_rst && n > c->pin_rst_cap) {
+    const int64_t cap = std::max(n, c->pin_rst_cap + c->pin_rst_cap / 4);
+    if (c->pin_rst)
+      HIPCHK(hipHostFree(c->pin_rst));
+    c->pin_rst = nullptr;
+    c->pin_rst_cap = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_rst), size_t(cap), hipHostMallocDefault));
+    c->pin_rst_cap = cap;
+  }
+  return 0;
+}
+
+extern "C" {
+
 int lmmhip_res_values_pinned(lmmhip_ctx* c, int64_t n, const double** values, const uint8_t** reset) {
   if (!c || !c->uploaded || !c->res_flat)
     return fail(LMMHIP_E_STATE, "no resident flatten to read values from");
   if (n != c->res_flat_nv || !values || !reset)
     return fail(LMMHIP_E_ARG, "values: n must be the variable slot count of the last resident flatten");
   HIPCHK(hipSetDevice(c->device));
-  if (n > c->pin_cap) {
-    if (c->pin_vals)
-      HIPCHK(hipHostFree(c->pin_vals));
-    if (c->pin_rst)
-      HIPCHK(hipHostFree(c->pin_rst));
-    c->pin_vals = nullptr;
-    c->pin_rst = nullptr;
-    c->pin_cap = 0;
-    const int64_t cap = std::max(n, c->pin_cap + c->pin_cap / 4);
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_vals), size_t(cap) * sizeof(double), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_rst), size_t(cap), hipHostMallocDefault));
-    c->pin_cap = cap;
-  }
+  if (int rc = pin_grow(c, n, true))
+    return rc;
   double* vout = nullptr;
   if (int rc = scratch(c, c->rs_vout, n, &vout))
     return rc;
@@ -1181,19 +1181,8 @@ int lmmhip_res_values_sliced(lmmhip_ctx* c, int64_t n, int nslices, const double
   if (n != c->res_flat_nv || !values || nslices < 1 || nslices > 256)
     return fail(LMMHIP_E_ARG, "values: n must be the last resident flatten's slot count, 1 <= nslices <= 256");
   HIPCHK(hipSetDevice(c->device));
-  if (n > c->pin_cap) {
-    if (c->pin_vals)
-      HIPCHK(hipHostFree(c->pin_vals));
-    if (c->pin_rst)
-      HIPCHK(hipHostFree(c->pin_rst));
-    c->pin_vals = nullptr;
-    c->pin_rst = nullptr;
-    c->pin_cap = 0;
-    const int64_t cap = std::max(n, c->pin_cap + c->pin_cap / 4);
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_vals), size_t(cap) * sizeof(double), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin_rst), size_t(cap), hipHostMallocDefault));
-    c->pin_cap = cap;
-  }
+  if (int rc = pin_grow(c, n, false))
+    return rc;
   while (int(c->ev_slice.size()) < nslices) {
     hipEvent_t ev;
     HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1285,7 +1274,6 @@ int lmmhip_set_profiling(lmmhip_ctx* c, int on) {
 }
 
 static int solve_maxmin(lmmhip_ctx* c, double prec);
-static int solve_tail(lmmhip_ctx* c, double prec, int64_t nh);
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec);
 static int solve_maxmin_frontier(lmmhip_ctx* c, double prec);
 static int solve_fair(lmmhip_ctx* c, double prec);
@@ -1442,18 +1430,16 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   struct RowofOff {  // the other engines never see the row map / row records (their compactions do not
     Dev& d;          // maintain them)
     ~RowofOff() {
-      d.rowof = nullptr;
       d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
       d.rdq[0] = d.rdq[1] = nullptr;
       d.rqst = d.useg = d.ucnt = nullptr;
-      d.uent = nullptr;
     }
   } rowof_off{d};
   // packed row records for the re-votes (vote_row: the row's variable and CSR range from one 8-B record and
   // its successor instead of the cvar / crow arrays, one line per re-vote less): C2 25.94-26.00 vs 26.10-26.17
-  // ms, stress 28.83 vs 29.13 (same box).  Not with the target-ordered regroups; LMMHIP_CREC=0: off.
+  // ms, stress 28.83 vs 29.13 (same box).  LMMHIP_CREC=0: off.
   d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
-  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) == 0 && env_int("LMMHIP_CREC", 1)) {
+  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_CREC", 1)) {
     for (int k = 0; k < 3; k++) {
       uint2* p = nullptr;
       if (int rc = scratch(c, c->mm_crec[k], int64_t(d.nV) + 1, &p))
@@ -1466,7 +1452,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // 25.07-25.22 vs 25.34-25.39 ms, stress 28.29 vs 28.46, same box; LMMHIP_RDQ=0: the mm_ready pass)
   d.rdq[0] = d.rdq[1] = nullptr;
   d.rqst = d.useg = d.ucnt = nullptr;
-  d.uent = nullptr;
   // (<= kMaxBlocks) Update workgroups: 4 per CU, each with a longer segment, so that the saturation's prefix over
   // the segment counts is shorter — but enough of them to keep every segment within kUSeg (LMMHIP_UPDQ_BLOCKS).
   // Round 5, same box: C2 24.52-24.54 ms against 24.84-24.85 with one per 256 constraints (2,048 at C2), stress
@@ -1489,34 +1474,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     d.rqst = st;
     d.useg = sg;
     d.ucnt = uc;
-    // the candidates as records (ratio + CSC range with the id: the saturation's readiness test overlaps its
-    // first element loads) — LMMHIP_SATENT, A/B knob
-    d.uent = nullptr;
-    if (env_int("LMMHIP_SATENT", kSatEntDefault)) {
-      SatEnt* ue = nullptr;
-      if (int rc = scratch(c, c->mm_uent, gU_rdq * kUSeg, &ue))
-        return rc;
-      d.uent = ue;
-    }
-  }
-  // the saturation retires the rows of the variables it fixes (row map kept by init / cmp_write; not with
-  // the target-ordered regroups, whose unpack would have to maintain it too).  Opt-in (LMMHIP_RETIRE=1):
-  // measured on C2 at 26.8 ms vs 26.2 ms without (the extra row-map load and store per fixed variable
-  // cost more than the re-vote rows they save -- most fixed variables' rows are already off the list).
-  d.rowof = nullptr;
-  if ((c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) == 0 && env_int("LMMHIP_RETIRE", 0)) {
-    int32_t* ro = nullptr;
-    if (int rc = scratch(c, c->mm_rowof, std::max<int64_t>(d.nV, 1), &ro))
-      return rc;
-    d.rowof = ro;
   }
   c->vote_bits = env_int("LMMHIP_VOTE_BITS", 1) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   const int gC = grid_for(d.nC, kBlock);
-  if (c->cont)  // a handed-off tail (lmm_tail_kernels.hpp): the constraint state came with the system
-    LAUNCH(0, -1, mm_init_cont, grid_for(d.nC, kBlock), kBlock, d);
-  else
-    LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
+  LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, mm_init_vars, grid_for(d.nV, kBlock), kBlock, d);
   LAUNCH(1, -1, mm_clist, std::min(gC, 2 * c->n_cu), kBlock, d, 1);
   HIPCHK(hipMemsetAsync(d.chgbits, 0, sizeof(uint64_t) * ((d.nC + 127) / 128 * 2 + 2), c->stream));
@@ -1544,29 +1506,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   const int cmp_every = env_int("LMMHIP_COMPACT_EVERY", 48);
   const int cmp_pct = env_int("LMMHIP_COMPACT_PCT", 75);
   const int cl_every = env_int("LMMHIP_CLIST_EVERY", 8);
-  // Short rows, LMMHIP_TGT=1 (measured and off by default): target-ordered alive rows
-  // (mm_vote_tgt), regrouped after the first chunk and then every tgt_every rounds by a radix sort on
-  // (target + 1) / 16, instead of the bitmap-filter vote on order-preserving compactions
-  const bool tgt = (c->group == 4 || c->group == 8) && env_int("LMMHIP_TGT", 0) != 0;
-
-  const int tgt_every = env_int("LMMHIP_TGT_EVERY", 16);
-  const uint32_t tg_dead = uint32_t((int64_t(d.nC) + 1) >> 4) + 1;
-  const int tg_bits = 32 - __builtin_clz(tg_dead);
-  void* tg_tmp = nullptr;
-  size_t tg_tb = 0;
-  if (tgt) {
-    int rc = scratch(c, c->tg_kin, d.nV, &d.sk_in);
-    rc = rc ? rc : scratch(c, c->tg_kout, d.nV, &d.sk_out);
-    rc = rc ? rc : scratch(c, c->tg_vin, d.nV, &d.sv_in);
-    rc = rc ? rc : scratch(c, c->tg_vout, d.nV, &d.sv_out);
-    if (rc)
-      return rc;
-    HIPCHK(sort_pairs_u32_u64(nullptr, tg_tb, d.sk_in, d.sk_out, d.sv_in, d.sv_out, d.nV, tg_bits, c->stream));
-    uint8_t* t = nullptr;
-    if (int rc2 = scratch(c, c->tg_tmp, int64_t(tg_tb), &t))
-      return rc2;
-    tg_tmp = t;
-  }
   // Every round fixes at least one variable (progress), so nV + 2 rounds bound it.
   const int64_t max_rounds = int64_t(d.nV) + 2;
   // Host view of the sizes (upper bounds: rows and constraints only leave), refreshed at every poll; they
@@ -1592,10 +1531,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
                                      int(int64_t(d.nV) * std::max(0, env_int("LMMHIP_CHUNK_TAIL_PCT", 5)) / 100));
   const int64_t ctail_cnst = env_int("LMMHIP_CHUNK_TAIL_CNST", 0);
   const int ctail = std::max(1, env_int("LMMHIP_CHUNK_TAIL", 4));
-  // tail hand-off (lmm_tail_kernels.hpp; LMMHIP_TAIL_ROWS, 0 = off): not from a continued solve itself, not in
-  // the profiling mode (it times this engine's launches), not with the target-ordered rows
-  const int64_t tail_rows = env_int("LMMHIP_TAIL_ROWS", kTailRows);
-  const bool tail_ok = tail_rows > 0 && !c->cont && !c->profiling && !tgt;
   bool pending = false;
   int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
   int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
@@ -1604,23 +1539,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   for (;;) {
     const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
-      if (tgt) {
-        const int gv = std::min(grid_for(nrows, kBlock * kFilt), kDiagSlot);  // (vstat: a slot per block)
-        if (c->profiling && c->vote_diag)  // measurement: the filter alone (slot 7)
-          LAUNCH(7, r, (mm_vote_tgt<kBlock, 1>), gv, kBlock, d, int(r));
-        LAUNCH(2, r, mm_vote_tgt<kBlock>, gv, kBlock, d, int(r));
-      } else if (int rc = launch_vote(c, r, nrows))
+      if (int rc = launch_vote(c, r, nrows))
         return rc;
-      if (d.rdq[0] && d.uent) {  // the update's candidates as records (LMMHIP_SATENT)
-        if (sat_k == 1)
-          LAUNCH(4, r, (mm_saturate_q<1, true>), capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_k == 2)
-          LAUNCH(4, r, (mm_saturate_q<2, true>), capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        else
-          LAUNCH(4, r, (mm_saturate_q<4, true>), capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        LAUNCH(5, r, (mm_update<true, true>), gUq, kBlock, d, int(r), prec);
-        continue;
-      }
       if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
         if (sat_k == 1)
           LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
@@ -1647,27 +1567,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       last_clist = r;
       cl = true;
     }
-    if (tgt && r - last_compact >= (last_compact == 0 ? 1 : tgt_every) && nrows > 4096) {  // regroup by target
-      const int g = grid_for(nrows, kBlock * 4);
-      LAUNCH(6, r, srt_prep, g, kBlock, d, nrows, tg_dead);
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      if (c->profiling) {
-        if (int rc = prof_event(c, &e0))
-          return rc;
-        HIPCHK(hipEventRecord(e0, c->stream));
-      }
-      HIPCHK(sort_pairs_u32_u64(tg_tmp, tg_tb, d.sk_in, d.sk_out, d.sv_in, d.sv_out, nrows, tg_bits, c->stream));
-      if (c->profiling) {
-        if (int rc = prof_event(c, &e1))
-          return rc;
-        HIPCHK(hipEventRecord(e1, c->stream));
-        c->launch_slot.push_back(6);
-        c->launch_round.push_back(int(r));
-      }
-      LAUNCH(6, r, srt_unpack, g, kBlock, d, nrows);
-      LAUNCH(6, r, srt_flip, 1, 1, d);
-      last_compact = r;
-    } else if (!tgt && r - last_compact >= cmp_every && nrows > 4096) {  // order-preserving compaction of the alive rows
+    if (r - last_compact >= cmp_every && nrows > 4096) {  // order-preserving compaction of the alive rows
       const int nblk = int((nrows + kCompactRows - 1) / kCompactRows);
       LAUNCH(6, r, cmp_count, nblk, kBlock, d);
       LAUNCH(6, r, cmp_scan, 1, 1024, d, nblk, cmp_pct);
@@ -1686,9 +1586,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
         break;
       ncl = h[CTL_NCL0 + h[CTL_CB]];
       nrows = h[CTL_NROWS + h[CTL_BUF]];
-      // few rows left: the rest of the solve on the compacted remaining system (after the queued chunk)
-      if (tail_ok && nrows <= tail_rows && r >= 2)
-        return solve_tail(c, prec, nrows);
     }
     pending = true;
     slot ^= 1;
@@ -1702,172 +1599,9 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   return poll_ctl(c);  // (the queued tail has run: final words for the stats)
 }
 
-// Tail hand-off (lmm_tail_kernels.hpp): the rest of a max-min solve on the compacted remaining system, in a child
-// context on this context's stream.  nh: the host's bound of the rows in the alive-row buffer in use.  The kernels
-// queue behind the rounds already queued; one host round trip reads the child's sizes (and whether the solve
-// ended in the meantime).
-static int solve_tail(lmmhip_ctx* c, double prec, int64_t nh) {
-  Dev& d = c->d;
-  int64_t *cf = nullptr, *cmap = nullptr, *rl = nullptr, *rlo = nullptr, *rf = nullptr, *rvo = nullptr,
-          *cnt = nullptr;
-  int rc = scratch(c, c->tl_cf, int64_t(d.nC) + 1, &cf);
-  rc = rc ? rc : scratch(c, c->tl_cmap, int64_t(d.nC) + 1, &cmap);
-  rc = rc ? rc : scratch(c, c->tl_rl, nh + 1, &rl);
-  rc = rc ? rc : scratch(c, c->tl_rlo, nh + 1, &rlo);
-  rc = rc ? rc : scratch(c, c->tl_rf, nh + 1, &rf);
-  rc = rc ? rc : scratch(c, c->tl_rvo, nh + 1, &rvo);
-  rc = rc ? rc : scratch(c, c->tl_cnt, 4, &cnt);
-  if (rc)
-    return rc;
-  LAUNCH(6, -1, tl_cflag, grid_for(int64_t(d.nC) + 1, kBlock), kBlock, d, cf);
-  if (int rc2 = dev_scan(c, cf, cmap, int64_t(d.nC) + 1))
-    return rc2;
-  LAUNCH(6, -1, tl_rowlen, grid_for(nh + 1, kBlock), kBlock, d, nh, cf, rl, rf);
-  if (int rc2 = dev_scan(c, rl, rlo, nh + 1) | dev_scan(c, rf, rvo, nh + 1))
-    return rc2;
-  HIPCHK(hipMemcpyAsync(cnt, cmap + d.nC, sizeof(int64_t), hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(cnt + 1, rlo + nh, sizeof(int64_t), hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(cnt + 2, rvo + nh, sizeof(int64_t), hipMemcpyDeviceToDevice, c->stream));
-  int64_t n3[3] = {0, 0, 0};
-  HIPCHK(hipMemcpyAsync(n3, cnt, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  if (int rc2 = poll_ctl(c))  // (synchronises: the words and the sizes)
-    return rc2;
-  if (c->h_ctl[CTL_DONE])  // the queued rounds finished the solve
-    return 0;
-  const int64_t nC2 = n3[0], nnz2 = n3[1], nV2 = n3[2];
-  const int32_t r0 = c->h_ctl[CTL_ROUNDS];  // rounds run here: the child's round 0 is this solve's round r0
-  const int32_t lastr = c->h_ctl[CTL_LASTR];
-  c->tail_handoffs += 1;
-  c->tail_round = r0;
-  if (nV2 == 0 || nC2 == 0) {  // nothing left to fix: every remaining variable drops at 0 (its value already)
-    c->h_ctl[CTL_DONE] = 1;
-    return 0;
-  }
-  if (!c->tail)
-    if (int rc2 = lmmhip_ctx_create(c->device, &c->tail))
-      return rc2;
-  lmmhip_ctx* t = c->tail;
-  t->stream = c->stream;
-  // the engine the remaining system's size calls for (AUTO; LMMHIP_TAIL_ENGINE: measurement / tests)
-  t->engine = env_int("LMMHIP_TAIL_ENGINE", LMMHIP_ENGINE_AUTO);
-  t->profiling = false;
-  FlatBufs fb;
-  if (int rc2 = alloc_flat(t, nV2, nC2, nnz2, 0, &fb))
-    return rc2;
-  uint32_t *sk0 = nullptr, *sk1 = nullptr;
-  unsigned long long *sv0 = nullptr, *sv1 = nullptr;
-  int32_t* vmap = nullptr;
-  rc = scratch(c, c->tl_sk0, nnz2, &sk0);
-  rc = rc ? rc : scratch(c, c->tl_sk1, nnz2, &sk1);
-  rc = rc ? rc : scratch(c, c->tl_sv0, nnz2, &sv0);
-  rc = rc ? rc : scratch(c, c->tl_sv1, nnz2, &sv1);
-  rc = rc ? rc : scratch(c, c->tl_vmap, nV2, &vmap);
-  if (rc)
-    return rc;
-  const Dev& td = t->d;
-  LAUNCH(6, -1, tl_rows, grid_for(nh, kBlock), kBlock, d, td, nh, cmap, cf, rlo, rvo, fb.vp, fb.csr_c, fb.csr_w,
-         fb.pen, fb.vb, fb.cvar0, vmap, sk0, sv0);
-  const int bits = nC2 > 1 ? 64 - __builtin_clzll(uint64_t(nC2 - 1)) : 1;
-  size_t tb = 0;
-  HIPCHK(sort_pairs_u32_u64(nullptr, tb, sk0, sk1, sv0, sv1, nnz2, bits, c->stream));
-  uint8_t* tmp = nullptr;
-  if (int rc2 = scratch(c, c->tl_tmp, int64_t(tb), &tmp))
-    return rc2;
-  HIPCHK(sort_pairs_u32_u64(tmp, tb, sk0, sk1, sv0, sv1, nnz2, bits, c->stream));
-  LAUNCH(6, -1, tl_csc, grid_for(std::max<int64_t>(nnz2, 1), kBlock), kBlock, nnz2, nC2, sk1, sv1, fb.csr_w,
-         fb.csc_v, fb.csc_w, fb.cp);
-  LAUNCH(6, -1, tl_cnsts, grid_for(d.nC, kBlock), kBlock, d, td, cmap, cf, fb.cb, fb.cf);
-  if (int rc2 = finish_flat(t, nV2, nC2, nnz2))  // per-element usage, CSR rows, duplicates, launch shape
-    return rc2;
-  t->cont = true;
-  const int rct = lmmhip_solve(t, LMMHIP_KIND_MAXMIN, prec);
-  t->cont = false;
-  if (rct)
-    return rct;
-  LAUNCH(6, -1, tl_scatter, grid_for(nV2, kBlock), kBlock, d, t->d, vmap, r0);
-  const int32_t tr = t->h_ctl[CTL_ROUNDS];
-  c->h_ctl[CTL_ROUNDS] = r0 + tr;
-  c->h_ctl[CTL_LASTR] = tr > 0 ? r0 + t->h_ctl[CTL_LASTR] : lastr;
-  c->h_ctl[CTL_DONE] = 1;
-  return 0;
-}
-
 // Frontier engine (lmm_frontier_kernels.hpp): three launches per round, work proportional to the touched
 // constraints and the moving votes.  Slots: 2 fr_vote, 4 fr_sat (+ fr_sat_big), 5 fr_update, 6 the per-chunk
 // control-word copy; 0 / 1 init.
-// The frontier engine's rounds in one persistent launch (lmm_frontier_persist.hpp, LMMHIP_FR_PERSIST), queued
-// after round 0's vote: serialised per device with the other persistent launches (g_persist_mu), the same launch
-// rendezvous with a deadline.  *closed: the rendezvous closed — nothing of the launch ran, the caller continues
-// with the multi-launch rounds from round 0's saturation.  A grid-barrier timeout (CTL_ERR 1) is returned as
-// LMMHIP_E_HIP with CTL_ERR left at 1: the caller re-runs the whole solve.
-static int frontier_persist_launch(lmmhip_ctx* c, const Dev& d, double prec, int spb, int bigch, int bigw, bool big,
-                                   bool long_rows, bool* closed) {
-  const void* kern = long_rows ? reinterpret_cast<const void*>(&fr_persist<16>)
-                               : reinterpret_cast<const void*>(&fr_persist<8>);
-  if (!c->pbar)
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->pbar), BAR_WORDS * sizeof(unsigned)));
-  int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kFB, 0));
-  if (per_cu < 1)
-    return fail(LMMHIP_E_HIP, "persistent frontier kernel: no workgroup fits a CU (occupancy query)");
-  const int64_t nblk = (int64_t(d.nC) + kFB - 1) / kFB;
-  // workgroups: one per CU at most (the grid barriers' cost grows with the arrivals), no more than the
-  // multi-launch grid's workgroups (LMMHIP_FRP_GRID, A/B knob)
-  int grid = int(std::min<int64_t>(std::max<int64_t>(1, nblk), c->n_cu));
-  grid = std::max(1, std::min(env_int("LMMHIP_FRP_GRID", grid), c->n_cu * per_cu));
-  const int max_rounds = int(std::min<int64_t>(int64_t(d.nV) + 2, INT32_MAX - 1));
-  long long rdv_ticks = 100000LL * env_int("LMMHIP_PERSIST_RDV_MS", 20);  // 100 MHz wall clock
-  int32_t* hflag = c->d_rdv;
-  unsigned* barw = c->pbar;
-  Dev dd = d;
-  int ibig = big ? 1 : 0;
-  void* args[] = {&dd, &barw, &prec, const_cast<int*>(&max_rounds), &spb, &bigch, &bigw, &ibig, &rdv_ticks, &hflag};
-  {
-    std::lock_guard<std::mutex> lk(g_persist_mu);
-    hipEvent_t& last = g_persist_last[c->device];
-    if (last && hipStreamWaitEvent(c->stream, last, 0) != hipSuccess) {  // (a stale event: make a new one)
-      (void)hipGetLastError();
-      (void)hipEventDestroy(last);
-      last = nullptr;
-    }
-    if (!last)
-      HIPCHK(hipEventCreateWithFlags(&last, hipEventDisableTiming));
-    HIPCHK(hipMemsetAsync(c->pbar, 0, BAR_WORDS * sizeof(unsigned), c->stream));
-    __atomic_store_n(c->h_rdv, 0, __ATOMIC_RELEASE);
-    HIPCHK(hipLaunchKernel(kern, dim3(grid), dim3(kFB), args, 0, c->stream));
-    HIPCHK(hipEventRecord(last, c->stream));
-  }
-  c->stats.kernel_launches[2] += 1;
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  c->ev1_done = true;
-  for (;;) {  // the launch, or its rendezvous closing (the mapped word), whichever comes first
-    const hipError_t q = hipEventQuery(c->ev1);
-    if (q == hipSuccess)
-      break;
-    if (q != hipErrorNotReady)
-      HIPCHK(q);
-    if (__atomic_load_n(c->h_rdv, __ATOMIC_ACQUIRE)) {
-      *closed = true;
-      c->ev1_done = false;
-      if (c->stream == c->own_stream) {  // (as solve_maxmin_persist_once: off the closed launch's stream)
-        hipStream_t ns = nullptr;
-        HIPCHK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
-        c->retired_streams.push_back(c->own_stream);
-        c->own_stream = c->stream = ns;
-      }
-      return 0;
-    }
-    std::this_thread::yield();
-  }
-  if (int rc = poll_ctl(c))
-    return rc;
-  if (c->h_ctl[CTL_ERR] == 1)
-    return fail(LMMHIP_E_HIP, "persistent frontier kernel: a grid-barrier wait timed out");
-  if (c->h_ctl[CTL_ERR] == 2)
-    return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
-  return 0;
-}
-
 static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   Dev d = c->d;  // (a copy: the frontier's buffers stay out of the context's Dev, which the other engines use)
   if (!c->vote_diag)  // per-round diagnostic counters only on request (LMMHIP_VOTE_DIAG): they cost atomics
@@ -1917,10 +1651,7 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
-  if (c->cont)  // a handed-off tail: the constraint state came with the system (32-bit keys from the ratios)
-    LAUNCH(0, -1, mm_init_cont, grid_for(d.nC, kBlock), kBlock, d);
-  else
-    LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
+  LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
   if (d.nnz > 0)
     HIPCHK(hipMemsetAsync(d.vslot, 0xFF, sizeof(uint32_t) * size_t(d.nnz), c->stream));  // kNoVoter
@@ -1941,41 +1672,11 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   for (int k = 0; k < 2; k++)
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
   const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
-  // the rounds in one persistent launch (LMMHIP_FR_PERSIST; not under profiling or the per-round diagnostics,
-  // which time / count per launch; not during a fallback's cooldown)
-  bool vote0 = false;
-  int frp = env_int("LMMHIP_FR_PERSIST", 0);
-  if (c->profiling || d.vstat || sat_old || mf_early)
-    frp = 0;
-  if (frp && c->persist_cool > 0) {
-    c->persist_cool -= 1;
-    frp = 0;
-  }
-  if (frp) {
-    LAUNCH(2, 0, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
-    LAUNCH(2, 0, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
-    vote0 = true;
-    c->h_ctl[CTL_ERR] = 0;
-    bool closed = false;
-    const int prc = frontier_persist_launch(c, d, prec, spb, bigch, bigw, big, long_rows, &closed);
-    if (!closed && (prc != LMMHIP_E_HIP || c->h_ctl[CTL_ERR] != 1))
-      return prc;
-    c->persist_fallbacks += 1;
-    c->persist_cool = env_int("LMMHIP_PERSIST_COOLDOWN", 64);
-    if (!closed) {  // a barrier timed out mid-solve: the whole solve again, multi-launch (cooldown)
-      HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
-      c->ev1_done = false;
-      return solve_maxmin_frontier(c, prec);
-    }
-    // closed before any store: the multi-launch rounds below continue from round 0's saturation
-  }
   for (;;) {
     for (int k = 0; k < chunk; k++, r++) {
       if (r == 0) {
-        if (!vote0) {
-          LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
-          LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
-        }
+        LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
+        LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
       } else if (long_rows) {  // (LV08 routes: ~12 elements per row)
         LAUNCH(2, r, (fr_vote<false, 16>), (nblk + spb - 1) / spb, kFB, d, int(r), spb);
       } else if (mf_early) {
@@ -2026,8 +1727,6 @@ static int engine_of(const lmmhip_ctx* c) {
   // the profiling mode times every phase launch: a multi-launch engine
   if (c->profiling)
     return eng == LMMHIP_ENGINE_FRONTIER ? LMMHIP_ENGINE_FRONTIER : LMMHIP_ENGINE_ROUNDS;
-  if (c->cont && eng == LMMHIP_ENGINE_PERSISTENT)
-    return LMMHIP_ENGINE_FRONTIER;
   if (eng != LMMHIP_ENGINE_AUTO)
     return eng;
   // AUTO (measured): one launch per solve where the host round-trips and launches of the
@@ -2036,7 +1735,7 @@ static int engine_of(const lmmhip_ctx* c) {
   // grids keep 32 waves per CU in flight instead of 16
   // round 4: the frontier engine between the two (C4, 1e5 LV08 flows: 3.54 ms against 4.34 persistent and
   // 4.48 rounds), the round engine above (C2: 25.8 against 28.2 frontier)
-  if (int64_t(c->d.nV) <= kAutoPersistMaxVars && !c->cont)  // (a handed-off tail: its init is a launch of its own)
+  if (int64_t(c->d.nV) <= kAutoPersistMaxVars)
     return LMMHIP_ENGINE_PERSISTENT;
   return int64_t(c->d.nV) <= kAutoPersistVars ? LMMHIP_ENGINE_FRONTIER : LMMHIP_ENGINE_ROUNDS;
 }
@@ -2058,7 +1757,32 @@ static int engine_of(const lmmhip_ctx* c) {
 // fallback that did not stick made every later solve under sustained contention pay the wait again).
 static int solve_maxmin_persist_once(lmmhip_ctx* c, double prec, bool* closed);
 
+// Streams left behind by closed persistent launches (their late workgroups may still run): each one whose work has
+// drained is destroyed; past kRetiredCap of them the oldest is waited for (under sustained contention
+// the list grew by one stream per close without bound).
+constexpr size_t kRetiredCap = 8;
+static int reap_retired_streams(lmmhip_ctx* c) {
+  auto& v = c->retired_streams;
+  for (size_t i = 0; i < v.size();) {
+    const hipError_t q = hipStreamQuery(v[i]);
+    if (q == hipErrorNotReady) {
+      i++;
+      continue;
+    }
+    (void)hipStreamDestroy(v[i]);
+    v.erase(v.begin() + long(i));
+  }
+  while (v.size() > kRetiredCap) {
+    HIPCHK(hipStreamSynchronize(v.front()));
+    (void)hipStreamDestroy(v.front());
+    v.erase(v.begin());
+  }
+  return 0;
+}
+
 static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
+  if (int rc = reap_retired_streams(c))
+    return rc;
   if (c->persist_cool > 0) {
     c->persist_cool -= 1;
     return solve_maxmin(c, prec);
@@ -2247,7 +1971,7 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
       LAUNCH(3, r, fbo_put_mu, gV, kBlock, d, c->fbo);
       break;
     }
-    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(r == 0), std::min(c->fb_longmin, c->fb_streammin));
+    LAUNCH(4, r, fbk_acc, gQ, kBlock, d, int(r == 0), c->fb_longmin);
     LAUNCH(4, r, fbk_accc, gC, kBlock, d);
     break;
   case 2:
@@ -2258,7 +1982,7 @@ static int fb_phase(lmmhip_ctx* c, int phase) {
     }
     // one context: element by element in the CSC order, bit-identical to the reference
     LAUNCH(5, r, fbk_update_seq, c->fb_nlb + grid_for(d.nC, kBlock / kWave), kBlock, d, c->fb_prec,
-           c->fb_longmin, std::min(c->fb_longmin, c->fb_streammin), c->fb_nlb, c->fb_lpt);
+           c->fb_longmin, c->fb_nlb);
     LAUNCH(5, r, fbk_unlist, gQ, kBlock, d, int(r > 0));  // (vstb is packed in rounds > 0)
     c->fb_round++;
     break;
@@ -2317,57 +2041,6 @@ static int fb_perm(lmmhip_ctx* c) {
   return 0;
 }
 
-// The renumbered copy of the system for the one-context solve (lmm_fb_kernels.hpp fbr_*): the CSR rows in the
-// locality order of fb_perm (once per uploaded structure), the penalties and bounds every solve.  Fills `r`
-// with the Dev the rounds run on.  LMMHIP_FB_RENUM=0 keeps the original order (measurement knob).
-static int fb_renum(lmmhip_ctx* c, Dev* r, double** px) {
-  Dev& d = c->d;
-  *r = d;
-  *px = nullptr;
-  if (!d.mu_p || d.nV == 0 || !env_int("LMMHIP_FB_RENUM", 0))
-    return 0;
-  const int32_t* order = static_cast<const int32_t*>(c->fbp_v1.p);  // the sort's values: old id of new id n
-  uint32_t* pvp = nullptr;
-  int32_t* pc = nullptr;
-  double *pw = nullptr, *ppen = nullptr, *pvb = nullptr;
-  const int64_t nnz = std::max<int64_t>(d.nnz, 1);
-  int rc = scratch(c, c->fbr_vp, int64_t(d.nV) + 1, &pvp);
-  rc = rc ? rc : scratch(c, c->fbr_c, nnz, &pc);
-  rc = rc ? rc : scratch(c, c->fbr_w, nnz, &pw);
-  rc = rc ? rc : scratch(c, c->fbr_pen, d.nV, &ppen);
-  rc = rc ? rc : scratch(c, c->fbr_vb, d.nV, &pvb);
-  rc = rc ? rc : scratch(c, c->fbr_x, d.nV, px);
-  if (rc)
-    return rc;
-  if (!c->fb_renum_ok) {
-    uint32_t* plen = nullptr;
-    if ((rc = scratch(c, c->fbp_k1, int64_t(d.nV) + 1, reinterpret_cast<unsigned long long**>(&plen))))
-      return rc;  // (fb_perm's key scratch, free once the order is known)
-    hipLaunchKernelGGL(fbr_len, dim3(grid_for(int64_t(d.nV) + 1, kBlock)), dim3(kBlock), 0, c->stream, d, order, plen);
-    HIPCHK(hipGetLastError());
-    size_t tb = 0;
-    HIPCHK(scan_u32(nullptr, tb, plen, pvp, int64_t(d.nV) + 1, c->stream));
-    uint8_t* t = nullptr;
-    if ((rc = scratch(c, c->rs_tmp, int64_t(tb), &t)))
-      return rc;
-    HIPCHK(scan_u32(t, tb, plen, pvp, int64_t(d.nV) + 1, c->stream));
-    hipLaunchKernelGGL(fbr_rows, dim3(grid_for(d.nV, kBlock)), dim3(kBlock), 0, c->stream, d, order, pvp, pc, pw);
-    HIPCHK(hipGetLastError());
-    c->fb_renum_ok = true;
-  }
-  hipLaunchKernelGGL(fbr_vars, dim3(grid_for(d.nV, kBlock)), dim3(kBlock), 0, c->stream, d, order, ppen, pvb);
-  HIPCHK(hipGetLastError());
-  r->var_ptr = pvp;
-  r->csr_c = pc;
-  r->csr_w = pw;
-  r->pen = ppen;
-  r->vbound = pvb;
-  r->csc_v = d.csc_vp;
-  r->mu_p = nullptr;
-  r->x = *px;
-  return 0;
-}
-
 static int solve_fair_rounds(lmmhip_ctx* c, double prec);
 
 static int solve_fair(lmmhip_ctx* c, double prec) {
@@ -2377,9 +2050,6 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   // (fb_chain_pull).  Pulling in round 0 and streaming fbk_acc's listed-variable rewrites afterwards measured
   // 3 % slower on C5 (9.68 vs 9.42 ms, same box): the increments' gathers move, they do not go away.
   c->fb_longmin = uint32_t(std::max(0, env_int("LMMHIP_FB_LONG", 16384)));
-  // shared constraints of at least this many elements (below longmin) stream fbk_acc's increments in their wave
-  // instead of gathering mu in the chain (LMMHIP_FB_STREAM, A/B knob; default: none)
-  c->fb_streammin = uint32_t(std::max(0, env_int("LMMHIP_FB_STREAM", 1 << 30)));
   if (c->fbd_cap < c->d.nnz) {  // increments in CSC order (fbk_acc -> fbk_update_seq)
     if (int rc = dalloc(c, &c->d.fbd, c->d.nnz))
       return rc;
@@ -2391,31 +2061,13 @@ static int solve_fair(lmmhip_ctx* c, double prec) {
   hipLaunchKernelGGL(fb_long_list, dim3(grid_for(c->d.nC, kBlock)), dim3(kBlock), 0, c->stream, c->d,
                      c->fb_longmin);
   HIPCHK(hipGetLastError());
-  // the long chains longest first, taken from a queue (LMMHIP_FB_LPT, A/B knob), by LMMHIP_FB_LONGWG workgroups
-  c->fb_lpt = env_int("LMMHIP_FB_LPT", 0) != 0 ? 1 : 0;
+  // the long chains by LMMHIP_FB_LONGWG workgroups
   c->fb_nlb = std::max(1, env_int("LMMHIP_FB_LONGWG", kLongBlocks));
-  if (c->fb_lpt) {
-    hipLaunchKernelGGL(fb_long_sort, dim3(1), dim3(1024), 0, c->stream, c->d);
-    HIPCHK(hipGetLastError());
-  }
   c->d.xnb = c->xnb_own;
   c->d.xmin = c->xmin_own;
   if (int rc = fb_perm(c))
     return rc;
-  Dev rn{};
-  double* px = nullptr;
-  if (int rc = fb_renum(c, &rn, &px))
-    return rc;
-  if (!px)
-    return solve_fair_rounds(c, prec);
-  const Dev saved = c->d;  // the rounds run on the renumbered copy; the context's Dev comes back after
-  c->d = rn;
-  const int rc = solve_fair_rounds(c, prec);
-  c->d = saved;
-  if (rc)
-    return rc;
-  LAUNCH(6, c->fb_round, fbr_unperm, grid_for(c->d.nV, kBlock), kBlock, c->d, px);
-  return 0;
+  return solve_fair_rounds(c, prec);
 }
 
 static int solve_fair_rounds(lmmhip_ctx* c, double prec) {
@@ -2558,16 +2210,6 @@ int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_
     t[i] = h[i];
   *nbar = kPBlkCap;
   *nblk = c->persist_grid;
-  return 0;
-}
-
-int lmmhip_tail_handoffs(lmmhip_ctx* c, int64_t* n, int64_t* round) {
-  if (!c)
-    return fail(LMMHIP_E_ARG, "null context");
-  if (n)
-    *n = c->tail_handoffs;
-  if (round)
-    *round = c->tail_round;
   return 0;
 }
 

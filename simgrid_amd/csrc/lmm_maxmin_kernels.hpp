@@ -147,8 +147,6 @@ __device__ __forceinline__ void init_vars_range(const Dev& s, int64_t t, int64_t
     const_cast<int32_t*>(s.cvar[0])[v] = cv;
     if (kRec && s.crec[0])
       s.crec[0][v] = make_uint2(uint32_t(cv), s.var_ptr[v]);
-    if (s.rowof)
-      s.rowof[v] = int32_t(v);  // buffer 0 is the CSR itself
   }
 }
 
@@ -451,16 +449,14 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
 
 // Re-vote of one row, one lane: the first R elements in registers (their loads in flight together), longer
 // rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
-// kCsr: the row's elements are read from the CSR (target-ordered rows, mm_vote_tgt: a row keeps its variable id
-// and CSR range); otherwise from the buffer's own row copy.
 // kRec: the row's variable and CSR range from the packed records (crec; the multi-launch engine's short-row
 // vote only — other instantiations, e.g. the persistent kernel, keep their register budget).
-template <int R, bool kCsr = false, bool kRec = false, bool kRdq = false>
+template <int R, bool kRec = false, bool kRdq = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems, const uint16_t* __restrict__ key) {
   const int32_t* __restrict__ cvar = s.cvar[buf];
   const uint32_t* __restrict__ crow = s.crow[buf];
-  const int32_t* __restrict__ ccol = kCsr ? s.csr_c : s.ccol[buf];
+  const int32_t* __restrict__ ccol = s.ccol[buf];
   int32_t* __restrict__ rtgt = s.rtgt[buf];
   uint16_t* __restrict__ skey = s.skey[buf];
   // (key: s.key, or its copy in LDS — persistent engine, small systems)
@@ -474,9 +470,8 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     e = r1.y;
   } else {
     cv = cvar[row];
-    // (target-ordered buffers 1 / 2 keep each row's CSR range in crow / rend; buffer 0 is the CSR itself)
     b = crow[row];
-    e = kCsr && buf != 0 ? s.rend[buf][row] : crow[row + 1];
+    e = crow[row + 1];
   }
   const int v = rvar(cv);
   const int32_t vst = s.vstate[v];
@@ -701,13 +696,13 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
         if (kDiag == 0)
-          vote_row<R, false, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key);
+          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
   if (kDiag == 0 && lane < qn)
-    vote_row<R, false, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key);
+    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key);
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
     for (int k = 0; k < 4; k++) {
@@ -843,165 +838,6 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   }
 }
 
-// ---- multi-launch engine, short rows, TARGET-ORDERED alive rows (the default for mean row length <= 8) ----
-// The alive rows are regrouped every few rounds by the constraint they vote for (srt_prep + a hipCUB radix sort
-// + srt_unpack: a buffer then holds only the variable id, target and floor of each row; the elements are read from
-// the CSR).  The filter then reads the target keys of 64 neighbouring rows from a handful of lines (rows of one
-// constraint sit together) instead of 64 random 2-B gathers, and needs no changed-constraint bitmap: a row
-// re-votes when its target's key reached its floor (keys only grow, so an unchanged key is still below it), or
-// — sensitive rows (floor 0) — when its target was touched last round (chg stamp).  Rows that re-voted since the
-// last regroup keep their position (their gathers are random again until the next one).  The row order does not
-// change any result: a vote depends on its own row only, the vote counts are integer atomics.
-template <int R, int F, int kDiag>
-__device__ __forceinline__ int vote_waves_tgt(const Dev& s, int buf, int round, int64_t nrows, int* qw,
-                                              int* st_rows, int* st_elems) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / kWave);
-  const int32_t* __restrict__ rtgt = s.rtgt[buf];
-  const uint16_t* __restrict__ skey = s.skey[buf];
-  const uint16_t* __restrict__ key = s.key;
-  const uint16_t prev = uint16_t(round - 1);
-  const unsigned long long below = (1ull << lane) - 1;
-  int qn = 0, nq = 0;
-  // steps of F * 64 rows, strided over the waves of the grid: the rows of one constraint are neighbours, so
-  // contiguous per-wave shares would leave a constraint's whole re-vote burst to one wave
-  for (int64_t base = wave * (int64_t(F) * kWave); base < nrows; base += nwaves * (int64_t(F) * kWave)) {
-    int tt[F];
-    unsigned sk[F];
-#pragma unroll
-    for (int u = 0; u < F; u++) {
-      const int64_t row = base + u * kWave + lane;
-      tt[u] = row < nrows ? rtgt[row] : kRetired;
-      sk[u] = row < nrows ? unsigned(skey[row]) : 1u;
-    }
-    unsigned kt[F], cg[F];
-#pragma unroll
-    for (int u = 0; u < F; u++) {  // target key (floored rows) / change stamp (sensitive rows), together
-      kt[u] = tt[u] >= 0 && sk[u] != 0 ? unsigned(key[tt[u]]) : 0u;
-      cg[u] = tt[u] >= 0 && sk[u] == 0 ? unsigned(s.chg[tt[u]]) : 0x10000u;
-    }
-    unsigned needm = 0;
-#pragma unroll
-    for (int u = 0; u < F; u++) {
-      const bool need = tt[u] == kUnvoted || (tt[u] >= 0 && (sk[u] == 0 ? cg[u] == prev : kt[u] >= sk[u]));
-      needm |= unsigned(need) << u;
-    }
-#pragma unroll 1
-    for (int u = 0; u < F; u++) {
-      const bool need = (needm >> u) & 1;
-      const unsigned long long m = __ballot(need);
-      if (need)
-        qw[qn + __popcll(m & below)] = int(base + u * kWave + lane);
-      qn += __popcll(m);
-      if (qn >= kWave) {  // wave-uniform: resolve the newest 64
-        __builtin_amdgcn_wave_barrier();
-        qn -= kWave;
-        nq += kWave;
-        const int row = qw[qn + lane];
-        __builtin_amdgcn_wave_barrier();
-        if (kDiag == 0)
-          vote_row<R, true>(s, buf, round, row, st_rows, st_elems, key);
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (kDiag == 0 && lane < qn)
-    vote_row<R, true>(s, buf, round, qw[lane], st_rows, st_elems, key);
-  return nq + qn;
-}
-
-// kDiag 1 (measurement only, LMMHIP_VOTE_DIAG): the filter alone, rows queued but not resolved.
-template <int B, int kDiag = 0> __global__ void __launch_bounds__(B) mm_vote_tgt(Dev s, int round) {
-  if (s.ctl[CTL_DONE])
-    return;
-  const int buf = s.ctl[CTL_BUF];
-  __shared__ int st_rows, st_elems;
-  __shared__ int q[(B / kWave) * kQW];  // per-wave queues of rows to re-vote
-  if (s.vstat) {
-    if (threadIdx.x == 0)
-      st_rows = st_elems = 0;
-    __syncthreads();
-  }
-  vote_waves_tgt<8, kFilt, kDiag>(s, buf, round, s.ctl[CTL_NROWS + buf], q + (threadIdx.x / kWave) * kQW, &st_rows,
-                                  &st_elems);
-  if (s.vstat && kDiag == 0) {
-    __syncthreads();
-    if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
-      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x)] = st_rows;
-      s.vstat[2 * (int64_t(round) * kMaxBlocks + blockIdx.x) + 1] = st_elems;
-    }
-  }
-}
-
-// Regroup, step 1: the rows of the buffer in use as (key, value) pairs — key = (target + 1) / 16 (16 constraints'
-// keys share a line), value = variable id | floor << 32 | the target's low bits << 48; dropped rows (retired, or
-// whose variable a saturation fixed: its target died) get `dead` and sort to the end.  nh = the host's upper bound
-// of the buffer's rows (the sort's length); the alive count goes to CTL_SORTN.
-__global__ void __launch_bounds__(kBlock) srt_prep(Dev s, int64_t nh, uint32_t dead) {
-  if (s.ctl[CTL_DONE])
-    return;
-  const int in = s.ctl[CTL_BUF];
-  const int64_t n = s.ctl[CTL_NROWS + in];
-  int cnt = 0;
-  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nh; i += int64_t(gridDim.x) * kBlock) {
-    uint32_t k = dead;
-    unsigned long long val = 0;
-    if (i < n) {
-      const int t = s.rtgt[in][i];
-      const int32_t cv = s.cvar[in][i];
-      // a variable is fixed only with its target (the saturated constraint every alive element of it votes
-      // for) or at its bound (retired by its re-vote)
-      bool alive = t != kRetired;
-      if (t >= 0 && s.key[t] == kDeadKey)
-        alive = s.vstate[rvar(cv)] == 0;
-      if (alive) {
-        const uint32_t t1 = uint32_t(t + 1);
-        k = t1 >> 4;
-        val = (unsigned long long)uint32_t(cv) | ((unsigned long long)s.skey[in][i] << 32) |
-              ((unsigned long long)(t1 & 15u) << 48);
-        cnt++;
-      }
-    }
-    s.sk_in[i] = k;
-    s.sv_in[i] = val;
-  }
-  cnt = grp_isum<kWave>(cnt);
-  if ((threadIdx.x & (kWave - 1)) == 0 && cnt)
-    atomicAdd(&s.ctl[CTL_SORTN], cnt);
-}
-
-// Regroup, step 3 (after the sort): the sorted alive rows into the other buffer.
-__global__ void __launch_bounds__(kBlock) srt_unpack(Dev s, int64_t nh) {
-  if (s.ctl[CTL_DONE])
-    return;
-  const int in = s.ctl[CTL_BUF], out = in == 1 ? 2 : 1;
-  const int64_t n = s.ctl[CTL_SORTN] < nh ? s.ctl[CTL_SORTN] : nh;
-  int32_t* ovar = const_cast<int32_t*>(s.cvar[out]);
-  uint32_t* orow = const_cast<uint32_t*>(s.crow[out]);
-  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-    const uint32_t k = s.sk_out[i];
-    const unsigned long long val = s.sv_out[i];
-    const int v = rvar(int32_t(uint32_t(val)));
-    orow[i] = s.var_ptr[v];  // the row's CSR range (one gather per regroup instead of one per re-vote)
-    s.rend[out][i] = s.var_ptr[v + 1];
-    ovar[i] = int32_t(uint32_t(val));
-    s.skey[out][i] = uint16_t(val >> 32);
-    s.rtgt[out][i] = int32_t((k << 4) | uint32_t((val >> 48) & 15u)) - 1;
-  }
-}
-
-// Regroup, step 4 (one thread): switch to the regrouped buffer.
-__global__ void srt_flip(Dev s) {
-  if (s.ctl[CTL_DONE])
-    return;
-  const int in = s.ctl[CTL_BUF], out = in == 1 ? 2 : 1;
-  s.ctl[CTL_NROWS + out] = s.ctl[CTL_SORTN];
-  s.ctl[CTL_NELEM + out] = 0;  // (elements stay in the CSR)
-  s.ctl[CTL_SORTN] = 0;
-  s.ctl[CTL_BUF] = out;
-}
-
 // Round phase 2 — ready list: alive constraints every alive element votes for.  Block b scans one
 // contiguous chunk of the alive-constraint list and writes its ready constraints into its own segment
 // of `ready` (LDS counter, no global atomic); bready[b] = segment length.
@@ -1048,19 +884,11 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
 #endif
 constexpr int kSatU = LMM_KSATU;
 
-// retire (multi-launch engine, round 4): the buffer's row targets; each claimed variable's alive row (rowof) is
-// marked kRetired, so the next vote's filter skips it instead of queueing a re-vote that only finds the
-// variable fixed (~6.4e4 rows per C2 round).
-// kChk (ready candidates listed as records, LMMHIP_SATENT): the constraint's key `kc` and count `nv` were loaded by
-// the caller but not yet tested; the test is made here, after the chunk's element loads are issued (so their
-// latency overlaps), and before any store — a constraint that is no longer ready returns false untouched.
-template <bool kChk = false>
-__device__ __forceinline__ bool saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
-                                               int round, int lane, int* pre, bool dup, int32_t* retire = nullptr,
-                                               unsigned kc = 0, int nv = 0) {
+__device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
+                                               int round, int lane, int* pre, bool dup) {
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
-  int32_t lv = -1, ro = 0;
+  int32_t lv = -1;
   double lp = 1.0, lx = 0.0;
   uint32_t rb = 0, re = 0;
   if (j < ce) {
@@ -1072,11 +900,7 @@ __device__ __forceinline__ bool saturate_chunk(const Dev& s, int32_t c, double r
     rb = uint32_t(row);
     re = uint32_t(row >> 32);
   }
-  if (kChk && !(kc != kDeadKey && nv == 0))  // wave-uniform: not ready after this round's vote
-    return false;
   if (j < ce) {
-    if (retire)
-      ro = s.rowof[lv];  // (issued with the state's load)
     if (s.vstate[lv] != 0)
       lv = -1;
     else if (!dup)
@@ -1089,8 +913,6 @@ __device__ __forceinline__ bool saturate_chunk(const Dev& s, int32_t c, double r
     lx = r / lp;
     s.x[lv] = lx;
     len = int(re - rb);
-    if (retire)
-      retire[ro] = kRetired;
   } else {
     rb = re = 0;
   }
@@ -1161,7 +983,6 @@ __device__ __forceinline__ bool saturate_chunk(const Dev& s, int32_t c, double r
     }
   }
   __builtin_amdgcn_wave_barrier();
-  return true;
 }
 
 // Ready test + saturation, block-cooperative.  In pass p, wave w of workgroup b tests the 64 constraints of
@@ -1268,21 +1089,20 @@ __device__ __forceinline__ bool sat_block(const Dev& s, int round, const int32_t
 // Multi-launch engine: saturation of mm_ready's list, K waves per ready constraint (chunks k, k + K, ...)
 // spread evenly over the whole grid — the ready list is global here, so the work balances across workgroups.
 template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int32_t c, int k, int round, int lane,
-                                                              int* pre, int32_t* retire) {
+                                                              int* pre) {
   const double r = ld_rlx(&s.cst[c].ratio);  // wave-uniform address: keep it off the scalar cache
   const uint32_t ce = s.cnst_ptr[c + 1];
   const bool dup = s.cdup[c] != 0;
   for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
-    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup, retire);
+    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup);
   if (k == 0 && lane == 0)  // c leaves the light table: mm_update (the owner of key / chg) retires it
     s.ctouch[c] = 2;
 }
 // (the same with the constraint's ratio, CSC range and duplicate flag already loaded)
 template <int K> __device__ __forceinline__ void saturate_one_pre(const Dev& s, int32_t c, int k, int round, int lane,
-                                                                  int* pre, int32_t* retire, double r, uint32_t cb,
-                                                                  uint32_t ce, bool dup) {
+                                                                  int* pre, double r, uint32_t cb, uint32_t ce, bool dup) {
   for (uint32_t base = cb + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
-    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup, retire);
+    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup);
   if (k == 0 && lane == 0)
     s.ctouch[c] = 2;
 }
@@ -1334,7 +1154,6 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
   const int64_t chunk = chunk_of(s.ctl[CTL_NCL0 + cb], ready_blocks);
-  int32_t* retire = s.rowof ? s.rtgt[s.ctl[CTL_BUF]] : nullptr;
   for (int64_t g = wave; g < int64_t(total) * K; g += nwaves) {
     const int64_t i = g / K;
     const int k = int(g % K);
@@ -1343,7 +1162,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
     for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
       if (lo + step < ready_blocks && pre[lo + step] <= i)
         lo += step;
-    saturate_one<K>(s, s.ready[lo * chunk + (i - pre[lo])], k, round, lane, wpre[w], retire);
+    saturate_one<K>(s, s.ready[lo * chunk + (i - pre[lo])], k, round, lane, wpre[w]);
   }
 }
 
@@ -1358,8 +1177,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 #ifndef LMM_SATQ_SPEC
 #define LMM_SATQ_SPEC 1
 #endif
-template <int K, bool kEnt = false>
-__global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
+template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1403,7 +1221,6 @@ __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ub
   const int32_t* __restrict__ q = s.rdq[round & 1];
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  int32_t* retire = s.rowof ? s.rtgt[s.ctl[CTL_BUF]] : nullptr;
   for (int64_t g = wave; g < (int64_t(total) + nq) * K; g += nwaves) {  // wave-uniform
     const int64_t i = g / K;
     const int k = int(g % K);
@@ -1414,21 +1231,6 @@ __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ub
       for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
         if (lo + step < ublocks && pre[lo + step] <= i)
           lo += step;
-      if (kEnt) {  // the record: ratio and CSC range with the id; readiness tested inside, after the first loads
-        const SatEnt e = s.uent[int64_t(lo) * kUSeg + (i - pre[lo])];
-        const unsigned kc = s.key[e.c];
-        const int nv = s.nvote[e.c];
-        bool ok = e.beg == e.end && kc != kDeadKey && nv == 0;  // (an empty column: nothing to fix)
-        for (uint32_t base = e.beg + uint32_t(k) * kWave; base < e.end; base += K * kWave)  // wave-uniform
-          if (!(ok = saturate_chunk<true>(s, e.c, e.ratio, base, e.end, round, lane, wpre[w], e.dup != 0, retire, kc,
-                                          nv)))
-            break;
-        if (ok && k == 0 && lane == 0) {
-          s.ctouch[e.c] = 2;  // c leaves the light table: mm_update (the owner of key / chg) retires it
-          s.ctl[CTL_LASTR] = round;
-        }
-        continue;
-      }
       c = s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
     } else {
       c = q[i - total];
@@ -1445,13 +1247,13 @@ __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ub
       continue;
     if (k == 0 && lane == 0)
       s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-    saturate_one_pre<K>(s, c, k, round, lane, wpre[w], retire, r, cb, cend, dup);
+    saturate_one_pre<K>(s, c, k, round, lane, wpre[w], r, cb, cend, dup);
 #else
     if (s.key[c] == kDeadKey || s.nvote[c] != 0)
       continue;
     if (k == 0 && lane == 0)
       s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-    saturate_one<K>(s, c, k, round, lane, wpre[w], retire);
+    saturate_one<K>(s, c, k, round, lane, wpre[w]);
 #endif
   }
 }
@@ -1466,10 +1268,7 @@ __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ub
 // K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups (key and touch
 // flag, then — touched constraints only — record, flags, scale, votes) is issued before any of them is
 // used, so a wave keeps K times the memory requests in flight.
-// kEnt (LMMHIP_SATENT): the ready candidates are written as records (SatEnt: ratio, CSC range, duplicate flag)
-// straight into the workgroup's segment of s.uent; their CSC range and flag are loaded with the record of every
-// touched constraint (coalesced in identity order).
-template <int K, bool kRdq = false, bool kEnt = false>
+template <int K, bool kRdq = false>
 __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
                                              bool* touch, int* ucnt_sh = nullptr, int32_t* ulist = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -1483,16 +1282,12 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
   unsigned long long qx[K], qy[K], qz[K];
   double rem[K], use[K], bnd[K];
   int32_t ce[K], nv[K];
-  uint32_t cpb[K], cpe[K];
-  int32_t cdp[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const int64_t c = base0 + k * stride + lane;
     qx[k] = qy[k] = qz[k] = 0;
     rem[k] = use[k] = bnd[k] = 0.0;
     ce[k] = nv[k] = 0;
-    cpb[k] = cpe[k] = 0;
-    cdp[k] = 0;
     if (okey[k] != kDeadKey && tf[k] == 1) {  // an untouched constraint keeps its record as it is
       const CstRec* rec = s.cst + c;
       qx[k] = rec->drem;
@@ -1503,11 +1298,6 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       bnd[k] = rec->bound;
       ce[k] = s.cexp[c];
       nv[k] = s.nvote[c];
-      if (kEnt) {
-        cpb[k] = s.cnst_ptr[c];
-        cpe[k] = s.cnst_ptr[c + 1];
-        cdp[k] = s.cdup[c];
-      }
     }
   }
   int alive = 0;
@@ -1585,18 +1375,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
           alive++;
           if (kRdq && nvn == 0) {  // its last elements voting elsewhere left with fixed variables: ready next
             const int slot = atomicAdd(ucnt_sh, 1);  // round (the stamp keeps the vote from queueing it too)
-            if (kEnt) {
-              SatEnt e;
-              e.ratio = r;
-              e.c = int32_t(c);
-              e.beg = cpb[k];
-              e.end = cpe[k];
-              e.dup = cdp[k];
-              e.pad[0] = e.pad[1] = 0;
-              s.uent[int64_t(blockIdx.x) * kUSeg + slot] = e;
-            } else {
-              ulist[slot] = int32_t(c);
-            }
+            ulist[slot] = int32_t(c);
             s.rqst[c] = round + 1;
           }
         }
@@ -1618,14 +1397,13 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
 #ifndef LMM_UPD_K
 #define LMM_UPD_K 4
 #endif
-template <bool kRdq = false, bool kEnt = false>
-__global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_ROUNDS] += 1;
   __shared__ int alive_cnt, ucnt_sh;
-  __shared__ int32_t ulist[kRdq && !kEnt ? kUSeg : 1];
+  __shared__ int32_t ulist[kRdq ? kUSeg : 1];
   if (threadIdx.x == 0)
     alive_cnt = ucnt_sh = 0;
   __syncthreads();
@@ -1634,7 +1412,7 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
        base += LMM_UPD_K * stride)  // wave-uniform; LMM_UPD_K groups of 64 constraints per step, loads in flight together
-    alive += update_groups<LMM_UPD_K, kRdq, kEnt>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
+    alive += update_groups<LMM_UPD_K, kRdq>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
@@ -1642,7 +1420,7 @@ __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double pre
     s.balive[blockIdx.x] = alive_cnt;
   if (kRdq) {  // the workgroup's ready candidates for the next round into its segment
     const int n = ucnt_sh;
-    for (int i = threadIdx.x; i < n && !kEnt; i += kBlock)
+    for (int i = threadIdx.x; i < n; i += kBlock)
       s.useg[int64_t(blockIdx.x) * kUSeg + i] = ulist[i];
     if (threadIdx.x == 0)
       s.ucnt[blockIdx.x] = n;
@@ -1871,8 +1649,6 @@ __global__ void __launch_bounds__(kBlock) cmp_write(Dev s) {
       ovar[o] = v;
       if (s.crec[out])
         s.crec[out][o] = make_uint2(uint32_t(v), uint32_t(pe + xe));
-      if (s.rowof)
-        s.rowof[rvar(v)] = o;
       s.rtgt[out][o] = s.rtgt[in][row];
       s.skey[out][o] = s.skey[in][row];
       orow[o] = uint32_t(pe + xe);

@@ -535,8 +535,9 @@ typename B::Cnst wifi_link_constraint(B& b, int model) {
 // crosstraffic each back-route link at 0.05.  route / back: indices into `links` and `cn`.  A WIFI route link
 // (network_cm02.cpp:239-260) weighs 1 / the source station's rate, or the destination's when the source is not
 // associated with that access point (neither associated: error); its bandwidth in the weight_S sum is the link's own,
-// 1 / bandwidth factor (LinkImpl::get_bandwidth of the NetworkWifiLink).  WIFI with crosstraffic (a back route) is
-// the reference's assertion "Cross-traffic is not yet supported when using WIFI": an error here too.
+// 1 / bandwidth factor (LinkImpl::get_bandwidth of the NetworkWifiLink).  WIFI with network/crosstraffic on (the
+// `crosstraffic` flag, whether or not the back route has links) is the reference's assertion "Cross-traffic is not
+// yet supported when using WIFI" (network_cm02.cpp:242): an error here too.
 struct Comm {
   double latency;          // NetworkAction::latency_ (route latency * latency factor)
   double lat_current;      // lat_current_ (route latency)
@@ -546,7 +547,7 @@ struct Comm {
 template <class B>
 typename B::Var communicate(B& b, int model, const std::vector<Link>& links, const std::vector<typename B::Cnst>& cn,
                             const std::vector<int>& route, const std::vector<int>& back, double lat, double rate,
-                            double tcp_gamma, bool paid, Comm* out = nullptr) {
+                            double tcp_gamma, bool paid, bool crosstraffic, Comm* out = nullptr) {
   const NetFactors f = net_factors(model);
   Comm a;
   a.sharing_penalty = lat;
@@ -560,7 +561,7 @@ typename B::Var communicate(B& b, int model, const std::vector<Link>& links, con
     const Link& k = links[size_t(l)];
     if (!k.wifi)
       continue;
-    if (!back.empty())
+    if (crosstraffic)
       throw std::invalid_argument(
           "Cross-traffic is not yet supported when using WIFI. Please use --cfg=network/crosstraffic:0");
     if (k.src_rate == -1 && k.dst_rate == -1)
@@ -641,7 +642,7 @@ void flows(B& b, const Platform& plat, const Params& p, std::vector<typename B::
       if (p.crosstraffic)
         plat.route(dst, src, back, nullptr);
       // rate -1 (no user rate), in the state once the latency is paid
-      v = communicate(b, p.model, plat.links, cn, route, back, lat, -1.0, p.tcp_gamma, true);
+      v = communicate(b, p.model, plat.links, cn, route, back, lat, -1.0, p.tcp_gamma, true, p.crosstraffic);
     }
     if (var_out)
       vars.push_back(v);

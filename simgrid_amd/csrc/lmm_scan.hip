@@ -26,14 +26,6 @@ hipError_t sort_pairs_i32(void* tmp, size_t& tmp_bytes, const int32_t* keys_in, 
   return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0, end_bit, s);
 }
 
-// Target-ordered alive rows (mm_vote_tgt): 32-bit keys (the voted constraint / 16), packed 64-bit rows.
-hipError_t sort_pairs_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                              const unsigned long long* vals_in, unsigned long long* vals_out, int64_t n, int end_bit,
-                              hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out, n, 0, end_bit, s);
-}
-
-// Locality order of the FairBottleneck mu gathers (fb_perm): 64-bit keys, variable ids.
 hipError_t sort_pairs_u64_i32(void* tmp, size_t& tmp_bytes, const unsigned long long* keys_in,
                               unsigned long long* keys_out, const int32_t* vals_in, int32_t* vals_out, int64_t n,
                               int end_bit, hipStream_t s) {

@@ -13,10 +13,6 @@ hipError_t scan_u32(void* tmp, size_t& tmp_bytes, const uint32_t* in, uint32_t* 
 hipError_t sort_pairs_i32(void* tmp, size_t& tmp_bytes, const int32_t* keys_in, int32_t* keys_out,
                           const int32_t* vals_in, int32_t* vals_out, int64_t n, int end_bit, hipStream_t s);
 
-hipError_t sort_pairs_u32_u64(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                              const unsigned long long* vals_in, unsigned long long* vals_out, int64_t n, int end_bit,
-                              hipStream_t s);
-
 hipError_t sort_pairs_u64_i32(void* tmp, size_t& tmp_bytes, const unsigned long long* keys_in,
                               unsigned long long* keys_out, const int32_t* vals_in, int32_t* vals_out, int64_t n,
                               int end_bit, hipStream_t s);

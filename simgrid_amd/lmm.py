@@ -120,7 +120,7 @@ SIGNATURES = {
     "lmm_link_new": (I64, [P, I, D, I]),
     "lmm_communicate": (I64, [P, P, I, I64, PI64, PD, PD, I64, PI64, D, D, I, P]),
     "lmm_wifi_link_new": (I64, [P, I]),
-    "lmm_communicate_ex": (I64, [P, P, I, I64, PI64, PD, PD, PD, I64, PI64, D, D, I, P]),
+    "lmm_communicate_ex": (I64, [P, P, I, I64, PI64, PD, PD, PD, I64, PI64, I, D, D, I, P]),
     "lmm_device_count": (I, []),
     "lmm_last_error": (ct.c_char_p, []),
     # include/lmm/lmm_hip.h
@@ -157,7 +157,6 @@ SIGNATURES = {
     "lmmhip_ctx_use_own_stream": (I, [P]),
     "lmmhip_ctx_set_engine": (I, [P, I]),
     "lmmhip_engine_fallbacks": (I, [P, PI64]),
-    "lmmhip_tail_handoffs": (I, [P, PI64, PI64]),
     "lmmhip_persist_profile": (I, [P, I, PI64, I64, PI64]),
     "lmmhip_persist_profile_blocks": (I, [P, PI64, I64, PI64, PI64]),
     "lmmhip_fb_shard_owner": (I, [P, I64, ct.POINTER(ct.c_int32), PI64, ct.POINTER(ct.c_int32), PD,
@@ -179,6 +178,7 @@ SIGNATURES = {
     "lmmhip_actions_lazy_download": (I, [P, PD, PD, PD, ct.POINTER(ct.c_uint8)]),
     "lmmhip_device_count": (I, []),
     "lmmhip_last_error": (ct.c_char_p, []),
+    "lmmhip_build_id": (ct.c_char_p, []),
 }
 
 _lib = None
@@ -232,6 +232,11 @@ def _check_hip(rc):
     if rc != 0:
         raise LmmError(lib().lmmhip_last_error().decode())
     return rc
+
+
+def build_id():
+    """The source hash compiled into the loaded library (lmmhip_build_id, simgrid_amd/build_id.py)."""
+    return lib().lmmhip_build_id().decode()
 
 
 def set_precision(p):
@@ -503,12 +508,6 @@ class System:
         phase per round, work proportional to what changed) or ENGINE_AUTO (default)."""
         _check_hip(lib().lmmhip_ctx_set_engine(self.device_ctx(), int(engine)))
 
-    def tail_handoffs(self):
-        """(solves whose tail was handed off to a compacted child system, round of the last hand-off)."""
-        n, r = I64(), I64()
-        _check_hip(lib().lmmhip_tail_handoffs(self.device_ctx(), ct.byref(n), ct.byref(r)))
-        return n.value, r.value
-
     def engine_fallbacks(self):
         """Persistent solves of this system's context re-run by the multi-launch engine after a grid-barrier
         timeout (lmmhip_engine_fallbacks)."""
@@ -681,23 +680,26 @@ class System:
             raise LmmError(lib().lmm_last_error().decode())
         return Constraint(self, h)
 
-    def communicate(self, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False, id_=None):
+    def communicate(self, model, route, back=(), rate=-1.0, tcp_gamma=4194304.0, paid=False, id_=None,
+                    crosstraffic=None):
         """NetworkCm02Model::communicate's LMM part (lmm_communicate): route = [(Constraint, bw, lat)] in route
         order — a WIFI access point as (Constraint, bw, lat, (src_rate, dst_rate)), the stations' rates on it
         (-1: not associated; lmm_communicate_ex) —, back = the back route's Constraints (crosstraffic), id_ = the
-        variable's opaque id (an int: the action; modified_action_ids() reports it).  Returns (Variable,
+        variable's opaque id (an int: the action; modified_action_ids() reports it), crosstraffic = the
+        network/crosstraffic configuration (None: on iff `back` has links).  Returns (Variable,
         dict(latency, lat_current, sharing_penalty, bound))."""
+        xt = bool(len(back)) if crosstraffic is None else bool(crosstraffic)
         n = len(route)
         rc = np.array([r[0].h for r in route], dtype=np.int64)
         rb = np.array([r[1] for r in route], dtype=np.float64)
         rl = np.array([r[2] for r in route], dtype=np.float64)
         bc = np.array([c.h for c in back], dtype=np.int64)
         info = CommInfo()
-        if any(len(r) > 3 for r in route):
+        if any(len(r) > 3 for r in route) or xt != bool(len(back)):
             rr = np.array([r[3] if len(r) > 3 else (0.0, 0.0) for r in route], dtype=np.float64).reshape(-1)
             h = lib().lmm_communicate_ex(self.h, id_, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
                                          rl.ctypes.data_as(PD), rr.ctypes.data_as(PD), len(bc),
-                                         bc.ctypes.data_as(PI64), rate, tcp_gamma, int(paid), ct.byref(info))
+                                         bc.ctypes.data_as(PI64), int(xt), rate, tcp_gamma, int(paid), ct.byref(info))
         else:
             h = lib().lmm_communicate(self.h, id_, model, n, rc.ctypes.data_as(PI64), rb.ctypes.data_as(PD),
                                       rl.ctypes.data_as(PD), len(bc), bc.ctypes.data_as(PI64), rate, tcp_gamma,

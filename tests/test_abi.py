@@ -64,3 +64,13 @@ def build_c_drive():
 def test_c_client_compiles_against_the_headers():
     """The boundary is a C ABI: a C99 program includes both headers and links the library."""
     assert os.path.exists(build_c_drive())
+
+
+def test_build_id_matches_source_tree():
+    """Build provenance: the loaded library's lmmhip_build_id() is the hash of this tree's sources
+    (simgrid_amd/build_id.py), so a stale or foreign liblmm_amd.so is caught."""
+    from simgrid_amd import build_id as B
+
+    if os.environ.get("LMM_AMD_LIB"):
+        pytest.skip("an A/B build was loaded on purpose")
+    assert L.build_id() == B.tree_id()

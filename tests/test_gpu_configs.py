@@ -147,18 +147,12 @@ def c5_1e6_oracle():
 
 # LMMHIP_FB_LONG: shared constraints with at least this many elements chain increments precomputed by fbk_acc,
 # shorter ones compute them inside the chain (fb_chain_pull); the C5 1e6 system's longest holds ~1.6e4
-# lpt*: the long chains longest first from a queue (LMMHIP_FB_LPT=1), with 4096-element long chains (56 of them
-# at 1e6 flows), over the default 128 workgroups or 3 (each then takes many chains from the queue)
-@pytest.mark.parametrize("longmin", ["default", "0", "4096", "1000000000", "stream256", "stream4096", "lpt4096",
-                                     "lpt4096w3", "static4096w3"])
+# w3: the long chains over 3 workgroups (each then takes many of them) instead of the default 128
+@pytest.mark.parametrize("longmin", ["default", "0", "4096", "1000000000", "4096w3"])
 def test_c5_1e6_flows_vs_oracle(c5_1e6_oracle, longmin, monkeypatch):
-    if longmin.startswith("stream"):  # (LMMHIP_FB_STREAM: shorter shared constraints stream fbk_acc's increments)
-        monkeypatch.setenv("LMMHIP_FB_STREAM", longmin[6:])
-    elif longmin.startswith(("lpt", "static")):
-        monkeypatch.setenv("LMMHIP_FB_LPT", "1" if longmin.startswith("lpt") else "0")
-        monkeypatch.setenv("LMMHIP_FB_LONG", "4096")
-        if longmin.endswith("w3"):
-            monkeypatch.setenv("LMMHIP_FB_LONGWG", "3")
+    if longmin.endswith("w3"):
+        monkeypatch.setenv("LMMHIP_FB_LONG", longmin[:-2])
+        monkeypatch.setenv("LMMHIP_FB_LONGWG", "3")
     elif longmin != "default":
         monkeypatch.setenv("LMMHIP_FB_LONG", longmin)
     p, y = c5_1e6_oracle

@@ -13,7 +13,7 @@ import subprocess
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "simgrid_amd", "csrc")
 HOT = ("mm_persist", "mm_vote_lane", "mm_vote", "mm_ready", "mm_saturate", "mm_update", "mm_batch_lds",
-       "mm_init_cnsts", "cmp_write", "fbk_", "fb_var_inc", "srt_", "fr_")
+       "mm_init_cnsts", "cmp_write", "fbk_", "fb_var_inc", "fr_")
 
 
 def resource_report():

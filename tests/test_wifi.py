@@ -84,6 +84,11 @@ def test_wifi_weights_and_errors():
         err = L.LmmError if backend == "product" else ValueError
         with pytest.raises(err, match="Cross-traffic"):
             comm([(ap, 0.0, 0.0, (6e6, -1.0))], back=[wl])
+        # the assertion tests the configuration, not the back route (network_cm02.cpp:242): crosstraffic on with an
+        # empty back route fails too, and a back route is no error once the caller says crosstraffic is off
+        with pytest.raises(err, match="Cross-traffic"):
+            comm([(ap, 0.0, 0.0, (6e6, -1.0))], back=[], crosstraffic=True)
+        comm([(ap, 0.0, 0.0, (6e6, -1.0))], back=[], crosstraffic=False)
         with pytest.raises(err, match="not associated"):
             comm([(ap, 0.0, 0.0, (-1.0, -1.0))])
         if backend == "product":  # (a rate of 0 would weigh 1 / 0: refused)
