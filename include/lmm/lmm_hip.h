@@ -219,6 +219,13 @@ int lmmhip_ctx_set_engine(lmmhip_ctx* ctx, int engine);
  * engine directly.  Persistent launches of one process are serialised per device, so two Systems never starve
  * each other. */
 int lmmhip_engine_fallbacks(lmmhip_ctx* ctx, int64_t* n);
+/* Round anatomy (diagnostic builds only: make EXTRA_HIPFLAGS=-DLMM_ANAT=1; scripts/anatomy.py): in the solves run
+ * with LMMHIP_ANAT_ROUNDS="r0,r1,..." (at most 4 rounds) every wave of the round engine's vote, saturation and update
+ * launches of those rounds writes a record of 20 words — entry and exit on the 100-MHz wall clock, its workgroup,
+ * and the clock ticks it spent at each dependent level of its work (lmm_dev.hpp, lmm_anat).  *n = the words of the
+ * record array ([slot 0..3][kernel vote / saturation / update][wave 0..8191][20]); out (cap words) gets them,
+ * rounds4 the recorded rounds.  LMMHIP_E_STATE in the product build. */
+int lmmhip_anatomy(lmmhip_ctx* ctx, unsigned long long* out, int64_t cap, int64_t* n, int32_t* rounds4);
 /* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the
  * wall-clock time (100 MHz) of the last workgroup's arrival and of workgroup 0's exit.  With t != NULL,
  * copies the last solve's records: t[2i] = last arrival at barrier i, t[2i+1] = exit (barrier 0 = the

@@ -186,6 +186,10 @@ struct Dev {
   uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
+  // round anatomy (diagnostic build LMM_ANAT=1 only, else null): per-wave stamps of the round engine's kernels in
+  // the rounds anat_r[0..kAnatSlots) (lmm_anat below)
+  unsigned long long* anat;
+  int32_t anat_r[4];
 };
 
 // Alive-row variable ids carry the variable's "bounded" flag in the sign bit (set at every solve's init),
@@ -308,5 +312,67 @@ inline int grid_for(int64_t n, int per_block) {
     g = kMaxBlocks;
   return int(g);
 }
+
+// ---- round anatomy (diagnostic build only: LMM_ANAT=1, scripts/anatomy.py) ----
+// In the rounds named by Dev::anat_r, every wave of mm_vote_lane / mm_saturate_q / mm_update writes one record of
+// kAnatFields words into anat[((slot * 3 + kernel) * kAnatWaves + wave) * kAnatFields]: its entry and exit on the
+// 100-MHz wall clock (s_memrealtime, one clock for the whole chip), its workgroup, and the time it spent at each
+// dependent level of its work (the clock read waits for the level's loaded values, so a level's time is from the
+// previous stamp to the arrival of that level's data).  The stamps serialise what the real kernel overlaps: read
+// the SHARES of a round, not the stamped build's length (cdna_hip_programming.md §7, in-kernel stamps).  In the
+// product build (LMM_ANAT=0) none of this is compiled.
+#ifndef LMM_ANAT
+#define LMM_ANAT 0
+#endif
+constexpr int kAnatSlots = 4;
+constexpr int kAnatFields = 20;
+constexpr int kAnatWaves = 8192;
+enum : int { ANAT_VOTE = 0, ANAT_SAT = 1, ANAT_UPD = 2 };
+#if LMM_ANAT
+__device__ __forceinline__ unsigned long long anat_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
+// the clock read after `v` has arrived (a use of its register)
+template <class T> __device__ __forceinline__ void anat_use(const T& v) {
+  if constexpr (sizeof(T) == 8)
+    asm volatile("" : : "v"(v) : "memory");
+  else
+    asm volatile("" : : "v"(uint32_t(v)) : "memory");
+}
+// per-wave accumulators of the dependent levels (registers; a field per level), and the running stamp
+struct AnatAcc {
+  unsigned lv[10];
+  unsigned long long at;
+};
+#define ANAT_LVL(aa, i, dep)                      \
+  do {                                            \
+    anat_use(dep);                                \
+    const unsigned long long t_ = anat_now();     \
+    (aa).lv[i] += unsigned(t_ - (aa).at);         \
+    (aa).at = t_;                                 \
+  } while (0)
+__device__ __forceinline__ unsigned anat_wmax(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    v = max(v, (unsigned)__shfl_xor(int(v), o, kWave));
+  return v;
+}
+__device__ __forceinline__ int anat_slot(const Dev& s, int round) {
+  if (!s.anat)
+    return -1;
+  for (int k = 0; k < kAnatSlots; k++)
+    if (s.anat_r[k] == round)
+      return k;
+  return -1;
+}
+__device__ __forceinline__ unsigned long long* anat_rec(const Dev& s, int slot, int kernel) {
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  if (slot < 0 || wave >= kAnatWaves)
+    return nullptr;
+  return s.anat + ((int64_t(slot) * 3 + kernel) * kAnatWaves + wave) * kAnatFields;
+}
+#endif
 
 }  // namespace lmmdev

@@ -91,6 +91,7 @@ struct lmmhip_ctx {
   double last_prec = 1e-5;  // precision of the last solve (lmmhip_get_saturated)
   bool solved = false;      // a solve completed since the last upload / flatten
   int32_t* vstat = nullptr;  // profiling counters of mm_vote ([round][block] x 2)
+  unsigned long long* anat = nullptr;  // round anatomy records (LMM_ANAT builds, LMMHIP_ANAT_ROUNDS)
   // maxmin engine (lmmhip_ctx_set_engine): one persistent launch per solve (default) or the
   // multi-launch round chain; grid-barrier words of the persistent launch
   int engine = LMMHIP_ENGINE_AUTO;
@@ -339,6 +340,8 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
     (void)hipEventDestroy(ev);
   if (c->vstat)
     (void)hipFree(c->vstat);
+  if (c->anat)
+    (void)hipFree(c->anat);
   if (c->pbar)
     (void)hipFree(c->pbar);
   for (void* p : {(void*)c->bt_voff, (void*)c->bt_coff, (void*)c->bt_rounds})
@@ -1305,6 +1308,28 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   c->d.vstat = c->profiling ? c->vstat : nullptr;
   if (c->profiling)
     HIPCHK(hipMemsetAsync(c->vstat, 0, stat_bytes, c->stream));
+  // round anatomy (diagnostic builds only): the round engine's waves stamp the rounds LMMHIP_ANAT_ROUNDS names
+  c->d.anat = nullptr;
+  for (int k = 0; k < kAnatSlots; k++)
+    c->d.anat_r[k] = -1000;
+  if (LMM_ANAT && std::getenv("LMMHIP_ANAT_ROUNDS")) {
+    const size_t bytes = sizeof(unsigned long long) * size_t(kAnatSlots) * 3 * kAnatWaves * kAnatFields;
+    if (!c->anat)
+      HIPCHK(hipMalloc(&c->anat, bytes));
+    HIPCHK(hipMemsetAsync(c->anat, 0, bytes, c->stream));
+    const char* e = std::getenv("LMMHIP_ANAT_ROUNDS");
+    for (int k = 0; k < kAnatSlots; k++) {
+      char* end = nullptr;
+      const long v = std::strtol(e, &end, 10);
+      if (end == e)
+        break;
+      c->d.anat_r[k] = int(v);
+      if (*end != ',')
+        break;
+      e = end + 1;
+    }
+    c->d.anat = c->anat;
+  }
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   c->last_kind = kind;
   c->last_prec = precision;
@@ -2210,6 +2235,28 @@ int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_
     t[i] = h[i];
   *nbar = kPBlkCap;
   *nblk = c->persist_grid;
+  return 0;
+}
+
+int lmmhip_anatomy(lmmhip_ctx* c, unsigned long long* out, int64_t cap, int64_t* n, int32_t* rounds4) {
+  if (!c || !n)
+    return fail(LMMHIP_E_ARG, "null argument");
+  const int64_t words = int64_t(kAnatSlots) * 3 * kAnatWaves * kAnatFields;
+  *n = 0;
+  if (!LMM_ANAT)
+    return fail(LMMHIP_E_STATE, "not an anatomy build (make EXTRA_HIPFLAGS=-DLMM_ANAT=1)");
+  if (!c->anat || !c->solved)
+    return fail(LMMHIP_E_STATE, "no solve recorded an anatomy (set LMMHIP_ANAT_ROUNDS)");
+  *n = words;
+  if (rounds4)
+    for (int k = 0; k < kAnatSlots; k++)
+      rounds4[k] = c->d.anat_r[k];
+  if (out) {
+    if (cap < words)
+      return fail(LMMHIP_E_ARG, "anatomy: cap too small");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(out, c->anat, size_t(words) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  }
   return 0;
 }
 

@@ -451,9 +451,28 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
 // rows loop over the rest.  Every load indexed by the row or its variable is issued at once.
 // kRec: the row's variable and CSR range from the packed records (crec; the multi-launch engine's short-row
 // vote only — other instantiations, e.g. the persistent kernel, keep their register budget).
+// (LMM_ANAT: `an` = record the dependent levels into aa.lv[0..5]: row record, variable state, row elements, keys,
+// exact ratios, the vote's stores and atomics)
+#if LMM_ANAT
+#define VR_ANAT_PARAMS , bool an = false, AnatAcc* aa = nullptr
+#define VR_LVL(i, dep)       \
+  do {                       \
+    if (an)                  \
+      ANAT_LVL(*aa, i, dep); \
+  } while (0)
+#else
+#define VR_ANAT_PARAMS
+#define VR_LVL(i, dep) \
+  do {                 \
+  } while (0)
+#endif
 template <int R, bool kRec = false, bool kRdq = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
-                                         int* st_elems, const uint16_t* __restrict__ key) {
+                                         int* st_elems, const uint16_t* __restrict__ key VR_ANAT_PARAMS) {
+#if LMM_ANAT
+  if (an)
+    aa->at = anat_now();
+#endif
   const int32_t* __restrict__ cvar = s.cvar[buf];
   const uint32_t* __restrict__ crow = s.crow[buf];
   const int32_t* __restrict__ ccol = s.ccol[buf];
@@ -473,11 +492,13 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     b = crow[row];
     e = crow[row + 1];
   }
+  VR_LVL(0, b + e + uint32_t(t) + uint32_t(cv));
   const int v = rvar(cv);
   const int32_t vst = s.vstate[v];
   const bool bnd = rbounded(cv);
   const double vb = bnd ? s.vbound[v] : -1.0;
   const double p = bnd ? s.pen[v] : 1.0;  // read below only when vb > 0
+  VR_LVL(1, vst);
   // (the row's gathers wait for the variable's state: a fixed variable's row — every variable once, when
   // its saturated target dies — retires without them; measured cheaper on C2 than issuing them early)
   if (vst != 0) {  // fixed by a saturation since: retire the row
@@ -493,6 +514,15 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 #pragma unroll
   for (int i = 0; i < R; i++)
     cc[i] = b + i < e ? ccol[b + i] : -1;
+#if LMM_ANAT
+  {
+    int32_t ccs = 0;
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      ccs += cc[i];
+    VR_LVL(2, ccs);
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < R; i++)
     kk[i] = cc[i] >= 0 ? key[cc[i]] : kDeadKey;
@@ -507,6 +537,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
 #pragma unroll 4
   for (uint32_t j = b + R; j < e; j++)
     mk = min(mk, (unsigned)key[ccol[j]]);
+  VR_LVL(3, mk + kt);
   if (mk == kDeadKey) {  // every constraint of v left the light table: v stays at 0
     s.vstate[v] = round + 1;  // fixed / dropped in this round
     rtgt[row] = kRetired;
@@ -552,6 +583,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
       }
     }
   }
+  VR_LVL(4, minr + double(newt));
   if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
     s.vstate[v] = round + 1;  // fixed / dropped in this round
     s.x[v] = vb;
@@ -584,8 +616,10 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   if (t >= 0 && kt != kDeadKey)
     atomicAdd(&s.nvote[t], mult_old);
   if (kRdq) {
-    if (atomicSub(&s.nvote[newt], mult_new) == mult_new)  // nothing votes elsewhere any more: ready
+    const int old = atomicSub(&s.nvote[newt], mult_new);
+    if (old == mult_new)  // nothing votes elsewhere any more: ready
       rdq_push(s, newt, round);
+    VR_LVL(5, old);
   } else {
     atomicSub(&s.nvote[newt], mult_new);
   }
@@ -618,11 +652,18 @@ __device__ __forceinline__ void vote_wave_range(int64_t lo, int64_t hi, int64_t&
 
 // kPre: the targets and floors of the wave's first filter step were loaded by the caller (tt0 / sk0, issued before
 // the bitmap copy, so that their latency overlaps it).
+// LMM_ANAT: `an` = stamp the filter steps and re-vote batches of this wave into aa (lv[6] filter loads, lv[7] filter
+// gathers, lv[8] re-vote batches; w[0] steps, w[1] batches) and vote_row's levels into ar.
+#if LMM_ANAT
+#define VW_ANAT_PARAMS , bool an = false, AnatAcc* aa = nullptr, AnatAcc* ar = nullptr, unsigned* wcnt = nullptr
+#else
+#define VW_ANAT_PARAMS
+#endif
 template <bool kBits, int R, int F, int kDiag, bool kRec = false, bool kRdq = false, bool kPre = false>
 __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
                                           const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
                                           const uint16_t* __restrict__ key, const int* tt0 = nullptr,
-                                          const unsigned* sk0 = nullptr) {
+                                          const unsigned* sk0 = nullptr VW_ANAT_PARAMS) {
   const int lane = threadIdx.x & (kWave - 1);
   int64_t wlo, whi;
   vote_wave_range(lo, hi, wlo, whi);
@@ -635,6 +676,12 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   for (int64_t base = wlo; base < whi; base += int64_t(F) * kWave) {  // wave-uniform
     int tt[F];
     unsigned sk[F];
+#if LMM_ANAT
+    if (an) {
+      aa->at = anat_now();
+      wcnt[0]++;
+    }
+#endif
     if (kPre && base == wlo) {  // wave-uniform
 #pragma unroll
       for (int u = 0; u < F; u++) {
@@ -649,6 +696,15 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         sk[u] = row < whi ? unsigned(skey[row]) : 1u;
       }
     }
+#if LMM_ANAT
+    if (an) {
+      int ts = 0;
+#pragma unroll
+      for (int u = 0; u < F; u++)
+        ts += tt[u] + int(sk[u]);
+      ANAT_LVL(*aa, 6, ts);
+    }
+#endif
     bool ch[F];
 #pragma unroll
     for (int u = 0; u < F; u++) {
@@ -663,6 +719,15 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
       kt[u] = ch[u] ? key[tt[u]] : 0u;
       cg[u] = (kBits && !ch[u] && tt[u] >= 0 && sk[u] == 0) ? unsigned(s.chg[tt[u]]) : 0x10000u;
     }
+#if LMM_ANAT
+    if (an) {
+      unsigned ks = 0;
+#pragma unroll
+      for (int u = 0; u < F; u++)
+        ks += kt[u] + cg[u];
+      ANAT_LVL(*aa, 7, ks);
+    }
+#endif
     unsigned needm = 0;
 #pragma unroll
     for (int u = 0; u < F; u++) {
@@ -695,14 +760,37 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         nq += kWave;
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
+#if LMM_ANAT
+        if (an) {
+          aa->at = anat_now();
+          wcnt[1]++;
+        }
+        if (kDiag == 0)
+          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, an, ar);
+        if (an)
+          ANAT_LVL(*aa, 8, 0u);
+#else
         if (kDiag == 0)
           vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key);
+#endif
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
+#if LMM_ANAT
+  if (an && qn > 0) {
+    aa->at = anat_now();
+    wcnt[1]++;
+  }
+  if (kDiag == 0 && lane < qn)
+    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, an, ar);
+  __builtin_amdgcn_wave_barrier();
+  if (an && qn > 0)
+    ANAT_LVL(*aa, 8, 0u);
+#else
   if (kDiag == 0 && lane < qn)
     vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key);
+#endif
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
     for (int k = 0; k < 4; k++) {
@@ -787,6 +875,13 @@ constexpr int kVBlock = 1024;
 #endif
 template <int B, bool kBits, int kDiag = 0, bool kRec = false, bool kRdq = false>
 __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
+#if LMM_ANAT
+  unsigned long long* arec = kDiag == 0 ? anat_rec(s, anat_slot(s, round), ANAT_VOTE) : nullptr;
+  const bool an = arec != nullptr;
+  AnatAcc aa{}, ar{};
+  unsigned wcnt[2] = {0, 0};
+  const unsigned long long t_in = an ? anat_now() : 0;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   const int buf = s.ctl[CTL_BUF];
@@ -815,6 +910,9 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (kBits)
     load_bits<B, LMM_BITS_STAGGER != 0, LMM_BITS_UNROLL>(s, bits);
   __syncthreads();
+#if LMM_ANAT
+  const unsigned long long t_bits = an ? anat_now() : 0;
+#endif
   if (kDiag == 2) {  // measurement only: the bitmap load alone, and the changed-constraint count
     if (kBits && blockIdx.x == 0 && s.vstat && round < kStatRounds) {
       int pc = 0;
@@ -826,9 +924,42 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
       s.ctl[CTL_WORDS - 1] = 1;
     return;
   }
+#if LMM_ANAT
+  int nq = 0;
+  if (lo < hi)
+    nq = vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits,
+                                                              q + (threadIdx.x / kWave) * kQW, &st_rows, &st_elems,
+                                                              s.key, tt0, sk0, an, &aa, &ar, wcnt);
+  if (an) {  // the wave's record (vote_row's levels: the slowest lane of the wave)
+    const unsigned long long t_out = anat_now();
+    unsigned lv[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+      lv[i] = anat_wmax(ar.lv[i]);
+    int64_t wlo, whi;
+    vote_wave_range(lo, hi, wlo, whi);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      arec[0] = t_in;
+      arec[1] = t_out;
+      arec[2] = blockIdx.x;
+      arec[3] = t_bits;
+      arec[4] = wcnt[0];
+      arec[5] = aa.lv[6];
+      arec[6] = aa.lv[7];
+      arec[7] = wcnt[1];
+      arec[8] = aa.lv[8];
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+        arec[9 + i] = lv[i];
+      arec[15] = unsigned(nq);
+      arec[16] = whi > wlo ? unsigned(whi - wlo) : 0u;
+    }
+  }
+#else
   if (lo < hi)
     vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
                                                          &st_rows, &st_elems, s.key, tt0, sk0);
+#endif
   if (s.vstat && kDiag == 0) {
     __syncthreads();
     if (threadIdx.x == 0 && round < kStatRounds && blockIdx.x < kMaxBlocks) {
@@ -884,8 +1015,32 @@ __global__ void __launch_bounds__(kBlock) mm_ready(Dev s) {
 #endif
 constexpr int kSatU = LMM_KSATU;
 
+// (LMM_ANAT: `an` = stamp the chunk's dependent levels into aa: lv[1] CSC element loads, lv[2] variable states and
+// claims, lv[3] the claimed rows' elements, lv[4] their constraints' words, lv[5] the pushes; wc[1] chunks, wc[2]
+// fixed variables, wc[3] pushed elements)
+#if LMM_ANAT
+#define SC_ANAT_PARAMS , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
+#define SC_ANAT_ARGS , an, aa, wc
+#define SC_LVL(i, dep)       \
+  do {                       \
+    if (an)                  \
+      ANAT_LVL(*aa, i, dep); \
+  } while (0)
+#else
+#define SC_ANAT_PARAMS
+#define SC_ANAT_ARGS
+#define SC_LVL(i, dep) \
+  do {                 \
+  } while (0)
+#endif
 __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t ce,
-                                               int round, int lane, int* pre, bool dup) {
+                                               int round, int lane, int* pre, bool dup SC_ANAT_PARAMS) {
+#if LMM_ANAT
+  if (an) {
+    aa->at = anat_now();
+    wc[1]++;
+  }
+#endif
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
   int32_t lv = -1;
@@ -900,6 +1055,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     rb = uint32_t(row);
     re = uint32_t(row >> 32);
   }
+  SC_LVL(1, uint32_t(lv) + rb + re);
   if (j < ce) {
     if (s.vstate[lv] != 0)
       lv = -1;
@@ -916,6 +1072,12 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
   } else {
     rb = re = 0;
   }
+#if LMM_ANAT
+  if (an) {
+    ANAT_LVL(*aa, 2, lv);
+    wc[2] += unsigned(__popcll(__ballot(lv >= 0)));
+  }
+#endif
   int incl = len;  // inclusive wave scan of the row lengths
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -944,6 +1106,15 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       cc[u] = f < total ? s.csr_c[kk[u]] : -1;
       ww[u] = f < total ? s.csr_w[kk[u]] : 0.0;  // with the constraint id: one round trip
     }
+#if LMM_ANAT
+    if (an) {
+      double sw = 0.0;
+#pragma unroll
+      for (int u = 0; u < kSatU; u++)
+        sw += ww[u] + double(cc[u]);
+      ANAT_LVL(*aa, 3, sw);
+    }
+#endif
     long long a0[kSatU], a1[kSatU];  // fixed-point decrements (CstRec)
     bool fat[kSatU];
 #pragma unroll
@@ -963,6 +1134,17 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
         a1[u] = fat[u] ? (long long)fat_bits(w / op) : (long long)dec_q(w / op, cexp_use(ce));
       }
     }
+#if LMM_ANAT
+    if (an) {
+      long long sa = 0;
+#pragma unroll
+      for (int u = 0; u < kSatU; u++) {
+        sa += a0[u] + a1[u];
+        wc[3] += unsigned(__popcll(__ballot(cc[u] >= 0)));
+      }
+      ANAT_LVL(*aa, 4, sa);
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < kSatU; u++) {
       const int nel = total - f0 - u * kWave;
@@ -981,6 +1163,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
           atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
       }
     }
+    SC_LVL(5, 0u);
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -1100,9 +1283,10 @@ template <int K> __device__ __forceinline__ void saturate_one(const Dev& s, int3
 }
 // (the same with the constraint's ratio, CSC range and duplicate flag already loaded)
 template <int K> __device__ __forceinline__ void saturate_one_pre(const Dev& s, int32_t c, int k, int round, int lane,
-                                                                  int* pre, double r, uint32_t cb, uint32_t ce, bool dup) {
+                                                                  int* pre, double r, uint32_t cb, uint32_t ce,
+                                                                  bool dup SC_ANAT_PARAMS) {
   for (uint32_t base = cb + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
-    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup);
+    saturate_chunk(s, c, r, base, ce, round, lane, pre, dup SC_ANAT_ARGS);
   if (k == 0 && lane == 0)
     s.ctouch[c] = 2;
 }
@@ -1178,6 +1362,14 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 #define LMM_SATQ_SPEC 1
 #endif
 template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
+#if LMM_ANAT
+  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
+  const bool an = arec != nullptr;
+  AnatAcc aa_s{};
+  AnatAcc* aa = &aa_s;
+  unsigned wc[4] = {0, 0, 0, 0};  // candidates, chunks, fixed variables, pushed elements
+  const unsigned long long t_in = an ? anat_now() : 0;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1217,6 +1409,9 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     acc += loc[k];
   }
   __syncthreads();
+#if LMM_ANAT
+  const unsigned long long t_pre = an ? anat_now() : 0;
+#endif
   const int nq = s.ctl[CTL_RDQ0 + (round & 1)];
   const int32_t* __restrict__ q = s.rdq[round & 1];
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
@@ -1224,6 +1419,12 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
   for (int64_t g = wave; g < (int64_t(total) + nq) * K; g += nwaves) {  // wave-uniform
     const int64_t i = g / K;
     const int k = int(g % K);
+#if LMM_ANAT
+    if (an) {
+      aa->at = anat_now();
+      wc[0]++;
+    }
+#endif
     int32_t c;
     if (i < total) {
       int lo = 0;  // last segment with pre[seg] <= i
@@ -1235,6 +1436,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     } else {
       c = q[i - total];
     }
+    SC_LVL(0, c);
 #if LMM_SATQ_SPEC
     // the constraint's ratio, CSC range and duplicate flag loaded with its key and count (one dependent level less;
     // a candidate that is not ready discards them)
@@ -1243,11 +1445,12 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     const double r = ld_rlx(&s.cst[c].ratio);
     const uint32_t cb = s.cnst_ptr[c], cend = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
+    SC_LVL(6, r + double(kc + unsigned(nv) + cb + cend + unsigned(dup)));
     if (kc == kDeadKey || nv != 0)
       continue;
     if (k == 0 && lane == 0)
       s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-    saturate_one_pre<K>(s, c, k, round, lane, wpre[w], r, cb, cend, dup);
+    saturate_one_pre<K>(s, c, k, round, lane, wpre[w], r, cb, cend, dup SC_ANAT_ARGS);
 #else
     if (s.key[c] == kDeadKey || s.nvote[c] != 0)
       continue;
@@ -1256,6 +1459,18 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     saturate_one<K>(s, c, k, round, lane, wpre[w]);
 #endif
   }
+#if LMM_ANAT
+  if (an && lane == 0) {
+    arec[0] = t_in;
+    arec[1] = anat_now();
+    arec[2] = blockIdx.x;
+    arec[3] = t_pre;
+    for (int f = 0; f < 7; f++)
+      arec[4 + f] = aa->lv[f];
+    for (int f = 0; f < 4; f++)
+      arec[11 + f] = wc[f];
+  }
+#endif
 }
 
 // Round phase 4 — constraint update: maxmin.cpp:603-658, one wave = 64 consecutive constraints (identity
@@ -1268,10 +1483,22 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
 // K groups of 64 constraints (base0 + k * stride) at once: every load of the K groups (key and touch
 // flag, then — touched constraints only — record, flags, scale, votes) is issued before any of them is
 // used, so a wave keeps K times the memory requests in flight.
+// (LMM_ANAT: `an` = stamp the steps into aa: lv[0] keys and touch flags, lv[1] touched records, lv[2] the rest;
+// wc[0] steps, wc[1] touched constraints)
 template <int K, bool kRdq = false>
 __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_t stride, int round, double prec,
-                                             bool* touch, int* ucnt_sh = nullptr, int32_t* ulist = nullptr) {
+                                             bool* touch, int* ucnt_sh = nullptr, int32_t* ulist = nullptr
+#if LMM_ANAT
+                                             , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
+#endif
+) {
   const int lane = threadIdx.x & (kWave - 1);
+#if LMM_ANAT
+  if (an) {
+    aa->at = anat_now();
+    wc[0]++;
+  }
+#endif
   unsigned okey[K], tf[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
@@ -1279,6 +1506,15 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     okey[k] = c < s.nC ? unsigned(s.key[c]) : kDeadKey;
     tf[k] = c < s.nC ? unsigned(s.ctouch[c]) : 0u;  // 1 = received decrements, 2 = saturated this round
   }
+#if LMM_ANAT
+  if (an) {
+    unsigned ks = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      ks += okey[k] + tf[k];
+    ANAT_LVL(*aa, 0, ks);
+  }
+#endif
   unsigned long long qx[K], qy[K], qz[K];
   double rem[K], use[K], bnd[K];
   int32_t ce[K], nv[K];
@@ -1300,6 +1536,17 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       nv[k] = s.nvote[c];
     }
   }
+#if LMM_ANAT
+  if (an) {
+    double rs = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      rs += rem[k] + use[k] + bnd[k] + double(qx[k] + qy[k] + qz[k]) + double(ce[k] + nv[k]);
+      wc[1] += unsigned(__popcll(__ballot(okey[k] != kDeadKey && tf[k] == 1)));
+    }
+    ANAT_LVL(*aa, 1, rs);
+  }
+#endif
   int alive = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
@@ -1385,6 +1632,10 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     if (lane == 0)
       s.chgbits[gbase >> 6] = word;
   }
+#if LMM_ANAT
+  if (an)
+    ANAT_LVL(*aa, 2, alive);
+#endif
   return alive;
 }
 
@@ -1398,6 +1649,13 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
 #define LMM_UPD_K 4
 #endif
 template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update(Dev s, int round, double prec) {
+#if LMM_ANAT
+  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_UPD);
+  const bool an = arec != nullptr;
+  AnatAcc aa{};
+  unsigned wc[2] = {0, 0};
+  const unsigned long long t_in = an ? anat_now() : 0;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1412,7 +1670,12 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = (int64_t(blockIdx.x) * kBlock + threadIdx.x) & ~int64_t(kWave - 1); base < s.nC;
        base += LMM_UPD_K * stride)  // wave-uniform; LMM_UPD_K groups of 64 constraints per step, loads in flight together
+#if LMM_ANAT
+    alive += update_groups<LMM_UPD_K, kRdq>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist, an, &aa, wc);
+  const unsigned long long t_loop = an ? anat_now() : 0;
+#else
     alive += update_groups<LMM_UPD_K, kRdq>(s, base, stride, round, prec, &any_touch, &ucnt_sh, ulist);
+#endif
   if (alive)
     atomicAdd(&alive_cnt, alive);
   __syncthreads();
@@ -1427,6 +1690,18 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
   }
   if (__syncthreads_or(any_touch) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
+#if LMM_ANAT
+  if (an && (threadIdx.x & (kWave - 1)) == 0) {
+    arec[0] = t_in;
+    arec[1] = anat_now();
+    arec[2] = blockIdx.x;
+    arec[3] = t_loop;
+    for (int f = 0; f < 3; f++)
+      arec[4 + f] = aa.lv[f];
+    arec[7] = wc[0];
+    arec[8] = wc[1];
+  }
+#endif
 }
 
 // Saturated set of the solved system: sat(c) = NOT double_positive(bound - U_c,

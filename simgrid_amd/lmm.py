@@ -179,6 +179,7 @@ SIGNATURES = {
     "lmmhip_device_count": (I, []),
     "lmmhip_last_error": (ct.c_char_p, []),
     "lmmhip_build_id": (ct.c_char_p, []),
+    "lmmhip_anatomy": (I, [P, ct.POINTER(ct.c_uint64), I64, PI64, ct.POINTER(ct.c_int32)]),
 }
 
 _lib = None
