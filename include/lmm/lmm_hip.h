@@ -146,6 +146,9 @@ int lmmhip_solve(lmmhip_ctx* ctx, int kind, double precision);
 
 /* Copy the solved values (n_var doubles, CSR variable order) to host memory. */
 int lmmhip_get_values(lmmhip_ctx* ctx, double* values_out);
+/* Per variable of the last max-min solve (dense order, as lmmhip_get_values): 1 + the device round that fixed or
+ * dropped it (0: never; measurement — the dependency-depth comparison of scripts/depth.py). */
+int lmmhip_get_var_rounds(lmmhip_ctx* ctx, int32_t* rounds_out);
 /* Saturated set of the last solve, one byte per constraint of the solved system (dense order):
  *   MAXMIN: sat(c) = NOT double_positive(bound - U_c, bound * precision), U_c = Constraint::get_usage()
  *           (maxmin.cpp:948-961) from the solved values — the saturated_constraint_set the reference

@@ -163,6 +163,10 @@ typedef struct lmm_platform_params {
   double tcp_gamma;            /* network/TCP-gamma */
 } lmm_platform_params;
 int lmm_platform_size(const lmm_platform_params* p, int64_t* n_links, int64_t* n_hosts);
+/* DRAGONFLY only: DragonflyZone::rankId_to_coords (DragonflyZone.cpp:26-35) of every host — coords_out[4 h .. 4 h + 3]
+ * = (group, chassis, blade, node) of host h, up to cap ints; returns the host count, or -1 (not a dragonfly, bad
+ * topo_parameters: the errors of DragonflyZone::parse_specific_arguments). */
+int64_t lmm_platform_dragonfly_coords(const lmm_platform_params* p, int32_t* coords_out, int64_t cap);
 /* constraints: one per link (creation order), then for L07 one CPU per host; returns n_flows or -1 */
 int64_t lmm_gen_platform_flows(lmm_sys* s, const lmm_platform_params* p, int64_t* cnst_out, int64_t* var_out);
 

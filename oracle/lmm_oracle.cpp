@@ -442,8 +442,34 @@ template <class List> void System::solve_list(List& list) {
   }
   sat_var_update(tab, sat, this);
 
+  if (depth_on) {
+    depth_D = 0;
+    depth_sat_events = depth_bound_events = 0;
+    depth_hist.clear();
+    depth_bhist.clear();
+    for (Constraint& c : list) {
+      c.dep_lvl = 0;
+      c.sat_lvl = -1;
+      c.sat_round = -1;
+      for (Element& e : c.enabled) {
+        e.var->fix_lvl = -1;
+        e.var->fix_round = -1;
+        e.var->fix_by = 0;
+      }
+    }
+  }
+  std::vector<std::pair<Variable*, int>> depth_fixed;  // (variable, level) fixed this round (depth_on)
+  std::vector<Constraint*> depth_sat;                  // this round's minimal-ratio constraints
   do {
     last_rounds++;
+    if (depth_on) {  // this round's saturating constraints (used only if no bound fix preempts them)
+      depth_fixed.clear();
+      depth_sat.clear();
+      for (int i : sat) {
+        tab[i].cnst->sat_round = last_rounds;
+        depth_sat.push_back(tab[i].cnst);
+      }
+    }
     for (Variable& v : saturated_vars) {
       ORACLE_ASSERT(v.penalty > 0, "DIE_IMPOSSIBLE");
       if (v.bound > 0 && v.bound * v.penalty < min_usage) {
@@ -462,6 +488,22 @@ template <class List> void System::solve_list(List& list) {
       } else {
         saturated_vars.pop_front();
         continue;
+      }
+      if (depth_on) {  // the event's level, from the constraints' dependencies of earlier rounds only
+        int lvl = 0, by = 0;
+        for (Element& e : v.elems) {
+          Constraint* c = e.cnst;
+          if (min_bound >= 0) {  // a bound fix: its own node, after every constraint of the variable
+            lvl = std::max(lvl, c->dep_lvl + 1);
+          } else if (c->sat_round == last_rounds && c->dep_lvl + 1 > lvl) {  // this round's saturation of c (ties:
+            lvl = c->dep_lvl + 1;                                           // the deepest)
+            by = c->rank;
+          }
+        }
+        v.fix_lvl = lvl;
+        v.fix_round = last_rounds;
+        v.fix_by = by;
+        depth_fixed.emplace_back(&v, lvl);
       }
       for (Element& e : v.elems) {
         Constraint* c = e.cnst;
@@ -496,6 +538,36 @@ template <class List> void System::solve_list(List& list) {
       saturated_vars.pop_front();
     }
 
+    if (depth_on) {
+      const bool bound_round = min_bound >= 0;
+      for (auto& [v, lvl] : depth_fixed) {
+        if (int(depth_hist.size()) <= lvl) {
+          depth_hist.resize(size_t(lvl) + 1, 0);
+          depth_bhist.resize(size_t(lvl) + 1, 0);
+        }
+        if (bound_round)
+          depth_bhist[size_t(lvl)]++;
+        depth_bound_events += bound_round;
+        depth_D = std::max(depth_D, lvl);
+      }
+      if (!bound_round)
+        for (Constraint* c : depth_sat) {
+          c->sat_lvl = c->dep_lvl + 1;
+          depth_sat_events++;
+          if (int(depth_hist.size()) <= c->sat_lvl) {
+            depth_hist.resize(size_t(c->sat_lvl) + 1, 0);
+            depth_bhist.resize(size_t(c->sat_lvl) + 1, 0);
+          }
+          depth_hist[size_t(c->sat_lvl)]++;
+          depth_D = std::max(depth_D, c->sat_lvl);
+        }
+      else
+        for (Constraint* c : depth_sat)
+          c->sat_round = -1;  // preempted by the bound fixes: it saturates in a later round
+      for (auto& [v, lvl] : depth_fixed)  // then this round's fixes reach the constraints they touch
+        for (Element& e : v->elems)
+          e.cnst->dep_lvl = std::max(e.cnst->dep_lvl, lvl);
+    }
     min_usage = -1;
     min_bound = -1;
     sat.clear();

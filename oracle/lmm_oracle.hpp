@@ -135,6 +135,10 @@ struct Constraint {  // maxmin.hpp:179-282
   // recorded by the last lmm_solve init (the tesh 'Constraint ... usage: remaining:' lines)
   double init_usage = 0.0, init_remaining = 0.0;
   bool init_recorded = false;
+  // dependency depth (System::depth_on, measurement only): the deepest event that fixed one of its variables in an
+  // earlier sequential round, and its own saturation's level / sequential round (-1: never saturated)
+  int dep_lvl = 0, sat_lvl = -1;
+  long long sat_round = -1;
 
   int slack() const;  // maxmin.hpp:220-223
   double get_usage();
@@ -148,6 +152,9 @@ struct Variable {  // maxmin.hpp:290-365
   int share = 1;  // concurrency_share_
   int rank = 0;
   unsigned visited = 0;
+  int fix_lvl = -1;       // dependency depth of the event that fixed it (System::depth_on), -1: not fixed
+  long long fix_round = -1;  // its sequential round (depth_on)
+  int fix_by = 0;            // rank of the saturated constraint that fixed it, 0 = a bound fix (depth_on)
   void* user = nullptr;  // the Action* in the reference (opaque here)
   bool in_modified_set = false;
 
@@ -187,6 +194,15 @@ public:
   unsigned visited_counter = 1;
   int next_var_rank = 1, next_cnst_rank = 1;  // per-system (reference: global statics)
   long long last_rounds = 0;                  // number of outer rounds of the last solve
+  // Dependency depth of the last lmm_solve (measurement only, depth_on; VERDICT r05 Next #1a): events are the
+  // saturations (a constraint of the minimal ratio fixing its variables, maxmin.cpp:583) and the bound fixes
+  // (:587-589, one node per variable); an event's level is 1 + the deepest level of the events that fixed a
+  // variable of its constraint(s) in EARLIER sequential rounds (a bound fix: of any constraint of its variable).
+  // depth_D = the longest such chain; depth_hist[l] = saturation events at level l, depth_bhist[l] bound fixes.
+  bool depth_on = false;
+  int depth_D = 0;
+  long long depth_sat_events = 0, depth_bound_events = 0;
+  std::vector<long long> depth_hist, depth_bhist;
 
 protected:
   void var_free(Variable* v);

@@ -46,6 +46,40 @@ void oracle_solve(void* s) { S(s)->solve(); }
 long long oracle_last_rounds(void* s) { return S(s)->last_rounds; }
 int oracle_is_modified(void* s) { return S(s)->modified; }
 
+// Dependency depth of the next solves (System::depth_on; measurement only).  oracle_depth_stats: D, the saturation and
+// bound-fix event counts, and the per-level histograms (saturations, bound fixes) into hist / bhist (cap entries);
+// returns the number of levels (D + 1).
+void oracle_set_depth(void* s, int on) { S(s)->depth_on = on != 0; }
+int oracle_depth_stats(void* s, int* D, long long* sat_events, long long* bound_events, long long* hist,
+                       long long* bhist, int cap) {
+  System* y = S(s);
+  *D = y->depth_D;
+  *sat_events = y->depth_sat_events;
+  *bound_events = y->depth_bound_events;
+  const int n = int(y->depth_hist.size());
+  for (int i = 0; i < n && i < cap; i++) {
+    hist[i] = y->depth_hist[size_t(i)];
+    bhist[i] = y->depth_bhist[size_t(i)];
+  }
+  return n;
+}
+// Per variable (the given handles): the level and sequential round of the event that fixed it, and the rank of the
+// constraint whose saturation fixed it (0: a bound fix; -1 / -1 / 0: never fixed).
+void oracle_variable_depth(void*, void** vs, long long n, int* lvl, long long* round, int* by) {
+  for (long long i = 0; i < n; i++) {
+    lvl[i] = V(vs[i])->fix_lvl;
+    round[i] = V(vs[i])->fix_round;
+    by[i] = V(vs[i])->fix_by;
+  }
+}
+// Per constraint (the given handles): its saturation level and sequential round (-1: never saturated).
+void oracle_constraint_depth(void*, void** cs, long long n, int* lvl, long long* round) {
+  for (long long i = 0; i < n; i++) {
+    lvl[i] = C(cs[i])->sat_lvl;
+    round[i] = C(cs[i])->sat_round;
+  }
+}
+
 // Times one solve() with steady_clock, excluding construction (maxmin_bench.cpp:81-83).
 double oracle_timed_solve(void* s) {
   auto t0 = std::chrono::steady_clock::now();

@@ -279,6 +279,13 @@ class Dragonfly(_Links):
                 self.blue[ri] = u
                 self.blue[rj] = d
 
+    def coords(self, r):
+        """DragonflyZone::rankId_to_coords (DragonflyZone.cpp:26-35) of host rank(s) r: (group, chassis, blade,
+        node)."""
+        C, B, N = self.C, self.B, self.N
+        r = np.asarray(r, dtype=np.int64)
+        return r // (C * B * N), r % (C * B * N) // (B * N), r % (B * N) // N, r % N
+
     def routes(self, src, dst):
         """DragonflyZone.cpp:238-336 for arrays of (src, dst): (link matrix padded with -1, in route order;
         latency of each route: the hops', not the limiters')."""
@@ -288,8 +295,7 @@ class Dragonfly(_Links):
         n = len(src)
         lat = np.array(self.lat)
 
-        def coords(r):  # DragonflyZone.cpp:26-35
-            return r // (C * B * N), r % (C * B * N) // (B * N), r % (B * N) // N, r % N
+        coords = self.coords  # DragonflyZone.cpp:26-35
 
         m0, m1, m2, m3 = coords(src)
         t0, t1, t2, t3 = coords(dst)

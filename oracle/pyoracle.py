@@ -56,6 +56,10 @@ _SIGS = {
     "oracle_solve": (None, [P]),
     "oracle_timed_solve": (D, [P]),
     "oracle_last_rounds": (LL, [P]),
+    "oracle_set_depth": (None, [P, I]),
+    "oracle_depth_stats": (I, [P, ct.POINTER(I), ct.POINTER(LL), ct.POINTER(LL), ct.POINTER(LL), ct.POINTER(LL), I]),
+    "oracle_constraint_depth": (None, [P, ct.POINTER(P), LL, ct.POINTER(I), ct.POINTER(LL)]),
+    "oracle_variable_depth": (None, [P, ct.POINTER(P), LL, ct.POINTER(I), ct.POINTER(LL), ct.POINTER(I)]),
     "oracle_is_modified": (I, [P]),
     "oracle_constraint_new": (P, [P, D]),
     "oracle_constraint_unshare": (None, [P, P]),
@@ -251,6 +255,42 @@ class System:
 
     def timed_solve(self):
         return lib().oracle_timed_solve(self.h)
+
+    def set_depth(self, on):
+        """Record the dependency depth of the next solves (measurement only; lmm_oracle.hpp depth_on)."""
+        lib().oracle_set_depth(self.h, int(bool(on)))
+
+    def depth_stats(self):
+        """(D, saturation events, bound-fix events, per-level saturation histogram, per-level bound-fix histogram)."""
+        import numpy as np
+        d, ns, nb = I(), LL(), LL()
+        cap = 1 << 20
+        h = np.zeros(cap, dtype=np.int64)
+        bh = np.zeros(cap, dtype=np.int64)
+        n = lib().oracle_depth_stats(self.h, ct.byref(d), ct.byref(ns), ct.byref(nb),
+                                     h.ctypes.data_as(ct.POINTER(LL)), bh.ctypes.data_as(ct.POINTER(LL)), cap)
+        return d.value, ns.value, nb.value, h[:n].copy(), bh[:n].copy()
+
+    def variable_depth(self, vs):
+        """Per variable handle: (level, sequential round, rank of the constraint that fixed it: 0 = bound fix)."""
+        import numpy as np
+        arr = vs if isinstance(vs, ct.Array) else (P * len(vs))(*[getattr(v, "h", v) for v in vs])
+        lv = np.zeros(len(vs), dtype=np.int32)
+        rd = np.zeros(len(vs), dtype=np.int64)
+        by = np.zeros(len(vs), dtype=np.int32)
+        lib().oracle_variable_depth(self.h, arr, len(vs), lv.ctypes.data_as(ct.POINTER(I)),
+                                    rd.ctypes.data_as(ct.POINTER(LL)), by.ctypes.data_as(ct.POINTER(I)))
+        return lv, rd, by
+
+    def constraint_depth(self, cs):
+        """Per constraint handle: (saturation level, sequential round), -1 if it never saturated."""
+        import numpy as np
+        arr = (P * len(cs))(*[c.h for c in cs])
+        lv = np.zeros(len(cs), dtype=np.int32)
+        rd = np.zeros(len(cs), dtype=np.int64)
+        lib().oracle_constraint_depth(self.h, arr, len(cs), lv.ctypes.data_as(ct.POINTER(I)),
+                                      rd.ctypes.data_as(ct.POINTER(LL)))
+        return lv, rd
 
     @property
     def last_rounds(self):

@@ -464,6 +464,25 @@ int lmm_platform_size(const lmm_platform_params* p, int64_t* n_links, int64_t* n
   }
 }
 
+int64_t lmm_platform_dragonfly_coords(const lmm_platform_params* p, int32_t* coords_out, int64_t cap) {
+  try {
+    if (!p || p->topology != 1)
+      throw std::invalid_argument("lmm_platform_dragonfly_coords: not a dragonfly platform");
+    const lmm_plat::Dragonfly df(lmm_plat::params_from(*p));
+    const int64_t n = df.n_hosts;
+    for (int64_t h = 0; coords_out && h < n && 4 * (h + 1) <= cap; h++) {
+      int c[4];
+      df.coords(int(h), c);
+      for (int k = 0; k < 4; k++)
+        coords_out[4 * h + k] = c[k];
+    }
+    return n;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 int64_t lmm_gen_platform_flows(lmm_sys* s, const lmm_platform_params* p, int64_t* cnst_out, int64_t* var_out) {
   try {
     const lmm_plat::Params prm = lmm_plat::params_from(*p);

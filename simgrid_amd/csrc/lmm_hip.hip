@@ -2807,6 +2807,18 @@ int lmmhip_get_values(lmmhip_ctx* c, double* out) {
   return 0;
 }
 
+int lmmhip_get_var_rounds(lmmhip_ctx* c, int32_t* out) {
+  if (!c || !c->solved || c->last_kind != LMMHIP_KIND_MAXMIN)
+    return fail(LMMHIP_E_STATE, "no max-min solve to read rounds from");
+  if (!out && c->d.nV)
+    return fail(LMMHIP_E_ARG, "null output");
+  HIPCHK(hipSetDevice(c->device));
+  if (c->d.nV)
+    HIPCHK(hipMemcpyAsync(out, c->d.vstate, sizeof(int32_t) * c->d.nV, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 int lmmhip_get_saturated(lmmhip_ctx* c, uint8_t* sat) {
   if (!c || !c->uploaded || !c->solved)
     return fail(LMMHIP_E_STATE, "no solved system");

@@ -351,7 +351,11 @@ class Dragonfly : public Platform {
       throw std::out_of_range("dragonfly: no such link");
     return v[i];
   }
-  void coords(int rank, int c[4]) const {  // DragonflyZone.cpp:26-35
+
+ public:
+  // rankId_to_coords (DragonflyZone.cpp:26-35): group, chassis, blade, node of host `rank`; pinned to the 120 lines
+  // s4u-routing-get-clusters.tesh prints for cluster_dragonfly.xml (tests/test_platforms.py)
+  void coords(int rank, int c[4]) const {
     const int per_group = chassis_ * blades_ * nodes_, per_chassis = blades_ * nodes_;
     c[0] = rank / per_group;
     rank %= per_group;
@@ -361,7 +365,6 @@ class Dragonfly : public Platform {
     c[3] = rank % nodes_;
   }
 
- public:
   explicit Dragonfly(const Params& p) {
     const auto parts = split(p.topo, ';');
     if (parts.size() != 4)

@@ -116,6 +116,7 @@ SIGNATURES = {
     "lmm_gen_maxmin_bench": (I, [P, I, I, PI64, PI64, PI, PI]),
     "lmm_gen_synthetic": (I64, [P, I64, I64, I, U64, I, I, I, I, PI64]),
     "lmm_platform_size": (I, [ct.POINTER(PlatformParams), PI64, PI64]),
+    "lmm_platform_dragonfly_coords": (I64, [ct.POINTER(PlatformParams), ct.POINTER(ct.c_int32), I64]),
     "lmm_gen_platform_flows": (I64, [P, ct.POINTER(PlatformParams), PI64, PI64]),
     "lmm_link_new": (I64, [P, I, D, I]),
     "lmm_communicate": (I64, [P, P, I, I64, PI64, PD, PD, I64, PI64, D, D, I, P]),
@@ -144,6 +145,7 @@ SIGNATURES = {
     "lmmhip_solve": (I, [P, I, D]),
     "lmmhip_set_batch": (I, [P, I64, PI64, PI64]),
     "lmmhip_get_values": (I, [P, PD]),
+    "lmmhip_get_var_rounds": (I, [P, ct.POINTER(ct.c_int32)]),
     "lmmhip_values_device_ptr": (I, [P, ct.POINTER(P)]),
     "lmmhip_get_saturated": (I, [P, ct.POINTER(ct.c_uint8)]),
     "lmmhip_get_touched_vars": (I, [P, ct.POINTER(ct.c_int32), I64, PI64]),
@@ -270,6 +272,18 @@ def platform_size(p):
     nl, nh = I64(), I64()
     _check(lib().lmm_platform_size(ct.byref(p), ct.byref(nl), ct.byref(nh)))
     return nl.value, nh.value
+
+
+def dragonfly_coords(p):
+    """(n_hosts x 4) array of DragonflyZone::rankId_to_coords (group, chassis, blade, node) of every host of the
+    dragonfly `p` describes (lmm_platform_dragonfly_coords)."""
+    n = lib().lmm_platform_dragonfly_coords(ct.byref(p), None, 0)
+    if n < 0:
+        raise LmmError(lib().lmm_last_error().decode())
+    out = np.zeros(4 * n, np.int32)
+    _check(0 if lib().lmm_platform_dragonfly_coords(ct.byref(p), out.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                                                    4 * n) == n else -1)
+    return out.reshape(n, 4)
 
 
 class Constraint:
@@ -522,6 +536,14 @@ class System:
         x = np.empty(n, np.float64)
         _check_hip(lib().lmmhip_get_values(self.device_ctx(), x.ctypes.data_as(PD)))
         return x
+
+    def device_var_rounds(self):
+        """1 + the device round that fixed each variable of the last max-min solve, dense order
+        (lmmhip_get_var_rounds; 0 = never)."""
+        n = self.last_stats()["n_var"]
+        r = np.empty(n, np.int32)
+        _check_hip(lib().lmmhip_get_var_rounds(self.device_ctx(), r.ctypes.data_as(ct.POINTER(ct.c_int32))))
+        return r
 
     def device_saturated(self):
         """Saturated set of the last solve, dense constraint order (lmmhip_get_saturated)."""

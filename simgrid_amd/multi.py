@@ -274,6 +274,18 @@ class DeviceBatch:
         self._check(self.L.lmmhip_get_values(self.ctx, x.ctypes.data_as(ct.POINTER(ct.c_double))))
         return x
 
+    def saturated(self):
+        """The device's saturated set of the last solve (lmmhip_get_saturated: SURVEY.md A.6, maxmin.cpp:948-961),
+        one flag per dense constraint of the concatenated systems."""
+        out = np.empty(self.n_cnst, np.uint8)
+        self._check(self.L.lmmhip_get_saturated(self.ctx, out.ctypes.data_as(ct.POINTER(ct.c_uint8))))
+        return out.astype(bool)
+
+    def flat(self):
+        """The concatenated flattened system as a Flat (dense ids; var_ids / csc_order unset)."""
+        vp, ci, w, pen, vb, cb, cf = self.arrays
+        return Flat(vp, ci, w, pen, vb, cb, cf, None, None)
+
     def close(self):
         if self.ctx:
             self.L.lmmhip_ctx_destroy(self.ctx)

@@ -42,22 +42,59 @@ def c3_oracle():
     return np.array([v.get_value() for v in vs])
 
 
+@pytest.fixture(scope="module")
+def c3_oracle_saturated():
+    """The oracle's saturated set of the 4096 medium systems (SURVEY.md A.6 through Constraint::get_usage,
+    maxmin.cpp:948-961): (system, constraint position) pairs."""
+    out = set()
+    for i in range(4096):
+        o = O.System(False)
+        cs = o.gen_maxmin_bench(1, i)[0]
+        o.solve()
+        out |= {(i, k) for k in K.saturated(o, dict(enumerate(cs)), L.get_precision())}
+    return out
+
+
+def _sat_dense(f, x, prec):
+    """Saturated constraints (NOT double_positive(bound - get_usage(), bound * prec), with get_usage =
+    sum, FATPIPE max, of w x over the constraint's elements, maxmin.cpp:948-961 / :470-480) of the flattened system
+    `f` under dense values `x`, as a boolean per dense constraint."""
+    rows = np.repeat(np.arange(len(f.penalty)), np.diff(f.var_ptr))
+    wx = f.weight * x[rows]
+    use = np.bincount(f.cnst_idx, weights=wx, minlength=len(f.cbound))
+    fat = (f.cflags & 1).astype(bool)
+    if fat.any():
+        mx = np.zeros(len(f.cbound))
+        np.maximum.at(mx, f.cnst_idx, wx)
+        use = np.where(fat, mx, use)
+    return ~(f.cbound - use > f.cbound * prec)
+
+
 def _close(x, y):
     tol = np.maximum(K.ABS_TOL, K.REL_TOL * np.abs(y))
     bad = np.nonzero(~(np.abs(x - y) <= tol))[0]
     return bad, (float(np.max(np.abs(x - y))) if len(x) else 0.0)
 
 
-def test_c3_disjoint_union_vs_oracle(c3_oracle):
+def test_c3_disjoint_union_vs_oracle(c3_oracle, c3_oracle_saturated):
     s = L.System(False)
-    ids = []
+    ids, cs = [], {}
     for i in range(4096):
-        ids.extend(v.h for v in s.gen_maxmin_bench(1, i)[1])
+        c, v, _, _ = s.gen_maxmin_bench(1, i)
+        ids.extend(x.h for x in v)
+        cs.update({(i, k): ck for k, ck in enumerate(c)})
+    f = M.export_flat(s)
     s.solve()
     x = s.values_of(np.array(ids, np.int64))
     bad, worst = _close(x, c3_oracle)
     assert len(bad) == 0, (len(bad), worst)
     assert s.last_stats()["n_var"] > 100_000
+    # the same saturated set (SURVEY.md A.6): through the drop-in Constraint::get_usage of every constraint, and the
+    # device's own (mm_saturated) against the oracle's values on the flattened system
+    assert K.saturated(s, cs, L.get_precision()) == c3_oracle_saturated
+    pos = {int(h): j for j, h in enumerate(ids)}
+    y = c3_oracle[[pos[int(h)] for h in f.var_ids]]
+    np.testing.assert_array_equal(s.device_saturated(), _sat_dense(f, y, L.get_precision()))
 
 
 def test_c3_solve_batch_vs_oracle(c3_oracle):
@@ -94,11 +131,24 @@ def test_c3_device_batch_vs_oracle_and_global_engine(c3_oracle, monkeypatch):
             k += 1
     bad, worst = _close(xo, y)
     assert len(bad) == 0, (len(bad), worst)
+    # the same saturated set: the batch kernel's device set against the oracle's values on the
+    # concatenated flattened systems
+    yd = np.zeros(b.n_var)
+    k = 0
+    for i in range(4096):
+        pos = {int(h): j for j, h in enumerate(hid[i])}
+        for j, h in enumerate(b.var_ids[i]):
+            yd[b.var_off[i] + j] = y[k + pos[int(h)]]
+        k += len(hid[i])
+    prec = L.get_precision()
+    sat_b = b.saturated()
+    np.testing.assert_array_equal(sat_b, _sat_dense(b.flat(), yd, prec))
     monkeypatch.setenv("LMMHIP_BATCH", "0")
     b.solve()
     xg = b.values()
     bad, worst = _close(x, xg)
     assert len(bad) == 0, (len(bad), worst)
+    np.testing.assert_array_equal(b.saturated(), sat_b)  # the global engine: the same set
     assert 0 < rounds <= 64
     b.close()
 
@@ -124,14 +174,24 @@ def test_c3_batch_goldens():
 def test_c4_full_size_vs_oracle():
     p = dict(model=L.LV08, n_flows=100_000, seed=1, **C4_PLATFORM)
     s, o = L.System(False), O.System(False)
-    _, vs = s.gen_platform_flows(L.platform_params(**p))
-    _, ov = o.gen_platform_flows(O.platform_params(**p))
+    pc, vs = s.gen_platform_flows(L.platform_params(**p))
+    oc, ov = o.gen_platform_flows(O.platform_params(**p))
+    f = M.export_flat(s)
     s.solve()
     o.solve()
     x, y = s.values_of(vs), o.values_of(ov, len(vs))
     bad, worst = _close(x, y)
     assert len(bad) == 0, (len(bad), worst)
     assert np.all(y > 0)
+    # the same saturated set (maxmin.cpp:948-961 / :470-480): every link through the drop-in
+    # Constraint::get_usage, and the device's own (mm_saturated) against the oracle's values on the flattened system
+    prec = L.get_precision()
+    sat_p = K.saturated(s, {k: L.Constraint(s, int(c)) for k, c in enumerate(pc)}, prec)
+    sat_o = K.saturated(o, dict(enumerate(oc)), prec)
+    assert sat_p == sat_o and len(sat_o) > 0, (len(sat_p ^ sat_o), len(sat_o))
+    pos = {int(h): j for j, h in enumerate(vs)}
+    yd = y[[pos[int(h)] for h in f.var_ids]]
+    np.testing.assert_array_equal(s.device_saturated(), _sat_dense(f, yd, prec))
     excess, infeasible, unbottlenecked = s.check_certificate()
     assert infeasible == 0 and unbottlenecked == 0, (excess, infeasible, unbottlenecked)
 

@@ -67,3 +67,32 @@ def test_wifi_flows_device_match_oracle(model):
     bf = 0.97 if model == 1 else 1.0
     for v in vs:
         assert v.get_value() == pytest.approx(bf * (1.0 / bf) / (2 / 54e6 + 1 / 6e6), rel=1e-9)
+
+
+def test_reference_dragonfly_coords_and_flows_on_device():
+    """The reference's cluster_dragonfly.xml ("3,4;4,3;5,1;2", 120 hosts), pinned by s4u-routing-get-clusters.tesh
+    (tests/golden/dragonfly_coords.json): the library loaded on the GPU box reproduces every `rank: (group, chassis,
+    blade, node)` line (DragonflyZone.cpp:26-35) and the host count, and LV08 flows between hosts of different groups
+    (the blue links the coordinates route over) and of one blade solve on the device to the oracle's values and
+    saturated set."""
+    import json
+    import os
+
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "dragonfly_coords.json")))
+    want = np.array(fx["coords"], dtype=np.int64)[:, 1:]
+    p = dict(model=L.LV08, n_flows=4000, seed=5, **EX_DRAGONFLY)
+    assert L.dragonfly_coords(L.platform_params(**p)).tolist() == want.tolist()
+    assert L.platform_size(L.platform_params(**p))[1] == len(fx["hosts"]) == 120
+    s, o = L.System(False), O.System(False)
+    pc, vs = s.gen_platform_flows(L.platform_params(**p))
+    oc, ov = o.gen_platform_flows(O.platform_params(**p))
+    s.solve()
+    o.solve()
+    got, ref = s.values_of(vs), o.values_of(ov, len(vs))
+    tol = np.maximum(ABS_TOL, REL_TOL * np.abs(ref))
+    assert np.all(np.abs(got - ref) <= tol), float(np.max(np.abs(got - ref)))
+    from tests.lmm_cases import saturated
+
+    prec = L.get_precision()
+    sat_p = saturated(s, {k: L.Constraint(s, int(c)) for k, c in enumerate(pc)}, prec)
+    assert sat_p == saturated(o, dict(enumerate(oc)), prec) and len(sat_p) > 0

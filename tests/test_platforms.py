@@ -193,3 +193,35 @@ def test_product_and_oracle_build_the_same_system(plat, model, kind):
 def test_oracle_restatement_rejects_bad_parameters(kw):
     with pytest.raises(ValueError):
         O.System(False).gen_platform_flows(O.platform_params(**kw))
+
+
+def test_dragonfly_coords_pinned_to_reference_tesh():
+    """DragonflyZone::rankId_to_coords (DragonflyZone.cpp:26-35) and the host count of cluster_dragonfly.xml
+    ("3,4;4,3;5,1;2", hosts node-0 .. node-119), against the 120 host lines and 120 `rank: (group, chassis, blade,
+    node)` lines s4u-routing-get-clusters.tesh prints for it (tests/golden/dragonfly_coords.json): the product's
+    coordinates through the C ABI (lmm_platform_dragonfly_coords) and the oracle's restatement (oracle/platforms.py)."""
+    import json
+    import os
+
+    import numpy as np
+
+    from oracle import platforms as PL
+
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "dragonfly_coords.json")))
+    assert fx["topo_parameters"] == DRAGONFLY["topo_parameters"] and len(fx["coords"]) == 120
+    want = np.array(fx["coords"], dtype=np.int64)
+    assert want[:, 0].tolist() == list(range(120))  # one line per rank, in rank order
+    lo, hi = (int(x) for x in fx["radical"].split("-"))
+    assert fx["hosts"] == [f"node-{i}.simgrid.org" for i in range(lo, hi + 1)]
+    p = L.platform_params(**DRAGONFLY)
+    assert L.platform_size(p)[1] == len(fx["hosts"]) == 120
+    got = L.dragonfly_coords(p)
+    assert got.tolist() == want[:, 1:].tolist()
+    op = O.params_dict(O.platform_params(**DRAGONFLY))
+    plat = PL.make_platform(op)
+    assert plat.n_hosts == 120 and PL.platform_size(op)[1] == 120
+    oc = np.stack(plat.coords(np.arange(120)), axis=1)
+    assert oc.tolist() == want[:, 1:].tolist()
+    # and the other topologies are refused
+    with pytest.raises(L.LmmError, match="not a dragonfly"):
+        L.dragonfly_coords(L.platform_params(**FAT_TREE))
