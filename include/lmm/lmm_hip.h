@@ -226,7 +226,8 @@ int lmmhip_engine_fallbacks(lmmhip_ctx* ctx, int64_t* n);
  * with LMMHIP_ANAT_ROUNDS="r0,r1,..." (at most 4 rounds) every wave of the round engine's vote, saturation and update
  * launches of those rounds writes a record of 20 words — entry and exit on the 100-MHz wall clock, its workgroup,
  * and the clock ticks it spent at each dependent level of its work (lmm_dev.hpp, lmm_anat).  *n = the words of the
- * record array ([slot 0..3][kernel vote / saturation / update][wave 0..8191][20]); out (cap words) gets them,
+ * record array ([slot 0..3][kernel vote / saturation / update / big-constraint saturation][wave 0..8191][20]); out
+ * (cap words) gets them,
  * rounds4 the recorded rounds.  LMMHIP_E_STATE in the product build. */
 int lmmhip_anatomy(lmmhip_ctx* ctx, unsigned long long* out, int64_t cap, int64_t* n, int32_t* rounds4);
 /* Measurement of the persistent engine: on = record, for every grid barrier of the next solves, the

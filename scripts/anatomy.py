@@ -28,7 +28,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SLOTS, KERN, WAVES, FIELDS = 4, 3, 8192, 20
+SLOTS, KERN, WAVES, FIELDS = 4, 4, 8192, 20
 TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 VOTE_LEVELS = ["row record (rtgt, crec)", "variable state (vstate, bound)", "row elements (ccol)",
@@ -38,6 +38,85 @@ SAT_LEVELS = ["candidate id (update segment / vote queue)", "CSC elements (csc_v
               "their constraints' words (cexp)", "decrement pushes (atomics) issued", "candidate state (key, nvote, "
               "ratio, CSC range)"]
 UPD_LEVELS = ["keys + touch flags", "touched constraints' records", "arithmetic + stores + bitmap ballot"]
+# frontier engine (C4): fr_vote / fr_sat / fr_sat_big / fr_update records (lmm_frontier_kernels.hpp)
+FRV_LEVELS = ["queue entry (fq_a, fq_b)", "row (csr_cs) + bound / penalty", "keys + registered floors",
+              "rest of the row + exact ratios", "vote stores + atomics issued"]
+FRS_LEVELS = ["ready test + workgroup collection (LDS)", "(unused)", "CSC elements + variable states",
+              "claimed rows' elements (csr_c, csr_w)", "their constraints' words (cexp)", "decrement pushes issued",
+              "claims + values stored"]
+FRU_LEVELS = ["keys + touch flags", "touched records + floors", "arithmetic + scan prefix + barrier",
+              "slots (vslot)", "queued voters (csc_v, csc_row)", "stores + barriers"]
+
+
+def frontier_view(rec, kind):
+    """A frontier kernel's waves: span, entry / exit spread, the critical wave's levels (kind: fr_vote / fr_sat /
+    fr_satb / fr_upd)."""
+    live = rec[rec[:, 0] > 0]
+    if len(live) == 0:
+        return None
+    t_in, t_out = live[:, 0].astype(np.int64), live[:, 1].astype(np.int64)
+    first, last = int(t_in.min()), int(t_out.max())
+    crit = live[int(np.argmax(t_out))]
+    c_in, c_out = int(crit[0]), int(crit[1])
+    v = {"waves": int(len(live)), "first_entry": first, "last_exit": last, "span_us": us(last - first),
+         "entry_spread_us": {"p50": us(np.median(t_in) - first), "max": us(t_in.max() - first)},
+         "wave_time_us": {"p50": us(np.median(t_out - t_in)), "max": us((t_out - t_in).max())}}
+    seg = {"dispatch/fill (critical wave's entry - first entry)": us(c_in - first)}
+    if kind == "fr_vote":
+        names, cols = ["queue counts (fq_n, segment offsets)"] + FRV_LEVELS, list(range(3, 9))
+        v["counts"] = {"queued_rows": int(live[::4, 10].sum()), "max_revotes_per_lane": int(live[:, 9].max())}
+    elif kind in ("fr_sat", "fr_satb"):
+        names, cols = FRS_LEVELS, list(range(3, 10))
+        v["counts"] = {"chunks": int(live[:, 11].sum()), "fixed_vars": int(live[:, 12].sum()),
+                       "pushes": int(live[:, 13].sum()), "critical_wave_chunks": int(crit[11])}
+        if kind == "fr_satb":
+            v["counts"]["big_constraints"] = int(live[0, 10])
+    else:
+        names, cols = FRU_LEVELS, list(range(3, 9))
+        v["counts"] = {"scanned_slots": int(live[:, 9].sum())}
+    named = 0
+    for n, c in zip(names, cols):
+        if n != "(unused)":
+            seg[n] = us(crit[c])
+            named += int(crit[c])
+    seg["other"] = us(c_out - c_in - named)
+    v["critical_wave"] = {"workgroup": int(crit[2]), "time_us": us(c_out - c_in), "segments_us": seg}
+    v["wave_us_summed_over_waves"] = {n: us(live[:, c].sum()) for n, c in zip(names, cols) if n != "(unused)"}
+    return v
+
+
+def frontier_round_view(recs, rounds, k):
+    r = rounds[k]
+    order = [("fr_vote", 0), ("fr_sat", 1), ("fr_satb", 3), ("fr_upd", 2)]
+    kv = {name: frontier_view(recs[k, i], name) for name, i in order}
+    if kv["fr_vote"] is None or kv["fr_sat"] is None or kv["fr_upd"] is None:
+        return None
+    seq = [n for n, _ in order if kv[n] is not None]
+    out = {"round": r, "kernels": kv}
+    gaps = {}
+    for a, b in zip(seq, seq[1:]):
+        gaps[f"{a} -> {b}"] = us(kv[b]["first_entry"] - kv[a]["last_exit"])
+    nxt = [j for j in range(SLOTS) if rounds[j] == r + 1]
+    end = kv["fr_upd"]["last_exit"]
+    if nxt and recs[nxt[0], 0][:, 0].max() > 0:
+        nv = recs[nxt[0], 0]
+        nfirst = int(nv[nv[:, 0] > 0][:, 0].min())
+        gaps["fr_update -> next fr_vote"] = us(nfirst - end)
+        end = nfirst
+    span = end - kv["fr_vote"]["first_entry"]
+    acc = {}
+    for n in seq:
+        for sg, x in kv[n]["critical_wave"]["segments_us"].items():
+            acc[f"{n}: {sg}"] = x
+    for g, x in gaps.items():
+        acc[f"boundary {g}"] = x
+    out["round_span_us_stamped"] = us(span)
+    out["boundary_gaps_us"] = gaps
+    out["accounting_us"] = acc
+    out["accounted_share"] = round(sum(acc.values()) / max(1e-9, us(span)), 4)
+    out["other_share"] = round(sum(x for sg, x in acc.items() if "other" in sg) / max(1e-9, us(span)), 4)
+    out["shares"] = {sg: round(x / max(1e-9, us(span)), 4) for sg, x in acc.items()}
+    return out
 
 
 def load_records(s, L):
@@ -158,6 +237,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--product-profile", default=None, help="bench.py --profile-json of the product build")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--raw", default=None, help="also save the raw per-wave records here (.npz)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4"], help="c4: the frontier engine on C4")
     args = ap.parse_args()
     assert os.environ.get("LMM_AMD_LIB"), "load the diagnostic build: LMM_AMD_LIB=simgrid_amd/_anat/liblmm_amd.so"
     import torch
@@ -167,37 +248,47 @@ def main():
     assert torch.cuda.is_available()
     s = L.System(False)
     t = time.time()
-    s.gen_synthetic(args.cnst, args.vars, args.k, seed=1, want_vars=False)
+    if args.workload == "c4":
+        s.gen_platform_flows(L.platform_params(model=L.LV08, n_flows=100_000, seed=1, topology=L.FAT_TREE,
+                                               topo_parameters="3;16,16,16;1,16,16;1,1,1", loopback_bw=1e8),
+                             want_vars=False)
+        sysname = "C4: 1e5 LV08 flows on fat tree 3;16,16,16;1,16,16;1,1,1 (seed 1), frontier engine"
+    else:
+        s.gen_synthetic(args.cnst, args.vars, args.k, seed=1, want_vars=False)
+        sysname = f"{args.cnst} x {args.vars} x {args.k} (C2 generator, seed 1)"
     s.prepare()
-    print(f"built {args.cnst}x{args.vars}x{args.k} in {time.time() - t:.1f}s", flush=True)
+    print(f"built {sysname} in {time.time() - t:.1f}s", flush=True)
     for _ in range(args.warmup):
         s.device_solve()
     os.environ["LMMHIP_ANAT_ROUNDS"] = args.rounds
     s.device_solve()
     st = s.last_stats()
     recs, rounds = load_records(s, L)
+    if args.raw:
+        np.savez_compressed(args.raw, recs=recs, rounds=np.array(rounds))
     del os.environ["LMMHIP_ANAT_ROUNDS"]
     s.device_solve()
     plain_ms = s.last_stats()["device_ms"]
-    out = {"system": f"{args.cnst} x {args.vars} x {args.k} (C2 generator, seed 1)", "rounds_total": st["rounds"],
+    out = {"system": sysname, "rounds_total": st["rounds"],
            "stamped_solve_ms": st["device_ms"], "same_build_unstamped_solve_ms": plain_ms,
            "clock": "s_memrealtime, 100 MHz (10 ns ticks), one clock for the chip", "recorded_rounds": rounds,
            "rounds": []}
     for k in range(SLOTS):
         if rounds[k] < 0:
             continue
-        rv = round_view(recs, rounds, k)
+        rv = (frontier_round_view if args.workload == "c4" else round_view)(recs, rounds, k)
         if rv is not None and any(rounds[j] == rounds[k] + 1 for j in range(SLOTS)):
             out["rounds"].append(rv)
     if args.product_profile and os.path.exists(args.product_profile):
         pp = json.load(open(args.product_profile))
-        names = {2: "vote", 4: "saturation", 5: "update"}
+        names = {2: "vote", 4: "saturation", 5: "update"}  # (frontier: slot 4 = fr_sat + fr_sat_big)
         slot, rnd, ms = np.array(pp["launch_slot"]), np.array(pp["launch_round"]), np.array(pp["launch_ms"])
         for rv in out["rounds"]:
             r = rv["round"]
             sel = {names[k]: round(float(1000 * ms[(slot == k) & (rnd == r)].sum()), 2) for k in names}
             rv["product_build_hip_event_us"] = sel
-            rv["product_alive_rows"] = int(pp["alive_vars"][r]) if r < len(pp["alive_vars"]) else None
+            if "alive_vars" in pp:
+                rv["product_alive_rows"] = int(pp["alive_vars"][r]) if r < len(pp["alive_vars"]) else None
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
     for rv in out["rounds"]:

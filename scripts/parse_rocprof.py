@@ -187,7 +187,7 @@ def main():
         for k, e in sorted(t["kernels"].items(), key=lambda kv: -(kv[1]["fetch_bytes"] + kv[1]["write_bytes"]))[:8]:
             print(f"   {k:24s} launches {e['launches']:5d}  fetch/launch {e['fetch_bytes_per_launch'] / 1e6:9.2f} MB"
                   f"  write/launch {e['write_bytes_per_launch'] / 1e6:9.2f} MB")
-    for w in ("c2",):
+    for w in ("c2", "c4", "c5"):
         t = workload_requests(w, tag)
         if t is None:
             continue

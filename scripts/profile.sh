@@ -41,12 +41,15 @@ if has pmc; then
     done
   done
 fi
-if has req; then  # request counts (the request-rate roofline): one counter per pass, C2 and calibration
+REQ_WORKLOADS=${REQ_WORKLOADS:-"c2"}
+if has req; then  # request counts (the request-rate roofline): one counter per pass, per workload
   run gpurun_out/rp_trace_cal.log 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp_trace_cal \
     -o run -- ./scripts/ubench_gather
   for ctr in TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum; do
-    run gpurun_out/rp_${ctr}_c2.log 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_${ctr}_c2 -o run \
-      -- python3 bench.py $(wl_args c2 2)
+    for w in $REQ_WORKLOADS; do
+      run gpurun_out/rp_${ctr}_$w.log 400 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_${ctr}_$w -o run \
+        -- python3 bench.py $(wl_args $w 2)
+    done
     run gpurun_out/rp_cal_$ctr.log 200 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/rp_cal_$ctr -o run \
       -- ./scripts/ubench_gather
   done

@@ -315,7 +315,7 @@ inline int grid_for(int64_t n, int per_block) {
 
 // ---- round anatomy (diagnostic build only: LMM_ANAT=1, scripts/anatomy.py) ----
 // In the rounds named by Dev::anat_r, every wave of mm_vote_lane / mm_saturate_q / mm_update writes one record of
-// kAnatFields words into anat[((slot * 3 + kernel) * kAnatWaves + wave) * kAnatFields]: its entry and exit on the
+// kAnatFields words into anat[((slot * kAnatKernels + kernel) * kAnatWaves + wave) * kAnatFields]: its entry and exit on the
 // 100-MHz wall clock (s_memrealtime, one clock for the whole chip), its workgroup, and the time it spent at each
 // dependent level of its work (the clock read waits for the level's loaded values, so a level's time is from the
 // previous stamp to the arrival of that level's data).  The stamps serialise what the real kernel overlaps: read
@@ -325,9 +325,11 @@ inline int grid_for(int64_t n, int per_block) {
 #define LMM_ANAT 0
 #endif
 constexpr int kAnatSlots = 4;
+constexpr int kAnatKernels = 4;
 constexpr int kAnatFields = 20;
 constexpr int kAnatWaves = 8192;
-enum : int { ANAT_VOTE = 0, ANAT_SAT = 1, ANAT_UPD = 2 };
+// the round engine's vote / saturation / update; the frontier engine's fr_vote / fr_sat / fr_update / fr_sat_big
+enum : int { ANAT_VOTE = 0, ANAT_SAT = 1, ANAT_UPD = 2, ANAT_SATB = 3 };
 #if LMM_ANAT
 __device__ __forceinline__ unsigned long long anat_now() {
   unsigned long long t;
@@ -371,7 +373,7 @@ __device__ __forceinline__ unsigned long long* anat_rec(const Dev& s, int slot, 
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
   if (slot < 0 || wave >= kAnatWaves)
     return nullptr;
-  return s.anat + ((int64_t(slot) * 3 + kernel) * kAnatWaves + wave) * kAnatFields;
+  return s.anat + ((int64_t(slot) * kAnatKernels + kernel) * kAnatWaves + wave) * kAnatFields;
 }
 #endif
 

@@ -130,8 +130,25 @@ __device__ __forceinline__ uint32_t row_floor32(uint32_t sk, uint32_t mk, double
   return fl <= mk ? 0u : fl;
 }
 
+// (LMM_ANAT: `an` = the dependent levels into ar->lv: 1 row (csr_cs) + bound / penalty, 2 keys + floors, 3 the rest of
+// the row + exact ratios, 4 the vote's stores and atomics issued)
 template <int R, bool kMinfl = true, bool kEarly = true>
-__device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b, uint32_t e, int round) {
+__device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b, uint32_t e, int round
+#if LMM_ANAT
+                                         , bool an = false, AnatAcc* ar = nullptr
+#endif
+) {
+#if LMM_ANAT
+#define FV_LVL(i, dep)       \
+  do {                       \
+    if (an)                  \
+      ANAT_LVL(*ar, i, dep); \
+  } while (0)
+#else
+#define FV_LVL(i, dep) \
+  do {                 \
+  } while (0)
+#endif
   const uint32_t* __restrict__ key = s.key32;
   // (a queued variable is alive: votes are registered only by alive variables, and the slot of a variable
   // fixed since — at its bound, by fr_revote — was cleared when it was queued)
@@ -145,12 +162,30 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
     cc[i] = x.x;
     sl[i] = uint32_t(x.y);
   }
+#if LMM_ANAT
+  if (an) {
+    int sc = 0;
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      sc += cc[i] + int(sl[i]);
+    FV_LVL(1, vb + p + double(sc));
+  }
+#endif
   uint32_t kk[R], mf[R];  // keys and registered floors of the row's constraints, their loads in flight together
 #pragma unroll
   for (int i = 0; i < R; i++) {
     kk[i] = cc[i] >= 0 ? key[cc[i]] : kDead32;
     mf[i] = kMinfl && kEarly && cc[i] >= 0 ? s.minfl[cc[i]] : 0u;
   }
+#if LMM_ANAT
+  if (an) {
+    uint32_t sk0 = 0;
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      sk0 += kk[i] + mf[i];
+    FV_LVL(2, sk0);
+  }
+#endif
   uint32_t mk = kDead32;
 #pragma unroll
   for (int i = 0; i < R; i++)
@@ -209,6 +244,7 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
       }
     }
   }
+  FV_LVL(3, minr + double(newt + nmin));
   if (vb > 0 && vb * p < minr) {  // fixed at its bound (maxmin.cpp:587-589)
     s.vstate[v] = round + 1;
     s.x[v] = vb;
@@ -250,12 +286,15 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
     mfn = s.minfl[newt];
   if (kMinfl && fl < mfn)
     atomicMin(&s.minfl[newt], fl);
-  if (newt == t)
+  if (newt == t) {
+    FV_LVL(4, 0u);
     return FR_STAY;
+  }
   if (t >= 0 && kt != kDead32)
     atomicAdd(&s.nvote[t], mult_old);
   atomicSub(&s.nvote[newt], mult_new);
   s.rtgt[0][v] = newt;
+  FV_LVL(4, 0u);
   return FR_MOVE;
 }
 
@@ -296,7 +335,12 @@ __global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
 // kP: called by the persistent kernel (fr_persist), where the counts were written in the same launch: read relaxed
 // (the multi-launch kernel's plain loads may come from the scalar cache, which a launch boundary keeps coherent).
 template <bool kEarly, int R, bool kP = false>
-__device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, int vb) {
+__device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, int vb
+#if LMM_ANAT
+                                            , bool an = false, AnatAcc* aa = nullptr, AnatAcc* ar = nullptr,
+                                            unsigned* wc = nullptr
+#endif
+) {
   // spb (<= kFVS) consecutive segments per workgroup: on C2 ~170 queued rows, one pass, and the launch's
   // workgroups resident at once; small systems keep one segment per workgroup (more workgroups)
   const int64_t nseg = (int64_t(s.nC) + kFB - 1) / kFB;
@@ -310,15 +354,34 @@ __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, in
     seg[k] = k < spb && sg < nseg ? s.cnst_ptr[sg * kFB] : 0u;
     pre[k + 1] = pre[k] + n[k];
   }
+#if LMM_ANAT
+  if (an) {
+    ANAT_LVL(*aa, 0, pre[kFVS] + int(seg[0]));
+    wc[0] = unsigned(pre[kFVS]);
+  }
+#endif
   for (int i = threadIdx.x; i < pre[kFVS]; i += kFB) {
     int k = 0;
 #pragma unroll
     for (int q = 1; q < kFVS; q++)
       k += i >= pre[q];
     const uint32_t at = seg[k] + uint32_t(i - pre[k]);
+#if LMM_ANAT
+    if (an) {
+      ar->at = anat_now();
+      wc[1]++;
+    }
+#endif
     const unsigned long long a = s.fq_a[at], rw = s.fq_b[at];
+#if LMM_ANAT
+    if (an)
+      ANAT_LVL(*ar, 0, a + rw);
+    const int o = fr_revote<R, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
+                                             uint32_t(rw >> 32), round, an, ar);
+#else
     const int o = fr_revote<R, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
                                              uint32_t(rw >> 32), round);
+#endif
     if (s.vstat) {
       fr_diag(s, round, 6, true);
       fr_diag(s, round, 4, o == FR_MOVE);
@@ -328,6 +391,14 @@ __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, in
 }
 
 template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
+#if LMM_ANAT
+  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_VOTE);
+  const bool an = arec != nullptr;
+  AnatAcc aa{}, ar{};
+  unsigned wc[2] = {0, 0};  // queued rows of the workgroup, this lane's re-votes
+  const unsigned long long t_in = an ? anat_now() : 0;
+  aa.at = t_in;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   if (s.ctl[CTL_PALIVE0 + ((round - 1) & 1)] == 0) {  // written by the last fr_update
@@ -337,7 +408,29 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
   }
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_PALIVE0 + (round & 1)] = 0;  // this round's fr_update raises it
+#if LMM_ANAT
+  fr_vote_blk<kEarly, R>(s, round, spb, blockIdx.x, an, &aa, &ar, wc);
+  if (an) {  // the wave's record: queue-count level (lane 0), the re-vote levels of its slowest lane
+    const unsigned long long t_out = anat_now();
+    unsigned lv[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++)
+      lv[i] = anat_wmax(ar.lv[i]);
+    const unsigned nre = anat_wmax(wc[1]);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      arec[0] = t_in;
+      arec[1] = t_out;
+      arec[2] = blockIdx.x;
+      arec[3] = aa.lv[0];
+      for (int i = 0; i < 5; i++)
+        arec[4 + i] = lv[i];
+      arec[9] = nre;
+      arec[10] = wc[0];
+    }
+  }
+#else
   fr_vote_blk<kEarly, R>(s, round, spb, blockIdx.x);
+#endif
 }
 
 // Saturation of one 64-element CSC chunk of ready constraint c: saturate_chunk's decisions and arithmetic
@@ -349,8 +442,30 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
 // atomicCAS, as before).
 constexpr int kFrSatU = 8;
 
+// (LMM_ANAT: `an` = the chunk's dependent levels into aa->lv: 2 CSC elements + variable states, 3 the claimed rows'
+// elements, 4 their constraints' words, 5 the pushes issued, 6 the claims / values stored; wc[1] chunks, wc[2] fixed
+// variables, wc[3] pushed elements)
 __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t cend,
-                                             int round, int lane, int* pre, bool dup) {
+                                             int round, int lane, int* pre, bool dup
+#if LMM_ANAT
+                                             , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
+#endif
+) {
+#if LMM_ANAT
+  if (an) {
+    aa->at = anat_now();
+    wc[1]++;
+  }
+#define FS_LVL(i, dep)       \
+  do {                       \
+    if (an)                  \
+      ANAT_LVL(*aa, i, dep); \
+  } while (0)
+#else
+#define FS_LVL(i, dep) \
+  do {                 \
+  } while (0)
+#endif
   const int q = lane & 3;
   const uint32_t j = j0 + lane;
   int32_t lv = -1;
@@ -374,6 +489,12 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
   } else {
     rb = re = 0;
   }
+#if LMM_ANAT
+  if (an) {
+    ANAT_LVL(*aa, 2, lv);
+    wc[2] += unsigned(__popcll(__ballot(lv >= 0)));
+  }
+#endif
   int incl = len;  // inclusive wave scan of the row lengths
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -401,10 +522,30 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
       cc[u] = f < total ? s.csr_c[k] : -1;
       ww[u] = f < total ? s.csr_w[k] : 0.0;
     }
+#if LMM_ANAT
+    if (an) {
+      double sw = 0.0;
+#pragma unroll
+      for (int u = 0; u < kFrSatU; u++) {
+        sw += ww[u] + double(cc[u]);
+        wc[3] += unsigned(__popcll(__ballot(cc[u] >= 0)));
+      }
+      ANAT_LVL(*aa, 3, sw);
+    }
+#endif
     int32_t cx[kFrSatU];
 #pragma unroll
     for (int u = 0; u < kFrSatU; u++)
       cx[u] = cc[u] >= 0 ? s.cexp[cc[u]] : kCexpDead;  // scales, policy and liveness in one word
+#if LMM_ANAT
+    if (an) {
+      int32_t sx = 0;
+#pragma unroll
+      for (int u = 0; u < kFrSatU; u++)
+        sx += cx[u];
+      ANAT_LVL(*aa, 4, sx);
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < kFrSatU; u++) {
       const double ox = __shfl(lx, ol[u], kWave);
@@ -436,6 +577,7 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
           atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
       }
     }
+    FS_LVL(5, 0u);
   }
   if (lv >= 0) {  // the claim and the value, last
     if (!dup)
@@ -443,11 +585,19 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
     s.x[lv] = lx;
   }
   __builtin_amdgcn_wave_barrier();
+  FS_LVL(6, 0u);
 }
 
 // The collected ready constraints' chunks, round-robin over the workgroup's waves (sat_flush with fr_sat_chunk).
+#if LMM_ANAT
+#define FR_ANAT_PARAMS , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
+#define FR_ANAT_ARGS , an, aa, wc
+#else
+#define FR_ANAT_PARAMS
+#define FR_ANAT_ARGS
+#endif
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L) {
+__device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int ta = L.na, tb = L.nb;
@@ -465,7 +615,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
                      s.cdup[cc] != 0);
     else
       fr_sat_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
-                   s.cdup[cc] != 0);
+                   s.cdup[cc] != 0 FR_ANAT_ARGS);
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -477,7 +627,8 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 constexpr int kFS = 1024;
 
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L) {
+__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L
+                                           FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t c = int64_t(vb) * NB + threadIdx.x;
@@ -527,15 +678,42 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
       s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
   }
   __syncthreads();
+#if LMM_ANAT
+  if (an) {  // the ready test and the workgroup's collection, then the chunks
+    ANAT_LVL(*aa, 0, ta);
+    wc[0] = unsigned(tb);
+  }
+#endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld>(s, round, L);
+    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
 }
 
 template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+#if LMM_ANAT
+  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
+  const bool an = arec != nullptr;
+  AnatAcc aa{};
+  unsigned wc[4] = {0, 0, 0, 0};  // the workgroup's chunks, this wave's chunks, fixed variables, pushed elements
+  const unsigned long long t_in = an ? anat_now() : 0;
+  aa.at = t_in;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   __shared__ SatLds<kFS, kFS> L;
+#if LMM_ANAT
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
+  if (an && (threadIdx.x & (kWave - 1)) == 0) {
+    arec[0] = t_in;
+    arec[1] = anat_now();
+    arec[2] = blockIdx.x;
+    for (int i = 0; i < 7; i++)
+      arec[3 + i] = aa.lv[i];
+    for (int i = 0; i < 4; i++)
+      arec[10 + i] = wc[i];
+  }
+#else
   fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
+#endif
 }
 
 // The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
@@ -543,7 +721,7 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
 // (the grid's waves over the list: wave / nwaves; wpre = the calling wave's 64-int LDS scratch)
 template <bool kP = false>
 __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bigw, int nb, int64_t wave,
-                                                 int64_t nwaves, int* wpre) {
+                                                 int64_t nwaves, int* wpre FR_ANAT_PARAMS) {
   const int lane = threadIdx.x & (kWave - 1);
   for (int64_t g = wave; g < int64_t(nb) * bigw; g += nwaves) {
     const int32_t c = kP ? ld_rlx(&s.ready[g / bigw]) : s.ready[g / bigw];
@@ -552,16 +730,32 @@ __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bi
     const uint32_t ce = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
     for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
-      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup);
+      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup FR_ANAT_ARGS);
     if (k == 0 && lane == 0)
       s.ctouch[c] = 2;
   }
 }
 
 __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round, int bigw) {
+#if LMM_ANAT
+  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SATB);
+  const bool an = arec != nullptr;
+  AnatAcc aa{};
+  unsigned wc[4] = {0, 0, 0, 0};
+  const unsigned long long t_in = an ? anat_now() : 0;
+  aa.at = t_in;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   const int nb = s.ctl[CTL_NREADY];
+#if LMM_ANAT
+  if (an && (threadIdx.x & (kWave - 1)) == 0) {
+    arec[0] = t_in;
+    arec[1] = anat_now();
+    arec[2] = blockIdx.x;
+    arec[10] = unsigned(nb);
+  }
+#endif
   if (nb == 0)
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -570,7 +764,18 @@ __global__ void __launch_bounds__(kBlock) fr_sat_big(Dev s, int round, int bigw)
   const int w = threadIdx.x / kWave;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+#if LMM_ANAT
+  fr_sat_big_waves(s, round, bigw, nb, wave, nwaves, wpre[w], an, &aa, wc);
+  if (an && (threadIdx.x & (kWave - 1)) == 0) {
+    arec[1] = anat_now();
+    for (int i = 0; i < 7; i++)
+      arec[3 + i] = aa.lv[i];
+    for (int i = 1; i < 4; i++)
+      arec[10 + i] = wc[i];
+  }
+#else
   fr_sat_big_waves(s, round, bigw, nb, wave, nwaves, wpre[w]);
+#endif
 }
 
 // Constraint update (maxmin.cpp:603-658; the arithmetic of update_groups) + slot scan.  Workgroup b owns
@@ -592,8 +797,11 @@ struct FrUpdLds {
 
 // kP: called by fr_persist (the control words another workgroup reads or adds to in the same launch: relaxed
 // atomic stores; the multi-launch kernel keeps its plain stores).
+// (LMM_ANAT: `an` = the levels into aa->lv: 0 keys + touch flags, 1 touched records, 2 arithmetic + scan prefix +
+// barrier, 3 slots, 4 queued voters' variable and row, 5 stores + barriers; wc[0] scanned slots)
 template <bool kP = false>
-__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int vb, FrUpdLds& U) {
+__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int vb, FrUpdLds& U
+                                              FR_ANAT_PARAMS) {
   int& qn = U.qn;
   auto& pre = U.pre;
   uint32_t* mf = U.mf;
@@ -612,6 +820,10 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   const bool in = c < s.nC;
   const uint32_t okey = in ? s.key32[c] : kDead32;
   const unsigned tf = in ? unsigned(s.ctouch[c]) : 0u;  // 1 = received decrements, 2 = saturated this round
+#if LMM_ANAT
+  if (an)
+    ANAT_LVL(*aa, 0, okey + tf);
+#endif
   const bool live0 = okey != kDead32;
   const bool sat = live0 && tf == 2;
   const bool live = live0 && !sat;
@@ -635,6 +847,10 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
     cb = s.cnst_ptr[c];
     cend = s.cnst_ptr[c + 1];
   }
+#if LMM_ANAT
+  if (an)
+    ANAT_LVL(*aa, 1, rem + use + bnd + double(qx + qy + qz) + double(ce + nv + int(mfl + cb + cend)));
+#endif
   const bool fat = tch && (ce & kCexpFat);
   // FATPIPE: recompute only when a removed element reached the usage (fat_bits in duse)
   const bool fre = fat && !(__longlong_as_double((long long)qy) < use);
@@ -702,6 +918,12 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   pre[w][lane] = incl - len;
   mf[threadIdx.x] = kNoVoter;
   __syncthreads();  // (qn, pre, mf)
+#if LMM_ANAT
+  if (an) {
+    ANAT_LVL(*aa, 2, total);
+    wc[0] = unsigned(total);
+  }
+#endif
   const uint32_t seg = s.cnst_ptr[int64_t(vb) * kFB];
   for (int f0 = 0; f0 < total; f0 += kFrScanU * kWave) {  // wave-uniform (one pass up to 512 slots)
     int ol[kFrScanU];
@@ -719,6 +941,15 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
       jj[u] = uint32_t(__shfl(int(cb), o, kWave)) + uint32_t(f - pre[w][o]);
       fl[u] = f < total ? s.vslot[jj[u]] : kNoVoter;
     }
+#if LMM_ANAT
+    if (an) {
+      uint32_t sf = 0;
+#pragma unroll
+      for (int u = 0; u < kFrScanU; u++)
+        sf += fl[u];
+      ANAT_LVL(*aa, 3, sf);
+    }
+#endif
     bool q[kFrScanU];
     int32_t qv[kFrScanU];
     unsigned long long qr[kFrScanU];
@@ -731,6 +962,15 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
       qv[u] = q[u] ? s.csc_v[jj[u]] : 0;
       qr[u] = q[u] ? s.csc_row[jj[u]] : 0ull;
     }
+#if LMM_ANAT
+    if (an) {
+      unsigned long long sq = 0;
+#pragma unroll
+      for (int u = 0; u < kFrScanU; u++)
+        sq += qr[u] + unsigned(qv[u]);
+      ANAT_LVL(*aa, 4, sq);
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < kFrScanU; u++) {
       const unsigned long long m = __ballot(q[u]);
@@ -783,13 +1023,37 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   }
   if (__syncthreads_or(tch || sat) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
+#if LMM_ANAT
+  if (an)
+    ANAT_LVL(*aa, 5, 0u);
+#endif
 }
 
 __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) {
+#if LMM_ANAT
+  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_UPD);
+  const bool an = arec != nullptr;
+  AnatAcc aa{};
+  unsigned wc[1] = {0};
+  const unsigned long long t_in = an ? anat_now() : 0;
+  aa.at = t_in;
+#endif
   if (s.ctl[CTL_DONE])
     return;
   __shared__ FrUpdLds U;
+#if LMM_ANAT
+  fr_update_blk(s, round, prec, blockIdx.x, U, an, &aa, wc);
+  if (an && (threadIdx.x & (kWave - 1)) == 0) {
+    arec[0] = t_in;
+    arec[1] = anat_now();
+    arec[2] = blockIdx.x;
+    for (int i = 0; i < 6; i++)
+      arec[3 + i] = aa.lv[i];
+    arec[9] = wc[0];
+  }
+#else
   fr_update_blk(s, round, prec, blockIdx.x, U);
+#endif
 }
 
 }  // namespace lmmdev

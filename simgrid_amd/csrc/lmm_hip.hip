@@ -1313,7 +1313,7 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   for (int k = 0; k < kAnatSlots; k++)
     c->d.anat_r[k] = -1000;
   if (LMM_ANAT && std::getenv("LMMHIP_ANAT_ROUNDS")) {
-    const size_t bytes = sizeof(unsigned long long) * size_t(kAnatSlots) * 3 * kAnatWaves * kAnatFields;
+    const size_t bytes = sizeof(unsigned long long) * size_t(kAnatSlots) * kAnatKernels * kAnatWaves * kAnatFields;
     if (!c->anat)
       HIPCHK(hipMalloc(&c->anat, bytes));
     HIPCHK(hipMemsetAsync(c->anat, 0, bytes, c->stream));
@@ -2241,7 +2241,7 @@ int lmmhip_persist_profile_blocks(lmmhip_ctx* c, int64_t* t, int64_t cap, int64_
 int lmmhip_anatomy(lmmhip_ctx* c, unsigned long long* out, int64_t cap, int64_t* n, int32_t* rounds4) {
   if (!c || !n)
     return fail(LMMHIP_E_ARG, "null argument");
-  const int64_t words = int64_t(kAnatSlots) * 3 * kAnatWaves * kAnatFields;
+  const int64_t words = int64_t(kAnatSlots) * kAnatKernels * kAnatWaves * kAnatFields;
   *n = 0;
   if (!LMM_ANAT)
     return fail(LMMHIP_E_STATE, "not an anatomy build (make EXTRA_HIPFLAGS=-DLMM_ANAT=1)");

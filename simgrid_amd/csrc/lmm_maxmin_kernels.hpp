@@ -179,6 +179,21 @@ __device__ __forceinline__ void rdq_push(const Dev& s, int32_t c, int qround) {
     s.rdq[q][atomicAdd(&s.ctl[CTL_RDQ0 + q], 1)] = c;
   }
 }
+// The same for a whole wave (every lane calls it; c < 0: nothing to queue): one returning atomic on the queue's
+// counter per wave instead of one per queued constraint.  Round 6 anatomy (profiles/r06_c2_round_anatomy.json): in
+// the tail, when the re-votes make many constraints ready at once, the per-lane adds on the one counter were the
+// vote's longest level (11 of 27 us in round 200's slowest wave).  The queue's order does not matter: the saturation
+// of one round's ready constraints commutes (no shared alive variable, fixed-point integer decrements).
+#ifndef LMM_RDQ_WAVE
+#define LMM_RDQ_WAVE 1  // (build knob, measurement: 0 = one queue-counter add per queued constraint, as in round 5)
+#endif
+__device__ __forceinline__ void rdq_push_wave(const Dev& s, int32_t c, int qround) {
+  const bool first = c >= 0 && atomicExch(&s.rqst[c], qround) != qround;
+  const int q = qround & 1;
+  const int pos = wave_append(first, &s.ctl[CTL_RDQ0 + q]);
+  if (first)
+    s.rdq[q][pos] = c;
+}
 
 __device__ __forceinline__ unsigned row_floor(unsigned sk, unsigned mk, double vb, double p) {
   unsigned fl = sk;
@@ -466,9 +481,12 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
   do {                 \
   } while (0)
 #endif
+// kRdq: a constraint this re-vote made ready (nothing votes elsewhere any more) is returned in *rdq_c for the
+// caller's wave-wide queueing (rdq_push_wave), or queued here when rdq_c is null.
 template <int R, bool kRec = false, bool kRdq = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
-                                         int* st_elems, const uint16_t* __restrict__ key VR_ANAT_PARAMS) {
+                                         int* st_elems, const uint16_t* __restrict__ key, int* rdq_c = nullptr
+                                         VR_ANAT_PARAMS) {
 #if LMM_ANAT
   if (an)
     aa->at = anat_now();
@@ -617,8 +635,12 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
     atomicAdd(&s.nvote[t], mult_old);
   if (kRdq) {
     const int old = atomicSub(&s.nvote[newt], mult_new);
-    if (old == mult_new)  // nothing votes elsewhere any more: ready
-      rdq_push(s, newt, round);
+    if (old == mult_new) {  // nothing votes elsewhere any more: ready
+      if (rdq_c)
+        *rdq_c = newt;
+      else
+        rdq_push(s, newt, round);
+    }
     VR_LVL(5, old);
   } else {
     atomicSub(&s.nvote[newt], mult_new);
@@ -760,18 +782,23 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
         nq += kWave;
         const int row = qw[qn + lane];
         __builtin_amdgcn_wave_barrier();
+        int pc = -1;  // (kRdq) a constraint this lane's re-vote made ready
 #if LMM_ANAT
         if (an) {
           aa->at = anat_now();
           wcnt[1]++;
         }
         if (kDiag == 0)
-          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, an, ar);
+          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr, an, ar);
+        if (kRdq && kDiag == 0)
+          rdq_push_wave(s, pc, round);
         if (an)
           ANAT_LVL(*aa, 8, 0u);
 #else
         if (kDiag == 0)
-          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key);
+          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr);
+        if (kRdq && kDiag == 0)
+          rdq_push_wave(s, pc, round);
 #endif
       }
     }
@@ -782,14 +809,21 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
     aa->at = anat_now();
     wcnt[1]++;
   }
+  int pc = -1;
   if (kDiag == 0 && lane < qn)
-    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, an, ar);
+    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr, an, ar);
   __builtin_amdgcn_wave_barrier();
+  if (kRdq && kDiag == 0 && qn > 0)
+    rdq_push_wave(s, pc, round);
   if (an && qn > 0)
     ANAT_LVL(*aa, 8, 0u);
 #else
+  int pc = -1;
   if (kDiag == 0 && lane < qn)
-    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key);
+    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr);
+  __builtin_amdgcn_wave_barrier();
+  if (kRdq && kDiag == 0 && qn > 0)  // (wave-uniform)
+    rdq_push_wave(s, pc, round);
 #endif
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
@@ -1355,11 +1389,11 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 // them, mm_saturate's prefix and binary search over their counts) then the vote's queue; K waves per entry;
 // an entry is saturated when it is still alive with nothing voting elsewhere (every vote of the round is in).
 // Block 0 empties the other parity's vote queue, which the next round's vote fills.
-// LMM_SATQ_SPEC: a candidate's ratio, CSC range and duplicate flag loaded with its key and vote count (build knob).
-// Round 5, same box, two passes (scripts/gpu_r05_spec2.sh, profiles/r05_ab_c2_spec2.json): C2 24.285-24.293 ms
-// against 24.309-24.340 without — small, but in both passes; kept.
-#ifndef LMM_SATQ_SPEC
-#define LMM_SATQ_SPEC 1
+// A candidate's ratio, CSC range and duplicate flag are loaded with its key and vote count (round 5, same box, two
+// passes, profiles/r05_ab_c2_spec2.json: C2 24.285-24.293 ms against 24.309-24.340 without).  LMM_SATQ_PIPE (build
+// knob): the next task's candidate state loaded ahead (round 6).
+#ifndef LMM_SATQ_PIPE
+#define LMM_SATQ_PIPE 1
 #endif
 template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
 #if LMM_ANAT
@@ -1416,8 +1450,53 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
   const int32_t* __restrict__ q = s.rdq[round & 1];
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  for (int64_t g = wave; g < (int64_t(total) + nq) * K; g += nwaves) {  // wave-uniform
+  const int64_t T = (int64_t(total) + nq) * K;  // tasks: (candidate, wave k of its K)
+  auto cand_of = [&](int64_t g) -> int32_t {   // the candidate of task g: the update's segments, then the vote's queue
     const int64_t i = g / K;
+    if (i >= total)
+      return q[i - total];
+    int lo = 0;  // last segment with pre[seg] <= i
+#pragma unroll
+    for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
+      if (lo + step < ublocks && pre[lo + step] <= i)
+        lo += step;
+    return s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
+  };
+#if LMM_SATQ_PIPE
+  // Software-pipelined over the wave's tasks (round 6): the next task's candidate state (key, vote count, ratio, CSC
+  // range, duplicate flag) and the candidate id of the task after it are loaded before this task's chunks, so a task
+  // starts with its CSC element loads instead of two dependent levels (candidate id, then its state).  The round
+  // anatomy (profiles/r06_c2_round_anatomy.json) shows a tail-round wave running ~9 tasks one after the other.
+  struct CandSt {
+    int32_t c;
+    unsigned kc;
+    int nv;
+    double r;
+    uint32_t cb, ce;
+    bool dup;
+  };
+  auto state_of = [&](int32_t c) -> CandSt {
+    CandSt x;
+    x.c = c;
+    if (c < 0) {
+      x.kc = kDeadKey;
+      x.nv = 1;
+      x.r = 0.0;
+      x.cb = x.ce = 0;
+      x.dup = false;
+      return x;
+    }
+    x.kc = s.key[c];
+    x.nv = s.nvote[c];
+    x.r = ld_rlx(&s.cst[c].ratio);
+    x.cb = s.cnst_ptr[c];
+    x.ce = s.cnst_ptr[c + 1];
+    x.dup = s.cdup[c] != 0;
+    return x;
+  };
+  CandSt cur = state_of(wave < T ? cand_of(wave) : -1);
+  int32_t cnext = wave + nwaves < T ? cand_of(wave + nwaves) : -1;
+  for (int64_t g = wave; g < T; g += nwaves) {  // wave-uniform
     const int k = int(g % K);
 #if LMM_ANAT
     if (an) {
@@ -1425,19 +1504,27 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
       wc[0]++;
     }
 #endif
-    int32_t c;
-    if (i < total) {
-      int lo = 0;  // last segment with pre[seg] <= i
-#pragma unroll
-      for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
-        if (lo + step < ublocks && pre[lo + step] <= i)
-          lo += step;
-      c = s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
-    } else {
-      c = q[i - total];
+    SC_LVL(6, cur.r + double(cur.kc + unsigned(cur.nv) + cur.cb + cur.ce + unsigned(cur.dup)));
+    const CandSt nxt = state_of(cnext);  // (issued before this task's chunk loads)
+    cnext = g + 2 * nwaves < T ? cand_of(g + 2 * nwaves) : -1;
+    if (cur.kc != kDeadKey && cur.nv == 0) {
+      if (k == 0 && lane == 0)
+        s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
+      saturate_one_pre<K>(s, cur.c, k, round, lane, wpre[w], cur.r, cur.cb, cur.ce, cur.dup SC_ANAT_ARGS);
     }
+    cur = nxt;
+  }
+#else
+  for (int64_t g = wave; g < T; g += nwaves) {  // wave-uniform
+    const int k = int(g % K);
+#if LMM_ANAT
+    if (an) {
+      aa->at = anat_now();
+      wc[0]++;
+    }
+#endif
+    const int32_t c = cand_of(g);
     SC_LVL(0, c);
-#if LMM_SATQ_SPEC
     // the constraint's ratio, CSC range and duplicate flag loaded with its key and count (one dependent level less;
     // a candidate that is not ready discards them)
     const unsigned kc = s.key[c];
@@ -1451,14 +1538,8 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     if (k == 0 && lane == 0)
       s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
     saturate_one_pre<K>(s, c, k, round, lane, wpre[w], r, cb, cend, dup SC_ANAT_ARGS);
-#else
-    if (s.key[c] == kDeadKey || s.nvote[c] != 0)
-      continue;
-    if (k == 0 && lane == 0)
-      s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-    saturate_one<K>(s, c, k, round, lane, wpre[w]);
-#endif
   }
+#endif
 #if LMM_ANAT
   if (an && lane == 0) {
     arec[0] = t_in;
