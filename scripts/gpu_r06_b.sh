@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6, second GPU pass: same-box A/B of the tail levers the round anatomy named (abl/base: round-5 vote queue +
-# saturation loop; abl/rdq: + the vote's wave-aggregated ready queue; the product build: + the saturation's
-# pipelined candidate loads), C2 and C2 stress; the C2 anatomy of the new build (raw records too), the C4 anatomy
+# saturation loop; abl/rdq: + the vote's wave-aggregated ready queue; abl/pipe: + the saturation's pipelined
+# candidate loads; the product build: + the update's candidates in 8 lists instead of ~1,024 segments), C2 and C2
+# stress; the C2 anatomy of the new build (raw records too), the C4 anatomy
 # (frontier engine), and the dependency-depth comparison (oracle depth vs device rounds, scripts/depth.py).
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -13,7 +14,7 @@ step() {  # name seconds cmd...
   if [ $rc -ne 0 ]; then echo "STOP $name rc=$rc"; tail -20 "gpurun_out/$name.log"; exit $rc; fi
 }
 for pass in 1 2; do
-  for v in base rdq new; do
+  for v in base rdq pipe new; do
     lib=abl/$v/liblmm_amd.so; [ $v = new ] && lib=simgrid_amd/_lib/liblmm_amd.so
     step ab_c2_${v}_$pass 200 env LMM_AMD_LIB=$lib python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dropin-steps 0
   done

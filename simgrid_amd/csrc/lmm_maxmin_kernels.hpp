@@ -173,6 +173,14 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
 // ready (rdq, one entry per constraint and round through the rqst stamps, which the update sets too).
 // mm_saturate_q re-checks every entry after the vote (alive, nothing voting elsewhere).
 constexpr int kUSeg = 1024;  // update candidates per workgroup segment (>= the constraints a workgroup updates)
+// LMM_UPD_XL (build knob): the update's workgroups append their ready candidates to 8 lists (workgroup b -> list
+// b % 8, i.e. its XCD under the round-robin placement: the adds on one length word come from one XCD; speed only)
+// instead of writing a segment each, so the saturation reads 8 lengths instead of building the prefix of ~1,024
+// segment counts in every workgroup (round 6 anatomy: 1.4-2.8 us at the start of every saturation launch).
+#ifndef LMM_UPD_XL
+#define LMM_UPD_XL 1
+#endif
+constexpr int kUXL = 8;
 __device__ __forceinline__ void rdq_push(const Dev& s, int32_t c, int qround) {
   if (atomicExch(&s.rqst[c], qround) != qround) {
     const int q = qround & 1;
@@ -1408,11 +1416,27 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     return;
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_RDQ0 + ((round + 1) & 1)] = 0;
+  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+#if LMM_UPD_XL
+  // the previous round's update wrote parity (round - 1) & 1; this round's update will add to parity round & 1, whose
+  // lengths the previous saturation read: reset here (block 0), before that update starts
+  if (blockIdx.x == 0 && threadIdx.x < kUXL)
+    s.ctl[CTL_UX0 + kUXL * (round & 1) + threadIdx.x] = 0;
+  int xpre[kUXL + 1];  // prefix of the 8 list lengths (wave-uniform, registers)
+  xpre[0] = 0;
+#pragma unroll
+  for (int x = 0; x < kUXL; x++)
+    xpre[x + 1] = xpre[x] + s.ctl[CTL_UX0 + kUXL * ((round - 1) & 1) + x];
+  const int total = xpre[kUXL];
+  const int64_t xcap = int64_t(ublocks + kUXL - 1) / kUXL * kUSeg;
+#if LMM_ANAT
+  const unsigned long long t_pre = an ? anat_now() : 0;
+#endif
+#else
   __shared__ int pre[kMaxBlocks + 1];
   __shared__ int wsum[kBlock / kWave];
-  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
   constexpr int kPer = kMaxBlocks / kBlock;
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   int loc[kPer];
   int sum = 0;
 #pragma unroll
@@ -1446,6 +1470,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
 #if LMM_ANAT
   const unsigned long long t_pre = an ? anat_now() : 0;
 #endif
+#endif
   const int nq = s.ctl[CTL_RDQ0 + (round & 1)];
   const int32_t* __restrict__ q = s.rdq[round & 1];
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
@@ -1455,12 +1480,20 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     const int64_t i = g / K;
     if (i >= total)
       return q[i - total];
+#if LMM_UPD_XL
+    int x = 0;  // the list holding candidate i
+#pragma unroll
+    for (int y = 1; y < kUXL; y++)
+      x += i >= xpre[y];
+    return s.useg[int64_t(x) * xcap + (i - xpre[x])];
+#else
     int lo = 0;  // last segment with pre[seg] <= i
 #pragma unroll
     for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
       if (lo + step < ublocks && pre[lo + step] <= i)
         lo += step;
     return s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
+#endif
   };
 #if LMM_SATQ_PIPE
   // Software-pipelined over the wave's tasks (round 6): the next task's candidate state (key, vote count, ratio, CSC
@@ -1762,6 +1795,19 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
   __syncthreads();
   if (threadIdx.x == 0)
     s.balive[blockIdx.x] = alive_cnt;
+#if LMM_UPD_XL
+  if (kRdq) {  // the workgroup's ready candidates for the next round, appended to list b % 8 (this round's parity)
+    const int n = ucnt_sh;
+    const int x = int(blockIdx.x % kUXL);
+    __shared__ int ubase;
+    if (threadIdx.x == 0)
+      ubase = n ? atomicAdd(&s.ctl[CTL_UX0 + kUXL * (round & 1) + x], n) : 0;
+    __syncthreads();
+    const int64_t base = int64_t(x) * (int64_t(gridDim.x + kUXL - 1) / kUXL) * kUSeg + ubase;
+    for (int i = threadIdx.x; i < n; i += kBlock)
+      s.useg[base + i] = ulist[i];
+  }
+#else
   if (kRdq) {  // the workgroup's ready candidates for the next round into its segment
     const int n = ucnt_sh;
     for (int i = threadIdx.x; i < n; i += kBlock)
@@ -1769,6 +1815,7 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
     if (threadIdx.x == 0)
       s.ucnt[blockIdx.x] = n;
   }
+#endif
   if (__syncthreads_or(any_touch) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
 #if LMM_ANAT
