@@ -23,6 +23,9 @@ for v in base new; do
   lib=abl/$v/liblmm_amd.so; [ $v = new ] && lib=simgrid_amd/_lib/liblmm_amd.so
   step ab_c2s_$v 200 env LMM_AMD_LIB=$lib python bench.py --variant stress --steps 10 --warmup 2 --no-cpu-baseline --dropin-steps 0
 done
+# knobs on the new build: the stamps' vote below 5e5 alive rows; 6 saturation workgroups per CU
+step ab_c2_vbr 200 env LMMHIP_VOTE_BITS_ROWS=500000 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dropin-steps 0
+step ab_c2_sb6 200 env LMMHIP_SAT_BLOCKS=1536 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dropin-steps 0
 step prof_c2b 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --dropin-steps 0 --profile-json gpurun_out/r06_prof_c2b.json
 step anat_c2b 200 env LMM_AMD_LIB=simgrid_amd/_anat/liblmm_amd.so python scripts/anatomy.py --rounds 70,71,200,201 \
   --product-profile gpurun_out/r06_prof_c2b.json --out gpurun_out/r06_c2_round_anatomy_b.json --raw gpurun_out/r06_anat_c2b.npz

@@ -98,6 +98,7 @@ struct lmmhip_ctx {
   int sat_waves = 1;  // waves per ready constraint in mm_saturate (mean 64-element CSC chunks, 1/2/4)
   bool vote_diag = std::getenv("LMMHIP_VOTE_DIAG") != nullptr;  // profiling: diagnostic vote launches
   bool vote_bits = true;  // short-row vote: changed-constraint bitmap in LDS (LMMHIP_VOTE_BITS=0: the stamps' path)
+  int64_t vote_bits_rows = 0;  // ... only while the alive rows (host view) are at least this many
   unsigned* pbar = nullptr;
   bool persist_prof = false;    // record barrier timestamps in the persistent launch
   long long* ptime = nullptr;   // [2 * kPersistProfCap] last arrival / exit per barrier
@@ -1415,7 +1416,9 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
   switch (G) {
   case 4:
   case 8:  // short rows: one lane per row (more gathers in flight per wave)
-    if (int64_t(d.nC) <= int64_t(kBitWords) * 64 && c->vote_bits) {
+    // the LDS bitmap of changed constraints (one 1024-thread workgroup per CU); below LMMHIP_VOTE_BITS_ROWS alive rows
+    // (host view, A/B knob; 0 = always) the change stamps gathered per row instead: no ~125-KB copy per CU
+    if (int64_t(d.nC) <= int64_t(kBitWords) * 64 && c->vote_bits && nrows >= c->vote_bits_rows) {
       if (c->profiling && c->vote_diag) {  // measurement: bitmap load alone, filter alone (slot 7)
         LAUNCH(7, r + 1000000, (mm_vote_lane<kVBlock, true, 2>), c->n_cu, kVBlock, d, int(r));
         LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
@@ -1501,6 +1504,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     d.ucnt = uc;
   }
   c->vote_bits = env_int("LMMHIP_VOTE_BITS", 1) != 0;
+  c->vote_bits_rows = env_int("LMMHIP_VOTE_BITS_ROWS", 0);
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   const int gC = grid_for(d.nC, kBlock);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
