@@ -38,10 +38,7 @@ enum : int {
   // fair bottleneck: the reference's work summed over the rounds, three uint64 words:
   // elements of the listed constraints, listed variables, listed constraints (words 24..29)
   CTL_FBW = 24,
-  // multi-launch maxmin (LMM_UPD_XL): the update's ready candidates in 8 lists (workgroup b -> list b % 8, one
-  // returning add per workgroup), their lengths per round parity (2 x 8 words)
-  CTL_UX0 = 32,
-  CTL_WORDS = 48
+  CTL_WORDS = 32
 };
 
 // maxmin per-constraint state, one 64-B line per constraint (array-of-structs): a constraint touched

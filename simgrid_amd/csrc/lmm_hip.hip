@@ -1492,7 +1492,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     int32_t *q0 = nullptr, *q1 = nullptr, *st = nullptr, *sg = nullptr, *uc = nullptr;
     const int64_t n = std::max<int64_t>(d.nC, 1);
     if (int rc = scratch(c, c->mm_rdq[0], n, &q0) | scratch(c, c->mm_rdq[1], n, &q1) |
-                 scratch(c, c->mm_rqst, n, &st) | scratch(c, c->mm_useg, (gU_rdq + kUXL - 1) / kUXL * kUXL * kUSeg, &sg) |
+                 scratch(c, c->mm_rqst, n, &st) | scratch(c, c->mm_useg, gU_rdq * kUSeg, &sg) |
                  scratch(c, c->mm_ucnt, kMaxBlocks, &uc))
       return rc;
     HIPCHK(hipMemsetAsync(st, 0xFF, size_t(n) * sizeof(int32_t), c->stream));

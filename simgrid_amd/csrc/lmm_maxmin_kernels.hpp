@@ -173,34 +173,48 @@ __global__ void __launch_bounds__(kBlock) mm_init_vars(Dev s) {
 // ready (rdq, one entry per constraint and round through the rqst stamps, which the update sets too).
 // mm_saturate_q re-checks every entry after the vote (alive, nothing voting elsewhere).
 constexpr int kUSeg = 1024;  // update candidates per workgroup segment (>= the constraints a workgroup updates)
-// LMM_UPD_XL (build knob): the update's workgroups append their ready candidates to 8 lists (workgroup b -> list
-// b % 8, i.e. its XCD under the round-robin placement: the adds on one length word come from one XCD; speed only)
-// instead of writing a segment each, so the saturation reads 8 lengths instead of building the prefix of ~1,024
-// segment counts in every workgroup (round 6 anatomy: 1.4-2.8 us at the start of every saturation launch).
-#ifndef LMM_UPD_XL
-#define LMM_UPD_XL 1
-#endif
-constexpr int kUXL = 8;
+// (Round 6 measured the update's candidates appended to 8 lists — one returning add per workgroup on the list of its
+// XCD — so that the saturation reads 8 lengths instead of a prefix of ~1,024 segment counts: the saturation gained
+// ~4 us per round, the update lost 7-8 us to the adds at its end; C2 24.31 ms against 23.62, removed.)
 __device__ __forceinline__ void rdq_push(const Dev& s, int32_t c, int qround) {
   if (atomicExch(&s.rqst[c], qround) != qround) {
     const int q = qround & 1;
     s.rdq[q][atomicAdd(&s.ctl[CTL_RDQ0 + q], 1)] = c;
   }
 }
-// The same for a whole wave (every lane calls it; c < 0: nothing to queue): one returning atomic on the queue's
-// counter per wave instead of one per queued constraint.  Round 6 anatomy (profiles/r06_c2_round_anatomy.json): in
-// the tail, when the re-votes make many constraints ready at once, the per-lane adds on the one counter were the
-// vote's longest level (11 of 27 us in round 200's slowest wave).  The queue's order does not matter: the saturation
-// of one round's ready constraints commutes (no shared alive variable, fixed-point integer decrements).
-#ifndef LMM_RDQ_WAVE
-#define LMM_RDQ_WAVE 1  // (build knob, measurement: 0 = one queue-counter add per queued constraint, as in round 5)
-#endif
-__device__ __forceinline__ void rdq_push_wave(const Dev& s, int32_t c, int qround) {
-  const bool first = c >= 0 && atomicExch(&s.rqst[c], qround) != qround;
+// The vote's queue through the workgroup (round 6): a constraint a re-vote made ready goes to an LDS list, and the
+// workgroup reserves its range of the global queue with ONE add at its end (rdq_flush_lds).  The round anatomy
+// (profiles/r06_c2_round_anatomy.json) found the queue's one counter word the longest wait of the tail's votes: per
+// lane (round 5), then per wave, every queued constraint or wave was a returning add on that one word, ~10-13 ns
+// each at the memory side, queued behind each other (11-17 us of a 27-us vote in round 200).  Past kRqCap
+// entries a workgroup queues directly (the old path).  The queue's order does not matter: the saturation of one
+// round's ready constraints commutes (no shared alive variable, fixed-point integer decrements).
+constexpr int kRqCap = 2048;
+struct RdqLds {
+  int n, base;
+  int32_t buf[kRqCap];
+};
+__device__ __forceinline__ void rdq_push_lds(const Dev& s, int32_t c, int qround, RdqLds* L) {
+  if (c >= 0 && atomicExch(&s.rqst[c], qround) != qround) {
+    const int pos = atomicAdd(&L->n, 1);  // (LDS)
+    if (pos < kRqCap) {
+      L->buf[pos] = c;
+    } else {
+      const int q = qround & 1;
+      s.rdq[q][atomicAdd(&s.ctl[CTL_RDQ0 + q], 1)] = c;
+    }
+  }
+}
+// (every thread of the workgroup, after its last push)
+__device__ __forceinline__ void rdq_flush_lds(const Dev& s, int qround, RdqLds* L) {
+  __syncthreads();
+  const int n = L->n < kRqCap ? L->n : kRqCap;
   const int q = qround & 1;
-  const int pos = wave_append(first, &s.ctl[CTL_RDQ0 + q]);
-  if (first)
-    s.rdq[q][pos] = c;
+  if (threadIdx.x == 0)
+    L->base = n ? atomicAdd(&s.ctl[CTL_RDQ0 + q], n) : 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    s.rdq[q][L->base + i] = L->buf[i];
 }
 
 __device__ __forceinline__ unsigned row_floor(unsigned sk, unsigned mk, double vb, double p) {
@@ -490,7 +504,7 @@ constexpr int kFilt = LMM_KFILT;  // rows per lane per filter step (their loads 
   } while (0)
 #endif
 // kRdq: a constraint this re-vote made ready (nothing votes elsewhere any more) is returned in *rdq_c for the
-// caller's wave-wide queueing (rdq_push_wave), or queued here when rdq_c is null.
+// caller's workgroup-wide queueing (rdq_push_lds), or queued here when rdq_c is null.
 template <int R, bool kRec = false, bool kRdq = false>
 __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64_t row, int* st_rows,
                                          int* st_elems, const uint16_t* __restrict__ key, int* rdq_c = nullptr
@@ -693,7 +707,7 @@ template <bool kBits, int R, int F, int kDiag, bool kRec = false, bool kRdq = fa
 __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int64_t lo, int64_t hi,
                                           const uint64_t* bits, int* qw, int* st_rows, int* st_elems,
                                           const uint16_t* __restrict__ key, const int* tt0 = nullptr,
-                                          const unsigned* sk0 = nullptr VW_ANAT_PARAMS) {
+                                          const unsigned* sk0 = nullptr, RdqLds* rql = nullptr VW_ANAT_PARAMS) {
   const int lane = threadIdx.x & (kWave - 1);
   int64_t wlo, whi;
   vote_wave_range(lo, hi, wlo, whi);
@@ -797,16 +811,16 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
           wcnt[1]++;
         }
         if (kDiag == 0)
-          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr, an, ar);
+          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, &pc, an, ar);
         if (kRdq && kDiag == 0)
-          rdq_push_wave(s, pc, round);
+          rdq_push_lds(s, pc, round, rql);
         if (an)
           ANAT_LVL(*aa, 8, 0u);
 #else
         if (kDiag == 0)
-          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr);
+          vote_row<R, kRec, kRdq>(s, buf, round, row, st_rows, st_elems, key, &pc);
         if (kRdq && kDiag == 0)
-          rdq_push_wave(s, pc, round);
+          rdq_push_lds(s, pc, round, rql);
 #endif
       }
     }
@@ -819,19 +833,18 @@ __device__ __forceinline__ int vote_waves(const Dev& s, int buf, int round, int6
   }
   int pc = -1;
   if (kDiag == 0 && lane < qn)
-    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr, an, ar);
+    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, &pc, an, ar);
   __builtin_amdgcn_wave_barrier();
-  if (kRdq && kDiag == 0 && qn > 0)
-    rdq_push_wave(s, pc, round);
+  if (kRdq && kDiag == 0)
+    rdq_push_lds(s, pc, round, rql);
   if (an && qn > 0)
     ANAT_LVL(*aa, 8, 0u);
 #else
   int pc = -1;
   if (kDiag == 0 && lane < qn)
-    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, LMM_RDQ_WAVE ? &pc : nullptr);
-  __builtin_amdgcn_wave_barrier();
-  if (kRdq && kDiag == 0 && qn > 0)  // (wave-uniform)
-    rdq_push_wave(s, pc, round);
+    vote_row<R, kRec, kRdq>(s, buf, round, qw[lane], st_rows, st_elems, key, &pc);
+  if (kRdq && kDiag == 0)
+    rdq_push_lds(s, pc, round, rql);
 #endif
   if (kDiag == 1 && s.vstat && round < kStatRounds) {
     int32_t* d = s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot);
@@ -930,8 +943,11 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   __shared__ int st_rows, st_elems;
   __shared__ int q[(B / kWave) * kQW];  // per-wave queues of rows to re-vote
   __shared__ __attribute__((aligned(16))) uint64_t bits[kBits ? kBitWords : 2];
-  if (threadIdx.x == 0)
+  __shared__ RdqLds rql;  // (kRdq) the constraints this workgroup's re-votes made ready
+  if (threadIdx.x == 0) {
     st_rows = st_elems = 0;
+    rql.n = 0;
+  }
   const int64_t nrows = s.ctl[CTL_NROWS + buf];
   const int64_t per = ((nrows + gridDim.x - 1) / gridDim.x + kWave - 1) / kWave * kWave;  // rows per workgroup
   const int64_t lo = int64_t(blockIdx.x) * per;
@@ -971,7 +987,9 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (lo < hi)
     nq = vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits,
                                                               q + (threadIdx.x / kWave) * kQW, &st_rows, &st_elems,
-                                                              s.key, tt0, sk0, an, &aa, &ar, wcnt);
+                                                              s.key, tt0, sk0, &rql, an, &aa, &ar, wcnt);
+  if (kRdq && kDiag == 0)
+    rdq_flush_lds(s, round, &rql);
   if (an) {  // the wave's record (vote_row's levels: the slowest lane of the wave)
     const unsigned long long t_out = anat_now();
     unsigned lv[6];
@@ -1000,7 +1018,9 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
 #else
   if (lo < hi)
     vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
-                                                         &st_rows, &st_elems, s.key, tt0, sk0);
+                                                         &st_rows, &st_elems, s.key, tt0, sk0, &rql);
+  if (kRdq && kDiag == 0)
+    rdq_flush_lds(s, round, &rql);
 #endif
   if (s.vstat && kDiag == 0) {
     __syncthreads();
@@ -1418,22 +1438,6 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     s.ctl[CTL_RDQ0 + ((round + 1) & 1)] = 0;
   __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (saturate_chunk)
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-#if LMM_UPD_XL
-  // the previous round's update wrote parity (round - 1) & 1; this round's update will add to parity round & 1, whose
-  // lengths the previous saturation read: reset here (block 0), before that update starts
-  if (blockIdx.x == 0 && threadIdx.x < kUXL)
-    s.ctl[CTL_UX0 + kUXL * (round & 1) + threadIdx.x] = 0;
-  int xpre[kUXL + 1];  // prefix of the 8 list lengths (wave-uniform, registers)
-  xpre[0] = 0;
-#pragma unroll
-  for (int x = 0; x < kUXL; x++)
-    xpre[x + 1] = xpre[x] + s.ctl[CTL_UX0 + kUXL * ((round - 1) & 1) + x];
-  const int total = xpre[kUXL];
-  const int64_t xcap = int64_t(ublocks + kUXL - 1) / kUXL * kUSeg;
-#if LMM_ANAT
-  const unsigned long long t_pre = an ? anat_now() : 0;
-#endif
-#else
   __shared__ int pre[kMaxBlocks + 1];
   __shared__ int wsum[kBlock / kWave];
   constexpr int kPer = kMaxBlocks / kBlock;
@@ -1470,7 +1474,6 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
 #if LMM_ANAT
   const unsigned long long t_pre = an ? anat_now() : 0;
 #endif
-#endif
   const int nq = s.ctl[CTL_RDQ0 + (round & 1)];
   const int32_t* __restrict__ q = s.rdq[round & 1];
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
@@ -1480,20 +1483,12 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     const int64_t i = g / K;
     if (i >= total)
       return q[i - total];
-#if LMM_UPD_XL
-    int x = 0;  // the list holding candidate i
-#pragma unroll
-    for (int y = 1; y < kUXL; y++)
-      x += i >= xpre[y];
-    return s.useg[int64_t(x) * xcap + (i - xpre[x])];
-#else
     int lo = 0;  // last segment with pre[seg] <= i
 #pragma unroll
     for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
       if (lo + step < ublocks && pre[lo + step] <= i)
         lo += step;
     return s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
-#endif
   };
 #if LMM_SATQ_PIPE
   // Software-pipelined over the wave's tasks (round 6): the next task's candidate state (key, vote count, ratio, CSC
@@ -1795,19 +1790,6 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
   __syncthreads();
   if (threadIdx.x == 0)
     s.balive[blockIdx.x] = alive_cnt;
-#if LMM_UPD_XL
-  if (kRdq) {  // the workgroup's ready candidates for the next round, appended to list b % 8 (this round's parity)
-    const int n = ucnt_sh;
-    const int x = int(blockIdx.x % kUXL);
-    __shared__ int ubase;
-    if (threadIdx.x == 0)
-      ubase = n ? atomicAdd(&s.ctl[CTL_UX0 + kUXL * (round & 1) + x], n) : 0;
-    __syncthreads();
-    const int64_t base = int64_t(x) * (int64_t(gridDim.x + kUXL - 1) / kUXL) * kUSeg + ubase;
-    for (int i = threadIdx.x; i < n; i += kBlock)
-      s.useg[base + i] = ulist[i];
-  }
-#else
   if (kRdq) {  // the workgroup's ready candidates for the next round into its segment
     const int n = ucnt_sh;
     for (int i = threadIdx.x; i < n; i += kBlock)
@@ -1815,7 +1797,6 @@ template <bool kRdq = false> __global__ void __launch_bounds__(kBlock) mm_update
     if (threadIdx.x == 0)
       s.ucnt[blockIdx.x] = n;
   }
-#endif
   if (__syncthreads_or(any_touch) && threadIdx.x == 0)
     s.ctl[CTL_LASTR] = round;  // plain store: the last round that changed a constraint
 #if LMM_ANAT
