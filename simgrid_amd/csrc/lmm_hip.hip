@@ -1526,6 +1526,8 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // mm_saturate: waves per ready constraint and the grid's block cap (measurement knobs)
   const int sat_k = env_int("LMMHIP_SAT_WAVES", c->sat_waves);
   const int sat_max = env_int("LMMHIP_SAT_GRID_MAX", kMaxBlocks);
+  // batched saturation (mm_saturate_qb): ready tasks' first chunks M = 2 / 4 at a time (0: mm_saturate_q)
+  const int sat_batch = env_int("LMMHIP_SATQ_BATCH", 0);
   auto sat_grid = [&](int64_t n) { return int(std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, sat_max))); };
   // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
   // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
@@ -1571,7 +1573,15 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows))
         return rc;
       if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
-        if (sat_k == 1)
+        if (sat_batch == 4 && sat_k == 2)
+          LAUNCH(4, r, (mm_saturate_qb<2, 4>), capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        else if (sat_batch == 2 && sat_k == 2)
+          LAUNCH(4, r, (mm_saturate_qb<2, 2>), capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        else if (sat_batch && sat_k == 1)
+          LAUNCH(4, r, (mm_saturate_qb<1, 4>), capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
+        else if (sat_batch && sat_k == 4)
+          LAUNCH(4, r, (mm_saturate_qb<4, 4>), capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
+        else if (sat_k == 1)
           LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
         else if (sat_k == 2)
           LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
@@ -1679,6 +1689,9 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int sat_b0 = int64_t(nblkS) >= 2 * int64_t(c->n_cu) ? kFS : 256;
   const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
+  // CSC elements per saturation chunk (LMMHIP_FR_SATCW: 64, 32 or 16)
+  const int sat_cw0 = env_int("LMMHIP_FR_SATCW", 64);
+  const int sat_cw = sat_old ? 64 : sat_cw0 <= 16 ? 16 : sat_cw0 <= 32 ? 32 : 64;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
@@ -1715,10 +1728,18 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       }
       if (sat_b == 256 && sat_old)
         LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
+      else if (sat_b == 256 && sat_cw == 16)
+        LAUNCH(4, r, (fr_sat<256, false, 16>), nblk, 256, d, int(r), bigch);
+      else if (sat_b == 256 && sat_cw == 32)
+        LAUNCH(4, r, (fr_sat<256, false, 32>), nblk, 256, d, int(r), bigch);
       else if (sat_b == 256)
         LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
       else if (sat_old)
         LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r), bigch);
+      else if (sat_cw == 16)
+        LAUNCH(4, r, (fr_sat<kFS, false, 16>), nblkS, kFS, d, int(r), bigch);
+      else if (sat_cw == 32)
+        LAUNCH(4, r, (fr_sat<kFS, false, 32>), nblkS, kFS, d, int(r), bigch);
       else
         LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
       if (big)
