@@ -11,11 +11,13 @@ step() {  # name seconds cmd...
   tail -c 200 "gpurun_out/$name.out"; echo
   if [ $rc -ne 0 ]; then echo "STOP $name rc=$rc"; tail -20 "gpurun_out/$name.log"; exit $rc; fi
 }
-echo "== tests (batch 4, cw 16)"
-LMMHIP_SATQ_BATCH=4 LMMHIP_FR_SATCW=16 timeout -k 10 500 python -u -m pytest tests/test_gpu_engines.py \
-  tests/test_gpu_parity.py "tests/test_gpu_configs.py::test_c4_full_size_vs_oracle" -x -v -p no:cacheprovider \
-  --timeout 300 --timeout-method thread > gpurun_out/r06_tests_d.log 2>&1 || { tail -30 gpurun_out/r06_tests_d.log; exit 1; }
-tail -n 2 gpurun_out/r06_tests_d.log
+for lever in LMMHIP_SATQ_BATCH=4 LMMHIP_FR_SATCW=16; do
+  echo "== tests ($lever)"
+  env $lever timeout -k 10 500 python -u -m pytest tests/test_gpu_engines.py tests/test_gpu_parity.py \
+    "tests/test_gpu_configs.py::test_c4_full_size_vs_oracle" -x -v -p no:cacheprovider --timeout 300 \
+    --timeout-method thread > gpurun_out/r06_tests_d_${lever%%=*}.log 2>&1 || { tail -30 gpurun_out/r06_tests_d_${lever%%=*}.log; exit 1; }
+  tail -n 2 gpurun_out/r06_tests_d_${lever%%=*}.log
+done
 for pass in 1 2; do
   for m in 0 2 4; do
     step abd_c2_b${m}_$pass 200 env LMMHIP_SATQ_BATCH=$m python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dropin-steps 0

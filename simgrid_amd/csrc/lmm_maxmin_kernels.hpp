@@ -1685,14 +1685,18 @@ __device__ __forceinline__ void sat_rows(const Dev& s, int lane, int* pre, uint3
 // 64 variables at a time (sat_rows).  mm_saturate_q runs a
 // wave's tasks one after the other, each a chain of ~5 dependent levels: a tail round of C2 gives a wave ~5 ready tasks
 // of ~1 claimed variable each (profiles/r06_c2_round_anatomy.json).  Chunks after a task's first (constraint degree
-// above K * 64) follow one at a time (saturate_chunk).
+// above K * CW) follow one at a time (saturate_chunk).  CW = 32: chunks of 32 elements, so that a mid-solve chunk
+// with many claimed variables (the critical wave of a mid-solve round: 43 of them, 301 pushes in two passes) is
+// spread over twice the waves.
 template <int M> struct SatBuf {
   double p[M * kWave];
   uint32_t rb[M * kWave];
   int len[M * kWave];
   uint8_t t[M * kWave];
 };
-template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb(Dev s, int round, int ublocks) {
+template <int K, int M, int CW = kWave>
+__global__ void __launch_bounds__(kBlock) mm_saturate_qb(Dev s, int round, int ublocks) {
+  static_assert(CW == kWave || CW == kWave / 2, "chunk width");
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -1777,7 +1781,7 @@ template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb
       const unsigned kc = s.key[c];
       const int nv = s.nvote[c];
       r = ld_rlx(&s.cst[c].ratio);
-      cb = s.cnst_ptr[c] + uint32_t(k) * kWave;
+      cb = s.cnst_ptr[c] + uint32_t(k) * CW;
       ce = s.cnst_ptr[c + 1];
       dup = s.cdup[c] != 0;
       rdy = kc != kDeadKey && nv == 0;
@@ -1812,7 +1816,7 @@ template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb
         rbv[u] = rev[u] = 0;
         if (tl[u] >= 0) {
           const uint32_t tb = uint32_t(__shfl(int(cb), tl[u], kWave));
-          const uint32_t te = min(uint32_t(__shfl(int(ce), tl[u], kWave)), tb + kWave);
+          const uint32_t te = min(uint32_t(__shfl(int(ce), tl[u], kWave)), tb + CW);
           const uint32_t j = tb + uint32_t(lane);
           if (j < te) {
             lv[u] = s.csc_v[j];
@@ -1841,8 +1845,8 @@ template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb
         st[u] = lv[u] >= 0 ? s.vstate[lv[u]] : 1;
 #pragma unroll
       for (int u = 0; u < M; u++) {
+        const bool tdup = __shfl(int(dup), max(tl[u], 0), kWave) != 0;  // (shuffles in uniform control flow)
         if (lv[u] >= 0) {
-          const bool tdup = __shfl(int(dup), tl[u], kWave) != 0;
           if (st[u] != 0)
             lv[u] = -1;
           else if (!tdup)
@@ -1855,8 +1859,9 @@ template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb
 #pragma unroll
       for (int u = 0; u < M; u++) {
         const uint64_t bal = __ballot(lv[u] >= 0);
+        const double tr = __shfl(r, max(tl[u], 0), kWave);
         if (lv[u] >= 0) {
-          s.x[lv[u]] = __shfl(r, tl[u], kWave) / lp[u];
+          s.x[lv[u]] = tr / lp[u];
           const int pos = n + __popcll(bal & below);
           B.p[pos] = lp[u];
           B.rb[pos] = rbv[u];
@@ -1883,7 +1888,7 @@ template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb
       }
       __builtin_amdgcn_wave_barrier();
     }
-    uint64_t mx = __ballot(rdy && ce > cb + uint32_t(K) * kWave);  // tasks of more than one chunk
+    uint64_t mx = __ballot(rdy && ce > cb + uint32_t(K) * CW);  // tasks of more than one chunk
     while (mx) {  // wave-uniform
       const int t = __builtin_ctzll(mx);
       mx &= mx - 1;
@@ -1891,9 +1896,10 @@ template <int K, int M> __global__ void __launch_bounds__(kBlock) mm_saturate_qb
       const double tr = __shfl(r, t, kWave);
       const uint32_t te = uint32_t(__shfl(int(ce), t, kWave));
       const bool tdup = __shfl(int(dup), t, kWave) != 0;
-      for (uint32_t base = uint32_t(__shfl(int(cb), t, kWave)) + uint32_t(K) * kWave; base < te;
-           base += uint32_t(K) * kWave)  // wave-uniform
-        saturate_chunk(s, tc, tr, base, te, round, lane, wpre[w], tdup SC_ANAT_ARGS);
+      for (uint32_t base = uint32_t(__shfl(int(cb), t, kWave)) + uint32_t(K) * CW; base < te;
+           base += uint32_t(K) * CW)  // wave-uniform
+        saturate_chunk(s, tc, tr, base, CW == kWave ? te : min(te, base + CW), round, lane, wpre[w],
+                       tdup SC_ANAT_ARGS);
     }
   }
 #if LMM_ANAT
