@@ -589,9 +589,6 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
 }
 
 // The collected ready constraints' chunks, round-robin over the workgroup's waves (sat_flush with fr_sat_chunk).
-// A chunk is CW <= 64 CSC elements: below 64 the lanes >= CW idle in the CSC load, but the claimed rows' pushes
-// (the chunk's long pole: the critical wave of a C4 round issues ~750 of them) are spread over CW / 64 as many
-// waves of the workgroup, which are otherwise mostly idle (a C4 round saturates ~50 chunks over ~390 waves).
 #if LMM_ANAT
 #define FR_ANAT_PARAMS , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
 #define FR_ANAT_ARGS , an, aa, wc
@@ -599,9 +596,8 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
 #define FR_ANAT_PARAMS
 #define FR_ANAT_ARGS
 #endif
-template <int NB, bool kOld, int CW>
+template <int NB, bool kOld>
 __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L FR_ANAT_PARAMS) {
-  static_assert(CW == kWave || (!kOld && CW >= 8 && CW < kWave), "chunk width");
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int ta = L.na, tb = L.nb;
@@ -617,11 +613,9 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
     if (kOld)  // (measurement: the multi-launch engine's chunk body)
       saturate_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
                      s.cdup[cc] != 0);
-    else {
-      const uint32_t j0 = s.cnst_ptr[cc] + uint32_t(ch) * CW, ce = s.cnst_ptr[cc + 1];
-      fr_sat_chunk(s, cc, r, j0, CW == kWave ? ce : min(ce, j0 + CW), round, lane, L.pre[w],
+    else
+      fr_sat_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
                    s.cdup[cc] != 0 FR_ANAT_ARGS);
-    }
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -632,7 +626,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 // (fr_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
 constexpr int kFS = 1024;
 
-template <int NB, bool kOld, int CW>
+template <int NB, bool kOld>
 __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L
                                            FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
@@ -642,11 +636,10 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   int nch = 0;
   if (c < s.nC && s.key32[c] != kDead32 && s.nvote[c] == 0) {
     rdy = true;
-    const uint32_t deg = s.cnst_ptr[c + 1] - s.cnst_ptr[c];
-    nch = int((deg + CW - 1) / CW);
+    nch = int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave);
     if (s.vstat)
       atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 5, 1);
-    if (int((deg + kWave - 1) / kWave) > bigch) {  // rare (fat-tree core links): spread over the grid by fr_sat_big
+    if (nch > bigch) {  // rare (fat-tree core links): spread over the grid by fr_sat_big
       s.ready[atomicAdd(&s.ctl[CTL_NREADY], 1)] = int32_t(c);
       rdy = false;
       nch = 0;
@@ -692,11 +685,10 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   }
 #endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld, CW>(s, round, L FR_ANAT_ARGS);
+    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
 }
 
-template <int kFS, bool kOld = false, int CW = kWave>
-__global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -709,7 +701,7 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
     return;
   __shared__ SatLds<kFS, kFS> L;
 #if LMM_ANAT
-  fr_sat_blk<kFS, kOld, CW>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -720,7 +712,7 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
       arec[10 + i] = wc[i];
   }
 #else
-  fr_sat_blk<kFS, kOld, CW>(s, round, bigch, blockIdx.x, L);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
 #endif
 }
 

@@ -1692,9 +1692,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int sat_b0 = int64_t(nblkS) >= 2 * int64_t(c->n_cu) ? kFS : 256;
   const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
-  // CSC elements per saturation chunk (LMMHIP_FR_SATCW: 64, 32 or 16)
-  const int sat_cw0 = env_int("LMMHIP_FR_SATCW", 64);
-  const int sat_cw = sat_old ? 64 : sat_cw0 <= 16 ? 16 : sat_cw0 <= 32 ? 32 : 64;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
@@ -1731,18 +1728,10 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       }
       if (sat_b == 256 && sat_old)
         LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
-      else if (sat_b == 256 && sat_cw == 16)
-        LAUNCH(4, r, (fr_sat<256, false, 16>), nblk, 256, d, int(r), bigch);
-      else if (sat_b == 256 && sat_cw == 32)
-        LAUNCH(4, r, (fr_sat<256, false, 32>), nblk, 256, d, int(r), bigch);
       else if (sat_b == 256)
         LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
       else if (sat_old)
         LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r), bigch);
-      else if (sat_cw == 16)
-        LAUNCH(4, r, (fr_sat<kFS, false, 16>), nblkS, kFS, d, int(r), bigch);
-      else if (sat_cw == 32)
-        LAUNCH(4, r, (fr_sat<kFS, false, 32>), nblkS, kFS, d, int(r), bigch);
       else
         LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
       if (big)
