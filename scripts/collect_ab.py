@@ -1,30 +1,53 @@
-"""Collect the same-box A/B lines of round-5 GPU scripts (gpurun_out/<prefix>_<tag>.json: bench.py JSON lines) into
-one profile summary: python scripts/collect_ab.py <out.json> <prefix> [<prefix> ...]"""
+"""Collect the round-6 same-box A/B bench lines (gpurun_out/ab*_*.out, one bench.py JSON line each) into
+profiles/r06_ab.json: per GPU pass (B, C, D, E: one box each) the variant's ms per solve and the launch-average of
+its dominant kernel, with what each variant was (scripts/gpu_r06_[b-e].sh)."""
 import glob
 import json
 import os
+import re
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PASSES = {
+    "ab_": ("B", "scripts/gpu_r06_b.sh", {
+        "base": "round-6 pruned build before the levers", "rdq": "+ wave-level vote ready queue",
+        "pipe": "+ saturation tasks pipelined (LMM_SATQ_PIPE)", "new": "+ per-XCD update candidate lists",
+        "sb6": "saturation grid 6 workgroups per CU", "vbr": "vote bitmap off in the tail (LMMHIP_VOTE_BITS_ROWS)"}),
+    "abc_": ("C", "scripts/gpu_r06_c.sh", {
+        "base": "round-5 code (abl/base)", "pipe": "+ pipelined saturation + wave-level vote queue",
+        "new": "+ workgroup-level vote queue (RdqLds) = product"}),
+    "abd_": ("D", "scripts/gpu_r06_d.sh", {
+        "b0": "mm_saturate_q (product)", "b2": "batched saturation M = 2", "b4": "batched saturation M = 4",
+        "w64": "frontier saturation 64-element chunks (product)", "w32": "32-element chunks", "w16": "16-element chunks"}),
+    "abe_": ("E", "scripts/gpu_r06_e.sh", {
+        "q": "mm_saturate_q (product)", "b64": "batched saturation M = 4", "b32": "batched, 32-element chunks"}),
+}
 
-def main():
-    out, prefixes = sys.argv[1], sys.argv[2:]
+
+def main(out=os.path.join(ROOT, "profiles", "r06_ab.json")):
     res = {}
-    for pre in prefixes:
-        for p in sorted(glob.glob(os.path.join("gpurun_out", f"{pre}_*.json"))):
+    for pre, (name, script, what) in PASSES.items():
+        rows = {}
+        for p in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", pre + "*.out"))):
+            m = re.match(re.escape(pre) + r"(c2s|c2|c4)_([a-z0-9]+?)(?:_(\d))?\.out$", os.path.basename(p))
+            if not m:
+                continue
             try:
                 d = json.loads(open(p).read().strip().splitlines()[-1])
-            except (OSError, ValueError, IndexError):
+            except (ValueError, IndexError):
                 continue
-            row = {"ms_per_step": d.get("ms_per_step"), "workload": d.get("config", {}).get("workload")}
-            drop = d.get("config", {}).get("dropin_step")
-            if drop:
-                row["dropin_step"] = drop
-            res[os.path.basename(p)[:-5]] = row
-    with open(out, "w") as f:
-        json.dump(res, f, indent=1)
-    for k, v in res.items():
-        print(k, v["ms_per_step"], (v.get("dropin_step") or {}).get("solve_step_ms", ""))
+            wl, var = m.group(1), m.group(2)
+            dk = d.get("roofline", {}).get("dominant_kernel") or {}
+            rows.setdefault(wl, {}).setdefault(var, {"what": what.get(var, var), "ms_per_step": []})
+            rows[wl][var]["ms_per_step"].append(d["ms_per_step"])
+            if dk:
+                rows[wl][var].setdefault("dominant_kernel_avg_us", []).append(dk.get("avg_us"))
+        if rows:
+            res[name] = {"script": script, "workloads": rows}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: {w: {v: x["ms_per_step"] for v, x in r.items()} for w, r in p["workloads"].items()}
+                      for k, p in res.items()}))
 
 
 if __name__ == "__main__":
-    main()
+    main(*sys.argv[1:])
