@@ -1526,9 +1526,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // mm_saturate: waves per ready constraint and the grid's block cap (measurement knobs)
   const int sat_k = env_int("LMMHIP_SAT_WAVES", c->sat_waves);
   const int sat_max = env_int("LMMHIP_SAT_GRID_MAX", kMaxBlocks);
-  // batched saturation (mm_saturate_qb): ready tasks' first chunks M = 2 / 4 at a time (0: mm_saturate_q)
-  const int sat_batch = env_int("LMMHIP_SATQ_BATCH", 0);
-  const int sat_cw = env_int("LMMHIP_SATQ_CW", 64);  // (with the batch: 32-element chunks, twice the waves)
   auto sat_grid = [&](int64_t n) { return int(std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, sat_max))); };
   // Compaction cadence (knobs): alive rows are re-counted every cmp_every rounds and rewritten when
   // fewer than cmp_pct % of the scanned rows are alive; the alive-constraint list every cl_every rounds.
@@ -1574,17 +1571,7 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       if (int rc = launch_vote(c, r, nrows))
         return rc;
       if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
-        if (sat_batch == 4 && sat_k == 2 && sat_cw == 32)
-          LAUNCH(4, r, (mm_saturate_qb<4, 4, 32>), capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_batch == 4 && sat_k == 2)
-          LAUNCH(4, r, (mm_saturate_qb<2, 4>), capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_batch == 2 && sat_k == 2)
-          LAUNCH(4, r, (mm_saturate_qb<2, 2>), capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_batch && sat_k == 1)
-          LAUNCH(4, r, (mm_saturate_qb<1, 4>), capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_batch && sat_k == 4)
-          LAUNCH(4, r, (mm_saturate_qb<4, 4>), capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_k == 1)
+        if (sat_k == 1)
           LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
         else if (sat_k == 2)
           LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);

@@ -1419,7 +1419,9 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 // Block 0 empties the other parity's vote queue, which the next round's vote fills.
 // A candidate's ratio, CSC range and duplicate flag are loaded with its key and vote count (round 5, same box, two
 // passes, profiles/r05_ab_c2_spec2.json: C2 24.285-24.293 ms against 24.309-24.340 without).  LMM_SATQ_PIPE (build
-// knob): the next task's candidate state loaded ahead (round 6).
+// knob): the next task's candidate state loaded ahead (round 6).  Also measured in round 6 and removed: a batched form
+// (a wave's 64 tasks' states in one load, the ready tasks' first chunks 2 / 4 at a time, the claimed variables gathered
+// in LDS and pushed 64 at a time; with 64- or 32-element chunks): 23.54-23.68 ms against 23.53 on the same box.
 #ifndef LMM_SATQ_PIPE
 #define LMM_SATQ_PIPE 1
 #endif
@@ -1568,340 +1570,6 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     saturate_one_pre<K>(s, c, k, round, lane, wpre[w], r, cb, cend, dup SC_ANAT_ARGS);
   }
 #endif
-#if LMM_ANAT
-  if (an && lane == 0) {
-    arec[0] = t_in;
-    arec[1] = anat_now();
-    arec[2] = blockIdx.x;
-    arec[3] = t_pre;
-    for (int f = 0; f < 7; f++)
-      arec[4 + f] = aa->lv[f];
-    for (int f = 0; f < 4; f++)
-      arec[11 + f] = wc[f];
-  }
-#endif
-}
-
-// The claimed variables' rows pushed (saturate_chunk's second half) for up to 64 variables gathered from several
-// chunks: per lane the row (rb, len), the variable's value and penalty, and the constraint that claimed it (cown: its
-// own element of the row gets no decrement); len = 0 on the lanes without a variable.
-__device__ __forceinline__ void sat_rows(const Dev& s, int lane, int* pre, uint32_t rb, int len, double lx, double lp,
-                                         int32_t cown SC_ANAT_PARAMS) {
-  const int q = lane & 3;
-  int incl = len;  // inclusive wave scan of the row lengths
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int t = __shfl_up(incl, o, kWave);
-    if (lane >= o)
-      incl += t;
-  }
-  const int total = __shfl(incl, kWave - 1, kWave);
-  pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
-  __builtin_amdgcn_wave_barrier();
-  for (int f0 = 0; f0 < total; f0 += kSatU * kWave) {  // wave-uniform
-    int32_t cc[kSatU];
-    int ol[kSatU];
-    double ww[kSatU];
-#pragma unroll
-    for (int u = 0; u < kSatU; u++) {  // owner lanes and element indices, then independent gathers
-      const int f = f0 + u * kWave + lane;
-      int o = 0;  // owner lane: last lane with pre <= f
-#pragma unroll
-      for (int step = kWave / 2; step > 0; step >>= 1)
-        if (pre[o + step] <= f)
-          o += step;
-      ol[u] = o;
-      const uint32_t k = uint32_t(__shfl(int(rb), o, kWave)) + uint32_t(f - pre[o]);
-      cc[u] = f < total ? s.csr_c[k] : -1;
-      ww[u] = f < total ? s.csr_w[k] : 0.0;
-    }
-#if LMM_ANAT
-    if (an) {
-      double sw = 0.0;
-#pragma unroll
-      for (int u = 0; u < kSatU; u++)
-        sw += ww[u] + double(cc[u]);
-      ANAT_LVL(*aa, 3, sw);
-    }
-#endif
-    long long a0[kSatU], a1[kSatU];  // fixed-point decrements (CstRec)
-    bool fat[kSatU];
-#pragma unroll
-    for (int u = 0; u < kSatU; u++) {
-      const double ox = __shfl(lx, ol[u], kWave);
-      const double op = __shfl(lp, ol[u], kWave);
-      const int32_t oc = __shfl(cown, ol[u], kWave);
-      fat[u] = false;
-      a0[u] = a1[u] = 0;
-      const int32_t ce = cc[u] >= 0 ? s.cexp[cc[u]] : kCexpDead;
-      if (cc[u] >= 0 && (cc[u] == oc || (ce & kCexpDead)))
-        cc[u] = -1;
-      if (cc[u] >= 0) {
-        s.ctouch[cc[u]] = 1;
-        fat[u] = ce & kCexpFat;
-        const double w = ww[u];
-        a0[u] = (long long)dec_q(w * ox, cexp_rem(ce));
-        a1[u] = fat[u] ? (long long)fat_bits(w / op) : (long long)dec_q(w / op, cexp_use(ce));
-      }
-    }
-#if LMM_ANAT
-    if (an) {
-      long long sa = 0;
-#pragma unroll
-      for (int u = 0; u < kSatU; u++) {
-        sa += a0[u] + a1[u];
-        wc[3] += unsigned(__popcll(__ballot(cc[u] >= 0)));
-      }
-      ANAT_LVL(*aa, 4, sa);
-    }
-#endif
-#pragma unroll
-    for (int u = 0; u < kSatU; u++) {
-      const int nel = total - f0 - u * kWave;
-#pragma unroll
-      for (int t = 0; t < kWave / 16; t++) {
-        if (t * 16 >= nel)
-          break;
-        const int e = t * 16 + (lane >> 2);
-        const int ec = __shfl(cc[u], e, kWave);
-        const int ef = __shfl(int(fat[u]), e, kWave);
-        const long long e0 = __shfl(a0[u], e, kWave);
-        const long long e1 = __shfl(a1[u], e, kWave);
-        if (ec >= 0 && q < 3 && (!ef || q == 2))
-          atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
-        if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
-          atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
-      }
-    }
-    SC_LVL(5, 0u);
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Batched saturation (round 6, LMMHIP_SATQ_BATCH = M): a wave takes its tasks 64 at a time — lane i the candidate of
-// task wave + i * nwaves, whose id and state are two loads for all 64 — then the ready tasks' first chunks M at a time:
-// the M chunks' CSC elements, then their variables' states, one dependent level each; the claimed variables are
-// gathered in the wave's LDS buffer (the row, the penalty and the task's lane, 17 bytes each) and their rows pushed
-// 64 variables at a time (sat_rows).  mm_saturate_q runs a
-// wave's tasks one after the other, each a chain of ~5 dependent levels: a tail round of C2 gives a wave ~5 ready tasks
-// of ~1 claimed variable each (profiles/r06_c2_round_anatomy.json).  Chunks after a task's first (constraint degree
-// above K * CW) follow one at a time (saturate_chunk).  CW = 32: chunks of 32 elements, so that a mid-solve chunk
-// with many claimed variables (the critical wave of a mid-solve round: 43 of them, 301 pushes in two passes) is
-// spread over twice the waves.
-template <int M> struct SatBuf {
-  double p[M * kWave];
-  uint32_t rb[M * kWave];
-  int len[M * kWave];
-  uint8_t t[M * kWave];
-};
-template <int K, int M, int CW = kWave>
-__global__ void __launch_bounds__(kBlock) mm_saturate_qb(Dev s, int round, int ublocks) {
-  static_assert(CW == kWave || CW == kWave / 2, "chunk width");
-#if LMM_ANAT
-  unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
-  const bool an = arec != nullptr;
-  AnatAcc aa_s{};
-  AnatAcc* aa = &aa_s;
-  unsigned wc[4] = {0, 0, 0, 0};  // candidates, chunks, fixed variables, pushed elements
-  const unsigned long long t_in = an ? anat_now() : 0;
-#endif
-  if (s.ctl[CTL_DONE])
-    return;
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    s.ctl[CTL_RDQ0 + ((round + 1) & 1)] = 0;
-  __shared__ int wpre[kBlock / kWave][kWave];  // per-wave row-length prefix (sat_rows, saturate_chunk)
-  __shared__ SatBuf<M> sbuf[kBlock / kWave];   // per-wave claimed variables (sat_rows)
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  __shared__ int pre[kMaxBlocks + 1];
-  __shared__ int wsum[kBlock / kWave];
-  constexpr int kPer = kMaxBlocks / kBlock;
-  int loc[kPer];
-  int sum = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const int seg = threadIdx.x * kPer + k;
-    loc[k] = seg < ublocks ? s.ucnt[seg] : 0;
-    sum += loc[k];
-  }
-  int incl = sum;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int t = __shfl_up(incl, o, kWave);
-    if (lane >= o)
-      incl += t;
-  }
-  if (lane == kWave - 1)
-    wsum[w] = incl;
-  __syncthreads();
-  int acc = incl - sum, total = 0;
-#pragma unroll
-  for (int i = 0; i < kBlock / kWave; i++) {
-    acc += i < w ? wsum[i] : 0;
-    total += wsum[i];
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    pre[threadIdx.x * kPer + k] = acc;
-    acc += loc[k];
-  }
-  __syncthreads();
-#if LMM_ANAT
-  const unsigned long long t_pre = an ? anat_now() : 0;
-  aa->at = t_pre;
-#endif
-  const int nq = s.ctl[CTL_RDQ0 + (round & 1)];
-  const int32_t* __restrict__ q = s.rdq[round & 1];
-  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  const int64_t T = (int64_t(total) + nq) * K;  // tasks: (candidate, wave k of its K)
-  SatBuf<M>& B = sbuf[w];
-  const uint64_t below = (1ull << lane) - 1;
-  for (int64_t g0 = wave; g0 < T; g0 += int64_t(kWave) * nwaves) {  // wave-uniform: 64 tasks at a time
-    const int64_t g = g0 + int64_t(lane) * nwaves;
-    int32_t c = -1;
-    if (g < T) {
-      const int64_t i = g / K;
-      if (i >= total) {
-        c = q[i - total];
-      } else {
-        int lo = 0;  // last segment with pre[seg] <= i
-#pragma unroll
-        for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
-          if (lo + step < ublocks && pre[lo + step] <= i)
-            lo += step;
-        c = s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
-      }
-    }
-    SC_LVL(0, c);
-    const int k = int(g % K);
-    bool rdy = false, dup = false;
-    double r = 0.0;
-    uint32_t cb = 0, ce = 0;  // this task's first chunk and the constraint's end
-    if (c >= 0) {
-      const unsigned kc = s.key[c];
-      const int nv = s.nvote[c];
-      r = ld_rlx(&s.cst[c].ratio);
-      cb = s.cnst_ptr[c] + uint32_t(k) * CW;
-      ce = s.cnst_ptr[c + 1];
-      dup = s.cdup[c] != 0;
-      rdy = kc != kDeadKey && nv == 0;
-    }
-    SC_LVL(6, r + double(cb + ce + unsigned(dup) + unsigned(rdy)));
-    const uint64_t mr = __ballot(rdy);
-    if (!mr)
-      continue;
-#if LMM_ANAT
-    if (an)
-      wc[0] += unsigned(__popcll(mr));
-#endif
-    if (lane == 0)
-      s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
-    if (rdy && k == 0)  // c leaves the light table: mm_update (the owner of key / chg) retires it
-      s.ctouch[c] = 2;
-    uint64_t m = __ballot(rdy && cb < ce);
-    while (m) {  // wave-uniform: M ready tasks' first chunks at a time
-      int tl[M];
-#pragma unroll
-      for (int u = 0; u < M; u++) {
-        tl[u] = m ? __builtin_ctzll(m) : -1;
-        m &= m - 1;
-      }
-      int32_t lv[M];
-      double lp[M];
-      uint32_t rbv[M], rev[M];
-#pragma unroll
-      for (int u = 0; u < M; u++) {
-        lv[u] = -1;
-        lp[u] = 1.0;
-        rbv[u] = rev[u] = 0;
-        if (tl[u] >= 0) {
-          const uint32_t tb = uint32_t(__shfl(int(cb), tl[u], kWave));
-          const uint32_t te = min(uint32_t(__shfl(int(ce), tl[u], kWave)), tb + CW);
-          const uint32_t j = tb + uint32_t(lane);
-          if (j < te) {
-            lv[u] = s.csc_v[j];
-            lp[u] = s.csc_p[j];
-            const unsigned long long row = s.csc_row[j];
-            rbv[u] = uint32_t(row);
-            rev[u] = uint32_t(row >> 32);
-          }
-        }
-      }
-#if LMM_ANAT
-      if (an) {
-        uint32_t sl = 0;
-#pragma unroll
-        for (int u = 0; u < M; u++)
-          sl += uint32_t(lv[u]) + rbv[u] + rev[u];
-        ANAT_LVL(*aa, 1, sl);
-#pragma unroll
-        for (int u = 0; u < M; u++)
-          wc[1] += unsigned(tl[u] >= 0);
-      }
-#endif
-      int st[M];
-#pragma unroll
-      for (int u = 0; u < M; u++)
-        st[u] = lv[u] >= 0 ? s.vstate[lv[u]] : 1;
-#pragma unroll
-      for (int u = 0; u < M; u++) {
-        const bool tdup = __shfl(int(dup), max(tl[u], 0), kWave) != 0;  // (shuffles in uniform control flow)
-        if (lv[u] >= 0) {
-          if (st[u] != 0)
-            lv[u] = -1;
-          else if (!tdup)
-            s.vstate[lv[u]] = round + 1;
-          else if (atomicCAS(&s.vstate[lv[u]], 0, round + 1) != 0)
-            lv[u] = -1;
-        }
-      }
-      int n = 0;  // variables in B
-#pragma unroll
-      for (int u = 0; u < M; u++) {
-        const uint64_t bal = __ballot(lv[u] >= 0);
-        const double tr = __shfl(r, max(tl[u], 0), kWave);
-        if (lv[u] >= 0) {
-          s.x[lv[u]] = tr / lp[u];
-          const int pos = n + __popcll(bal & below);
-          B.p[pos] = lp[u];
-          B.rb[pos] = rbv[u];
-          B.len[pos] = int(rev[u] - rbv[u]);
-          B.t[pos] = uint8_t(tl[u]);
-        }
-        n += __popcll(bal);
-      }
-#if LMM_ANAT
-      if (an) {
-        ANAT_LVL(*aa, 2, n);
-        wc[2] += unsigned(n);
-      }
-#endif
-      __builtin_amdgcn_wave_barrier();
-      for (int b0 = 0; b0 < n; b0 += kWave) {  // wave-uniform
-        const int e = b0 + lane;
-        const bool h = e < n;
-        const int t = h ? int(B.t[e]) : 0;
-        const double tp = h ? B.p[e] : 1.0;
-        const double tr = __shfl(r, t, kWave);
-        const int32_t tc = __shfl(c, t, kWave);
-        sat_rows(s, lane, wpre[w], h ? B.rb[e] : 0u, h ? B.len[e] : 0, tr / tp, tp, h ? tc : -1 SC_ANAT_ARGS);
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    uint64_t mx = __ballot(rdy && ce > cb + uint32_t(K) * CW);  // tasks of more than one chunk
-    while (mx) {  // wave-uniform
-      const int t = __builtin_ctzll(mx);
-      mx &= mx - 1;
-      const int32_t tc = __shfl(c, t, kWave);
-      const double tr = __shfl(r, t, kWave);
-      const uint32_t te = uint32_t(__shfl(int(ce), t, kWave));
-      const bool tdup = __shfl(int(dup), t, kWave) != 0;
-      for (uint32_t base = uint32_t(__shfl(int(cb), t, kWave)) + uint32_t(K) * CW; base < te;
-           base += uint32_t(K) * CW)  // wave-uniform
-        saturate_chunk(s, tc, tr, base, CW == kWave ? te : min(te, base + CW), round, lane, wpre[w],
-                       tdup SC_ANAT_ARGS);
-    }
-  }
 #if LMM_ANAT
   if (an && lane == 0) {
     arec[0] = t_in;
