@@ -21,6 +21,9 @@ PASSES = {
         "w64": "frontier saturation 64-element chunks (product)", "w32": "32-element chunks", "w16": "16-element chunks"}),
     "abe_": ("E", "scripts/gpu_r06_e.sh", {
         "q": "mm_saturate_q (product)", "b64": "batched saturation M = 4", "b32": "batched, 32-element chunks"}),
+    "abg_": ("G", "scripts/gpu_r06_g.sh", {
+        "prev": "build before the two levers (abl/prev)", "new": "tied ratios loaded together + deferred frontier pushes",
+        "nodf": "tied ratios loaded together, LMMHIP_FR_DEFER=0"}),
 }
 
 

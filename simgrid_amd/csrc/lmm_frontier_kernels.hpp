@@ -224,14 +224,16 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
   double minr = dinf();
   if (nmin > 1 || vb > 0) {  // exact ratios at the minimal key: lexicographic min of (ratio, id)
     newt = INT_MAX;
+    double rr[R];  // the tied constraints' ratios, all loads issued before the first compare (one dependent level:
+                   // a compare right after each conditional load waited for the loads one at a time)
 #pragma unroll
     for (int i = 0; i < R; i++)
-      if (kk[i] == mk) {
-        const double r = s.cst[cc[i]].ratio;
-        if (r < minr || (r == minr && cc[i] < newt)) {
-          minr = r;
-          newt = cc[i];
-        }
+      rr[i] = kk[i] == mk ? s.cst[cc[i]].ratio : dinf();
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      if (kk[i] == mk && (rr[i] < minr || (rr[i] == minr && cc[i] < newt))) {
+        minr = rr[i];
+        newt = cc[i];
       }
     for (uint32_t j = b + R; j < e; j++) {
       const int32_t c = s.csr_cs[j].x;
@@ -441,12 +443,23 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
 // variable, and a variable appears once in c's CSC unless c has a duplicate element (cdup: claimed by
 // atomicCAS, as before).
 constexpr int kFrSatU = 8;
+// Deferred pushes (round 6): a wave's loads wait for its older stores and atomics (vmcnt counts them in order), so in
+// a chunk whose claimed rows take two passes the second pass's row loads sat behind the first pass's pushes — the
+// critical wave of a C4 round (profiles/r06_c4_round_anatomy.json: rows 4.8 us, pushes 6.3 us over two passes).  With
+// `df`, each pass leaves its elements' (constraint, decrements) in the wave's LDS and the pushes of up to kFrDefer
+// elements are issued after the loads of all their passes.
+constexpr int kFrDefer = 2 * kFrSatU * kWave;
+constexpr int32_t kDfFat = 1 << 30;  // (constraint ids < 2^30 when deferring)
+struct FrDefer {
+  long long a0[kFrDefer], a1[kFrDefer];
+  int32_t ec[kFrDefer];
+};
 
 // (LMM_ANAT: `an` = the chunk's dependent levels into aa->lv: 2 CSC elements + variable states, 3 the claimed rows'
 // elements, 4 their constraints' words, 5 the pushes issued, 6 the claims / values stored; wc[1] chunks, wc[2] fixed
 // variables, wc[3] pushed elements)
 __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t cend,
-                                             int round, int lane, int* pre, bool dup
+                                             int round, int lane, int* pre, bool dup, FrDefer* df
 #if LMM_ANAT
                                              , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
 #endif
@@ -505,6 +518,13 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
   const int total = __shfl(incl, kWave - 1, kWave);
   pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
   __builtin_amdgcn_wave_barrier();
+  auto push = [&](int ec, bool ef, long long e0, long long e1) {  // one element's pushes by a quad of lanes
+    if (ec >= 0 && q < 3 && (!ef || q == 2))
+      atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
+    if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
+      atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
+  };
+  int gb = 0;  // (df) first element of the deferred group
   for (int f0 = 0; f0 < total; f0 += kFrSatU * kWave) {  // wave-uniform (one pass up to 512 elements)
     int32_t cc[kFrSatU];
     int ol[kFrSatU];
@@ -561,23 +581,36 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
         a0 = (long long)dec_q(ww[u] * ox, cexp_rem(cx[u]));
         a1 = fat ? (long long)fat_bits(ww[u] / op) : (long long)dec_q(ww[u] / op, cexp_use(cx[u]));
       }
+      if (df) {  // wave-uniform: kept for after the group's loads
+        const int g = f0 - gb + u * kWave + lane;
+        df->ec[g] = tc < 0 ? -1 : (tc | (fat ? kDfFat : 0));
+        df->a0[g] = a0;
+        df->a1[g] = a1;
+        continue;
+      }
       const int nel = total - f0 - u * kWave;
 #pragma unroll
       for (int t = 0; t < kWave / 16; t++) {  // each element's pushes by a quad of lanes: one atomic request
         if (t * 16 >= nel)
           break;
         const int e = t * 16 + (lane >> 2);
-        const int ec = __shfl(tc, e, kWave);
-        const int ef = __shfl(int(fat), e, kWave);
-        const long long e0 = __shfl(a0, e, kWave);
-        const long long e1 = __shfl(a1, e, kWave);
-        if (ec >= 0 && q < 3 && (!ef || q == 2))
-          atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
-        if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
-          atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
+        push(__shfl(tc, e, kWave), __shfl(int(fat), e, kWave) != 0, __shfl(a0, e, kWave), __shfl(a1, e, kWave));
       }
     }
-    FS_LVL(5, 0u);
+    const int fe = f0 + kFrSatU * kWave;
+    if (df && (fe - gb >= kFrDefer || fe >= total)) {  // wave-uniform: the group's pushes
+      const int n = min(fe, total) - gb;
+      __builtin_amdgcn_wave_barrier();
+      for (int e0 = 0; e0 < n; e0 += 16) {
+        const int e = e0 + (lane >> 2);
+        const int ecf = e < n ? df->ec[e] : -1;
+        push(ecf < 0 ? -1 : (ecf & ~kDfFat), (ecf & kDfFat) != 0, e < n ? df->a0[e] : 0ll, e < n ? df->a1[e] : 0ll);
+      }
+      __builtin_amdgcn_wave_barrier();
+      gb = fe;
+    }
+    if (!df || gb == fe)
+      FS_LVL(5, 0u);
   }
   if (lv >= 0) {  // the claim and the value, last
     if (!dup)
@@ -597,7 +630,7 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
 #define FR_ANAT_ARGS
 #endif
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L FR_ANAT_PARAMS) {
+__device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L, FrDefer* dfw FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int ta = L.na, tb = L.nb;
@@ -615,7 +648,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
                      s.cdup[cc] != 0);
     else
       fr_sat_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
-                   s.cdup[cc] != 0 FR_ANAT_ARGS);
+                   s.cdup[cc] != 0, dfw ? dfw + w : nullptr FR_ANAT_ARGS);
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -627,8 +660,8 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 constexpr int kFS = 1024;
 
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L
-                                           FR_ANAT_PARAMS) {
+__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L,
+                                           FrDefer* dfw FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t c = int64_t(vb) * NB + threadIdx.x;
@@ -685,10 +718,11 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   }
 #endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
+    fr_flush<NB, kOld>(s, round, L, dfw FR_ANAT_ARGS);
 }
 
-template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+template <int kFS, bool kOld = false, bool kDf = false>
+__global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -700,8 +734,11 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
   if (s.ctl[CTL_DONE])
     return;
   __shared__ SatLds<kFS, kFS> L;
+  // kDf: deferred pushes (FrDefer, 20 KB of LDS per wave: one 256-thread workgroup per CU)
+  __shared__ FrDefer dfs[kDf ? kFS / kWave : 1];
+  FrDefer* dfw = kDf ? dfs : nullptr;
 #if LMM_ANAT
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, dfw, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -712,7 +749,7 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
       arec[10 + i] = wc[i];
   }
 #else
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, dfw);
 #endif
 }
 
@@ -730,7 +767,7 @@ __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bi
     const uint32_t ce = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
     for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
-      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup FR_ANAT_ARGS);
+      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup, nullptr FR_ANAT_ARGS);
     if (k == 0 && lane == 0)
       s.ctouch[c] = 2;
   }

@@ -603,10 +603,20 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   double minr = dinf();
   if (nmin > 1 || vb > 0) {  // exact ratios at the minimal key: lexicographic min of (ratio, id)
     newt = INT_MAX;
+    // the tied constraints' ratios: all loads issued before the first compare (one dependent level: a compare right
+    // after each conditional load waits for the loads one at a time).  Not in the persistent kernel (kRec = kRdq =
+    // false), whose 128-VGPR budget the ratios array exceeds (47 VGPRs spilled).
+    constexpr bool kTieLd = kRec || kRdq;
+    double rr[kTieLd ? R : 1];
+    if (kTieLd) {
+#pragma unroll
+      for (int i = 0; i < R; i++)
+        rr[kTieLd ? i : 0] = kk[i] == mk ? s.cst[cc[i]].ratio : dinf();
+    }
 #pragma unroll
     for (int i = 0; i < R; i++)
       if (kk[i] == mk) {
-        const double r = s.cst[cc[i]].ratio;
+        const double r = kTieLd ? rr[kTieLd ? i : 0] : s.cst[cc[i]].ratio;
         if (r < minr || (r == minr && cc[i] < newt)) {
           minr = r;
           newt = cc[i];
