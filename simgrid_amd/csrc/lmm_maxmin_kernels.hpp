@@ -1690,9 +1690,11 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
       const int64_t cl = gbase + l;
       const uint32_t b = s.cnst_ptr[cl], e = s.cnst_ptr[cl + 1];
       double m = 0.0;
-      for (uint32_t j = b + lane; j < e; j += kWave)
-        if (!(s.x[s.csc_v[j]] > 0))
-          m = fmax(m, s.csc_u[j]);
+      // (the element's w/p loaded with its variable: no branch between a load and the next one)
+      for (uint32_t j = b + lane; j < e; j += kWave) {
+        const double u = s.csc_u[j];
+        m = !(s.x[s.csc_v[j]] > 0) ? fmax(m, u) : m;
+      }
       m = wave_max(m);
       if (lane == l)
         fuse = m;
