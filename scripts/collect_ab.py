@@ -24,6 +24,10 @@ PASSES = {
     "abg_": ("G", "scripts/gpu_r06_g.sh", {
         "prev": "build before the two levers (abl/prev)", "new": "tied ratios loaded together + deferred frontier pushes",
         "nodf": "tied ratios loaded together, LMMHIP_FR_DEFER=0"}),
+    "abh_": ("H", "scripts/gpu_r06_h.sh", {
+        "prev": "before the tie loads (abl/prev)", "tie": "tie loads, no deferral (abl/tie, LMMHIP_FR_DEFER=0)",
+        "nous": "+ one-level ready test with LDS-stashed state + floor read before the slot store, LMMHIP_FR_UPDSPEC=0",
+        "new": "+ fr_update state loads with the keys (LMMHIP_FR_UPDSPEC=1, the default)"}),
 }
 
 

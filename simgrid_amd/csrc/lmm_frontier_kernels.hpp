@@ -283,9 +283,9 @@ __device__ __forceinline__ int fr_revote(const Dev& s, int v, int t, uint32_t b,
   // (a floor of kDead32 — no other alive constraint, unbounded — is stored as kDead32 - 1: the vote then
   // moves only when newt itself dies, exactly as before)
   const uint32_t fl = min(row_floor32(sk, mk, vb, p), kNoVoter - 1u);
-  s.vslot[slot] = fl;
-  if (kMinfl && !kEarly)
+  if (kMinfl && !kEarly)  // (loaded before the slot's store: a load issued after a store waits for it)
     mfn = s.minfl[newt];
+  s.vslot[slot] = fl;
   if (kMinfl && fl < mfn)
     atomicMin(&s.minfl[newt], fl);
   if (newt == t) {
@@ -443,23 +443,14 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
 // variable, and a variable appears once in c's CSC unless c has a duplicate element (cdup: claimed by
 // atomicCAS, as before).
 constexpr int kFrSatU = 8;
-// Deferred pushes (round 6): a wave's loads wait for its older stores and atomics (vmcnt counts them in order), so in
-// a chunk whose claimed rows take two passes the second pass's row loads sat behind the first pass's pushes — the
-// critical wave of a C4 round (profiles/r06_c4_round_anatomy.json: rows 4.8 us, pushes 6.3 us over two passes).  With
-// `df`, each pass leaves its elements' (constraint, decrements) in the wave's LDS and the pushes of up to kFrDefer
-// elements are issued after the loads of all their passes.
-constexpr int kFrDefer = 2 * kFrSatU * kWave;
-constexpr int32_t kDfFat = 1 << 30;  // (constraint ids < 2^30 when deferring)
-struct FrDefer {
-  long long a0[kFrDefer], a1[kFrDefer];
-  int32_t ec[kFrDefer];
-};
+// (Round 6, measured and removed: the pushes of a chunk's passes kept in LDS and issued after all its loads, so that a
+// second pass's loads do not wait for the first pass's atomics — C4 3.27 ms against 3.14-3.19 without, same box.)
 
 // (LMM_ANAT: `an` = the chunk's dependent levels into aa->lv: 2 CSC elements + variable states, 3 the claimed rows'
 // elements, 4 their constraints' words, 5 the pushes issued, 6 the claims / values stored; wc[1] chunks, wc[2] fixed
 // variables, wc[3] pushed elements)
 __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t cend,
-                                             int round, int lane, int* pre, bool dup, FrDefer* df
+                                             int round, int lane, int* pre, bool dup
 #if LMM_ANAT
                                              , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
 #endif
@@ -518,13 +509,6 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
   const int total = __shfl(incl, kWave - 1, kWave);
   pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
   __builtin_amdgcn_wave_barrier();
-  auto push = [&](int ec, bool ef, long long e0, long long e1) {  // one element's pushes by a quad of lanes
-    if (ec >= 0 && q < 3 && (!ef || q == 2))
-      atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
-    if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
-      atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
-  };
-  int gb = 0;  // (df) first element of the deferred group
   for (int f0 = 0; f0 < total; f0 += kFrSatU * kWave) {  // wave-uniform (one pass up to 512 elements)
     int32_t cc[kFrSatU];
     int ol[kFrSatU];
@@ -581,36 +565,23 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
         a0 = (long long)dec_q(ww[u] * ox, cexp_rem(cx[u]));
         a1 = fat ? (long long)fat_bits(ww[u] / op) : (long long)dec_q(ww[u] / op, cexp_use(cx[u]));
       }
-      if (df) {  // wave-uniform: kept for after the group's loads
-        const int g = f0 - gb + u * kWave + lane;
-        df->ec[g] = tc < 0 ? -1 : (tc | (fat ? kDfFat : 0));
-        df->a0[g] = a0;
-        df->a1[g] = a1;
-        continue;
-      }
       const int nel = total - f0 - u * kWave;
 #pragma unroll
       for (int t = 0; t < kWave / 16; t++) {  // each element's pushes by a quad of lanes: one atomic request
         if (t * 16 >= nel)
           break;
         const int e = t * 16 + (lane >> 2);
-        push(__shfl(tc, e, kWave), __shfl(int(fat), e, kWave) != 0, __shfl(a0, e, kWave), __shfl(a1, e, kWave));
+        const int ec = __shfl(tc, e, kWave);
+        const int ef = __shfl(int(fat), e, kWave);
+        const long long e0 = __shfl(a0, e, kWave);
+        const long long e1 = __shfl(a1, e, kWave);
+        if (ec >= 0 && q < 3 && (!ef || q == 2))
+          atomicAdd(&s.cst[ec].drem + q, (unsigned long long)(q == 0 ? e0 : q == 1 ? e1 : 1ll));
+        if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
+          atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
       }
     }
-    const int fe = f0 + kFrSatU * kWave;
-    if (df && (fe - gb >= kFrDefer || fe >= total)) {  // wave-uniform: the group's pushes
-      const int n = min(fe, total) - gb;
-      __builtin_amdgcn_wave_barrier();
-      for (int e0 = 0; e0 < n; e0 += 16) {
-        const int e = e0 + (lane >> 2);
-        const int ecf = e < n ? df->ec[e] : -1;
-        push(ecf < 0 ? -1 : (ecf & ~kDfFat), (ecf & kDfFat) != 0, e < n ? df->a0[e] : 0ll, e < n ? df->a1[e] : 0ll);
-      }
-      __builtin_amdgcn_wave_barrier();
-      gb = fe;
-    }
-    if (!df || gb == fe)
-      FS_LVL(5, 0u);
+    FS_LVL(5, 0u);
   }
   if (lv >= 0) {  // the claim and the value, last
     if (!dup)
@@ -629,8 +600,21 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
 #define FR_ANAT_PARAMS
 #define FR_ANAT_ARGS
 #endif
+// The ready constraints a saturation workgroup collected, with their CSC chunk prefix and — loaded by the ready test
+// itself (round 6) — their CSC range, ratio and duplicate flag, so that a chunk's first loads are its CSC elements.
+template <int NB> struct FrSatLds {
+  int32_t rc[NB];      // collected ready constraints
+  int32_t rr[NB + 1];  // exclusive prefix of their chunk counts
+  uint32_t rb[NB], re[NB];
+  double rt[NB];
+  uint8_t rd[NB];
+  int wa[NB / kWave], wb[NB / kWave];
+  int na, nb;
+  int pre[NB / kWave][kWave];  // fr_sat_chunk's per-wave row-length prefix
+};
+
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>& L, FrDefer* dfw FR_ANAT_PARAMS) {
+__device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& L FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int ta = L.na, tb = L.nb;
@@ -642,13 +626,12 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
         k += step;
     const int32_t cc = L.rc[k];
     const int ch = g - L.rr[k];
-    const double r = ld_rlx(&s.cst[cc].ratio);  // wave-uniform address: keep it off the scalar cache
+    const double r = L.rt[k];
     if (kOld)  // (measurement: the multi-launch engine's chunk body)
-      saturate_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
-                     s.cdup[cc] != 0);
+      saturate_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0);
     else
-      fr_sat_chunk(s, cc, r, s.cnst_ptr[cc] + uint32_t(ch) * kWave, s.cnst_ptr[cc + 1], round, lane, L.pre[w],
-                   s.cdup[cc] != 0, dfw ? dfw + w : nullptr FR_ANAT_ARGS);
+      fr_sat_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0
+                   FR_ANAT_ARGS);
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -660,16 +643,37 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, SatLds<NB, NB>
 constexpr int kFS = 1024;
 
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, SatLds<NB, NB>& L,
-                                           FrDefer* dfw FR_ANAT_PARAMS) {
+__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, FrSatLds<NB>& L
+                                           FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t c = int64_t(vb) * NB + threadIdx.x;
   bool rdy = false;
   int nch = 0;
-  if (c < s.nC && s.key32[c] != kDead32 && s.nvote[c] == 0) {
+  // every load of the ready test in one dependent level (round 6; the short-circuit test took three: key, then vote
+  // count, then CSC range), and — in the 256-thread workgroups of the small systems, where the extra lines are few —
+  // the ratio and duplicate flag with them (coalesced: one constraint per lane)
+  uint32_t kc = kDead32, cb = 0, ce = 0;
+  int nv = 1;
+  double rt = 0.0;
+  bool dp = false;
+  if (c < s.nC) {
+    kc = s.key32[c];
+    nv = s.nvote[c];
+    cb = s.cnst_ptr[c];
+    ce = s.cnst_ptr[c + 1];
+    if (NB == 256) {
+      rt = s.cst[c].ratio;
+      dp = s.cdup[c] != 0;
+    }
+  }
+  if (kc != kDead32 && nv == 0) {
     rdy = true;
-    nch = int((s.cnst_ptr[c + 1] - s.cnst_ptr[c] + kWave - 1) / kWave);
+    if (NB != 256) {
+      rt = s.cst[c].ratio;
+      dp = s.cdup[c] != 0;
+    }
+    nch = int((ce - cb + kWave - 1) / kWave);
     if (s.vstat)
       atomicAdd(s.vstat + 2 * (int64_t(round) * kMaxBlocks + kDiagSlot) + 5, 1);
     if (nch > bigch) {  // rare (fat-tree core links): spread over the grid by fr_sat_big
@@ -701,8 +705,13 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
     tb += L.wb[k];
   }
   if (rdy) {
-    L.rc[oa + ia - 1] = int32_t(c);
-    L.rr[oa + ia - 1] = ob + ib - nch;
+    const int k = oa + ia - 1;
+    L.rc[k] = int32_t(c);
+    L.rr[k] = ob + ib - nch;
+    L.rb[k] = cb;
+    L.re[k] = ce;
+    L.rt[k] = rt;
+    L.rd[k] = uint8_t(dp);
   }
   if (threadIdx.x == 0) {
     L.na = ta;
@@ -718,11 +727,10 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   }
 #endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld>(s, round, L, dfw FR_ANAT_ARGS);
+    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
 }
 
-template <int kFS, bool kOld = false, bool kDf = false>
-__global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -733,12 +741,9 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #endif
   if (s.ctl[CTL_DONE])
     return;
-  __shared__ SatLds<kFS, kFS> L;
-  // kDf: deferred pushes (FrDefer, 20 KB of LDS per wave: one 256-thread workgroup per CU)
-  __shared__ FrDefer dfs[kDf ? kFS / kWave : 1];
-  FrDefer* dfw = kDf ? dfs : nullptr;
+  __shared__ FrSatLds<kFS> L;
 #if LMM_ANAT
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, dfw, an, &aa, wc);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -749,7 +754,7 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
       arec[10 + i] = wc[i];
   }
 #else
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, dfw);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
 #endif
 }
 
@@ -767,7 +772,7 @@ __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bi
     const uint32_t ce = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
     for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
-      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup, nullptr FR_ANAT_ARGS);
+      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup FR_ANAT_ARGS);
     if (k == 0 && lane == 0)
       s.ctouch[c] = 2;
   }
@@ -836,8 +841,10 @@ struct FrUpdLds {
 // atomic stores; the multi-launch kernel keeps its plain stores).
 // (LMM_ANAT: `an` = the levels into aa->lv: 0 keys + touch flags, 1 touched records, 2 arithmetic + scan prefix +
 // barrier, 3 slots, 4 queued voters' variable and row, 5 stores + barriers; wc[0] scanned slots)
+// spec (round 6, small systems): a constraint's record, scales, votes, floor and CSC range are loaded with its key and
+// touch flag whether or not it was touched (coalesced, one constraint per lane), one dependent level instead of two.
 template <bool kP = false>
-__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int vb, FrUpdLds& U
+__device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int vb, FrUpdLds& U, bool spec
                                               FR_ANAT_PARAMS) {
   int& qn = U.qn;
   auto& pre = U.pre;
@@ -870,7 +877,7 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   int32_t ce = 0, nv = 0;
   uint32_t mfl = kNoVoter;
   uint32_t cb = 0, cend = 0;
-  if (tch) {
+  if (spec ? in : tch) {
     const CstRec* rec = s.cst + c;
     qx = rec->drem;
     qy = rec->duse;
@@ -1069,7 +1076,7 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
 #endif
 }
 
-__global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) {
+__global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec, int spec) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_UPD);
   const bool an = arec != nullptr;
@@ -1082,7 +1089,7 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
     return;
   __shared__ FrUpdLds U;
 #if LMM_ANAT
-  fr_update_blk(s, round, prec, blockIdx.x, U, an, &aa, wc);
+  fr_update_blk(s, round, prec, blockIdx.x, U, spec != 0, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -1092,7 +1099,7 @@ __global__ void __launch_bounds__(kFB) fr_update(Dev s, int round, double prec) 
     arec[9] = wc[0];
   }
 #else
-  fr_update_blk(s, round, prec, blockIdx.x, U);
+  fr_update_blk(s, round, prec, blockIdx.x, U, spec != 0);
 #endif
 }
 

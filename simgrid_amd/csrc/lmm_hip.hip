@@ -1679,9 +1679,9 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int sat_b0 = int64_t(nblkS) >= 2 * int64_t(c->n_cu) ? kFS : 256;
   const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
   const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
-  // pushes deferred past the loads of a chunk's passes (fr_sat_chunk, FrDefer): 256-thread saturation workgroups of
-  // 85 KB of LDS, one per CU — when the grid fits the chip in one pass (C4: ~100 workgroups)
-  const bool sat_df = env_int("LMMHIP_FR_DEFER", 1) != 0 && nblk <= c->n_cu && d.nC < kDfFat;
+  // fr_update: every constraint's state loaded with its key (one dependent level less) on the small systems, where the
+  // 256-thread saturation workgroups run (LMMHIP_FR_UPDSPEC, A/B knob)
+  const int upd_spec = env_int("LMMHIP_FR_UPDSPEC", sat_b == 256 ? 1 : 0);
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
@@ -1718,8 +1718,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       }
       if (sat_b == 256 && sat_old)
         LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
-      else if (sat_b == 256 && sat_df)
-        LAUNCH(4, r, (fr_sat<256, false, true>), nblk, 256, d, int(r), bigch);
       else if (sat_b == 256)
         LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
       else if (sat_old)
@@ -1728,7 +1726,7 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
         LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
       if (big)
         LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r), bigw);
-      LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec);
+      LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec, upd_spec);
     }
     LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
     HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
