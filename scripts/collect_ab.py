@@ -28,6 +28,10 @@ PASSES = {
         "prev": "before the tie loads (abl/prev)", "tie": "tie loads, no deferral (abl/tie, LMMHIP_FR_DEFER=0)",
         "nous": "+ one-level ready test with LDS-stashed state + floor read before the slot store, LMMHIP_FR_UPDSPEC=0",
         "new": "+ fr_update state loads with the keys (LMMHIP_FR_UPDSPEC=1, the default)"}),
+    "abi_": ("I", "scripts/gpu_r06_i.sh", {
+        "ag0": "LMMHIP_FR_AGG=0 (pushes straight to the constraint records)",
+        "ag1": "pushes aggregated per constraint in LDS (default)",
+        "tie": "FairBottleneck before the load reorder (abl/tie)", "new": "FB chain / increment loads before stores"}),
 }
 
 
