@@ -40,7 +40,7 @@ def main(out=os.path.join(ROOT, "profiles", "r06_ab.json")):
     for pre, (name, script, what) in PASSES.items():
         rows = {}
         for p in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", pre + "*.out"))):
-            m = re.match(re.escape(pre) + r"(c2s|c2|c4)_([a-z0-9]+?)(?:_(\d))?\.out$", os.path.basename(p))
+            m = re.match(re.escape(pre) + r"(c2s|c2|c3|c4|c5)_([a-z0-9]+?)(?:_(\d))?\.out$", os.path.basename(p))
             if not m:
                 continue
             try:

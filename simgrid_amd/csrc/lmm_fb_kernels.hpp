@@ -166,9 +166,9 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
 // :89-105 — per listed variable: mu = min(usage/w, bound - value); value += mu; exact
 // `value == bound` drops it from the list.
 // :89-105 once the minimum of usage / w over the row is known: bound, value, exact `value == bound` delisting.
-// (vb, x: the variable's bound and value, loaded with its listed flag — round 6: a load after the row's LDS atomics
-// and the previous rows' stores waited for them)
-__device__ __forceinline__ int var_inc_finish(const Dev& s, int64_t v, double inc, int round, double vb, double x) {
+__device__ __forceinline__ int var_inc_finish(const Dev& s, int64_t v, double inc, int round) {
+  const double vb = s.vbound[v];
+  double x = s.x[v];
   if (vb > 0)
     inc = fmin(inc, vb - x);
   s.vtmp[v] = inc;
@@ -207,7 +207,6 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
     const bool in = v < s.nV;
     const bool listed = in && s.vst[v];
     const uint32_t b = in ? s.var_ptr[v] : 0u, e = in ? s.var_ptr[v + 1] : 0u;
-    const double vb = in ? s.vbound[v] : 0.0, x0 = in ? s.x[v] : 0.0;
     const int nlisted = __popcll(__ballot(listed));
     nvl += listed;
     if (nlisted == 0)
@@ -232,7 +231,7 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
           if (cc[k] >= 0)
             inc = fmin(inc, uu[k] / ww[k] + 0.0);
       }
-      any |= var_inc_finish(s, v, inc, round, vb, x0);
+      any |= var_inc_finish(s, v, inc, round);
       continue;
     }
     const int last = int(s.nV - 1 - base < kWave - 1 ? s.nV - 1 - base : kWave - 1);
@@ -269,7 +268,7 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
     }
     __builtin_amdgcn_wave_barrier();
     if (listed)
-      any |= var_inc_finish(s, v, __longlong_as_double((long long)wmn[lane]), round, vb, x0);
+      any |= var_inc_finish(s, v, __longlong_as_double((long long)wmn[lane]), round);
     __builtin_amdgcn_wave_barrier();
   }
   if (__any(any) && (threadIdx.x & (kWave - 1)) == 0)
@@ -801,7 +800,9 @@ __device__ void fb_long_chain(const Dev& s, int32_t c, double prec, double* sh) 
 // shorter shared ones through fb_chain_pull, FATPIPE ones from the chunk minima (fbk_accc); remaining <= 0
 // erases the constraint (:129).
 // nlb: the workgroups that take the long chains (list entries b, b + nlb, ...).  Round 5 measured taking them
-// longest first from a queue (LMMHIP_FB_LPT): 8.38 vs 8.35-8.37 ms on C5, removed in round 6.
+// longest first from a queue (LMMHIP_FB_LPT): 8.38 vs 8.35-8.37 ms on C5, removed in round 6.  Round 6 measured the
+// constraint's ratio / remaining loaded with its flags before the erased-flag store, with fb_var_inc's bound / value
+// loaded with the listed flags: 8.40-8.41 against 8.36-8.37, not kept.
 __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uint32_t longmin, int nlb) {
   if (s.ctl[CTL_DONE])
     return;
@@ -823,18 +824,15 @@ __global__ void __launch_bounds__(kBlock) fbk_update_seq(Dev s, double prec, uin
   double* d = dl[threadIdx.x / kWave];
   for (int64_t c = (int64_t(blockIdx.x - nlb) * kBlock + threadIdx.x) / kWave; c < s.nC;
        c += int64_t(gridDim.x - nlb) * (kBlock / kWave)) {  // wave-uniform
-    // the constraint's flags, range, ratio and remaining in one dependent level, all before the wave's first store (a
-    // load issued after a store waits for it: the ratio test came after the erased flag's store, round 5)
     const bool fat = s.cflags[c] & 1;
     const uint32_t cb = s.cnst_ptr[c], ce = s.cnst_ptr[c + 1];
-    const double rt = s.ratio[c];
-    double rem = s.rem[c];
     if (!fat && ce - cb >= longmin)  // a long constraint: its workgroup writes everything
       continue;
     if (lane == 0)
       s.erased[c] = 0;
-    if (rt != 0.0)
+    if (s.ratio[c] != 0.0)
       continue;
+    double rem = s.rem[c];
     if (fat) {
       double u;
       rem = fb_fat_update(s, c, rem, s.xmin[c], prec, &u);

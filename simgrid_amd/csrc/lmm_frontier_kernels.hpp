@@ -444,37 +444,16 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
 // atomicCAS, as before).
 constexpr int kFrSatU = 8;
 // (Round 6, measured and removed: the pushes of a chunk's passes kept in LDS and issued after all its loads, so that a
-// second pass's loads do not wait for the first pass's atomics — C4 3.27 ms against 3.14-3.19 without, same box.)
-//
-// Pushes aggregated per constraint (round 6, `ag`): the flows a saturating link carries share most of their other
-// links (a fat-tree host link's flows all take the host's link in the other direction and a few switch links), so one
-// pass of a C4 chunk sends ~50 of its ~580 pushes to the same constraint (tests on the C4 system: median of the chunks'
-// largest multiplicity 50) — atomics to one address serialise in the memory-side unit, ~12 ns each.  With `ag`, each
-// lane adds its element's fixed-point decrements into a per-wave LDS table keyed by the constraint (64-bit LDS atomics;
-// integer sums, so the result is bit-identical), and after the pass one lane per used slot pushes the sums: one
-// request per distinct constraint.  A lane whose probes find no slot pushes directly; FATPIPE elements (atomicMax) too.
-constexpr int kAggSlots = 256;  // per wave: 6 KB of LDS
-constexpr int kAggProbe = 8;
-struct FrAgg {
-  unsigned long long a0[kAggSlots], a1[kAggSlots];
-  int32_t key[kAggSlots];
-  uint32_t cnt[kAggSlots];
-};
-__device__ __forceinline__ void fr_agg_init(FrAgg* ag, int lane) {
-  for (int i = lane; i < kAggSlots; i += kWave) {
-    ag->key[i] = -1;
-    ag->a0[i] = ag->a1[i] = 0ull;
-    ag->cnt[i] = 0u;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
+// second pass's loads do not wait for the first pass's atomics — C4 3.27 ms against 3.14-3.19 without, same box; and
+// the pushes aggregated per constraint in a per-wave LDS hash table (CAS-probed slots, 64-bit LDS adds, one global
+// atomic per distinct constraint and pass) against the hot-address serialisation of a saturating host link's flows,
+// whose other links repeat ~50 times in a chunk — C4 3.63 ms against 3.12: the table's probing and flush cost more.)
 
 // (LMM_ANAT: `an` = the chunk's dependent levels into aa->lv: 2 CSC elements + variable states, 3 the claimed rows'
 // elements, 4 their constraints' words, 5 the pushes issued, 6 the claims / values stored; wc[1] chunks, wc[2] fixed
 // variables, wc[3] pushed elements)
 __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t cend,
-                                             int round, int lane, int* pre, bool dup, FrAgg* ag
+                                             int round, int lane, int* pre, bool dup
 #if LMM_ANAT
                                              , bool an = false, AnatAcc* aa = nullptr, unsigned* wc = nullptr
 #endif
@@ -589,31 +568,6 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
         a0 = (long long)dec_q(ww[u] * ox, cexp_rem(cx[u]));
         a1 = fat ? (long long)fat_bits(ww[u] / op) : (long long)dec_q(ww[u] / op, cexp_use(cx[u]));
       }
-      if (ag) {  // wave-uniform: into the wave's table (a lane whose probes fail pushes directly)
-        if (tc >= 0 && !fat) {
-          uint32_t h = (uint32_t(tc) * 2654435761u) >> 24;  // (kAggSlots = 256)
-          bool in = false;
-          for (int pr = 0; pr < kAggProbe; pr++, h = (h + 1) & (kAggSlots - 1)) {
-            const int old = atomicCAS(&ag->key[h], -1, tc);
-            if (old == -1 || old == tc) {
-              atomicAdd(&ag->a0[h], (unsigned long long)a0);
-              atomicAdd(&ag->a1[h], (unsigned long long)a1);
-              atomicAdd(&ag->cnt[h], 1u);
-              in = true;
-              break;
-            }
-          }
-          if (!in) {
-            atomicAdd(&s.cst[tc].drem, (unsigned long long)a0);
-            atomicAdd(&s.cst[tc].duse, (unsigned long long)a1);
-            atomicAdd(&s.cst[tc].dcnt, 1ull);
-          }
-        } else if (tc >= 0) {  // FATPIPE: the removed w/p (fat_bits), and the count
-          atomicMax(&s.cst[tc].duse, (unsigned long long)a1);
-          atomicAdd(&s.cst[tc].dcnt, 1ull);
-        }
-        continue;
-      }
       const int nel = total - f0 - u * kWave;
 #pragma unroll
       for (int t = 0; t < kWave / 16; t++) {  // each element's pushes by a quad of lanes: one atomic request
@@ -629,27 +583,6 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
         if (ec >= 0 && ef && q == 1)  // FATPIPE: the removed w/p (fat_bits)
           atomicMax(&s.cst[ec].duse, (unsigned long long)e1);
       }
-    }
-    if (ag) {  // wave-uniform: the pass's sums, one push per used slot (by a lane quad: one request each)
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (int i0 = 0; i0 < kAggSlots; i0 += 16) {
-        const int i = i0 + (lane >> 2);
-        const int ec = ag->key[i];
-        if (ec >= 0 && q < 3)
-          atomicAdd(&s.cst[ec].drem + q, q == 0 ? ag->a0[i] : q == 1 ? ag->a1[i] : (unsigned long long)ag->cnt[i]);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < kAggSlots; i += kWave) {
-        if (ag->key[i] >= 0) {
-          ag->key[i] = -1;
-          ag->a0[i] = ag->a1[i] = 0ull;
-          ag->cnt[i] = 0u;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
     }
     FS_LVL(5, 0u);
   }
@@ -684,12 +617,10 @@ template <int NB> struct FrSatLds {
 };
 
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& L, FrAgg* ag FR_ANAT_PARAMS) {
+__device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& L FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int ta = L.na, tb = L.nb;
-  if (ag && w < tb)
-    fr_agg_init(ag + w, lane);
   for (int g = w; g < tb; g += NBW) {  // wave-uniform
     int k = 0;  // last collected entry whose first chunk is <= g
 #pragma unroll
@@ -702,8 +633,8 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& 
     if (kOld)  // (measurement: the multi-launch engine's chunk body)
       saturate_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0);
     else
-      fr_sat_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0,
-                   ag ? ag + w : nullptr FR_ANAT_ARGS);
+      fr_sat_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0
+                   FR_ANAT_ARGS);
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -715,7 +646,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& 
 constexpr int kFS = 1024;
 
 template <int NB, bool kOld>
-__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, FrSatLds<NB>& L, FrAgg* ag
+__device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, FrSatLds<NB>& L
                                            FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -799,12 +730,10 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   }
 #endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld>(s, round, L, ag FR_ANAT_ARGS);
+    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
 }
 
-// kAgg: pushes aggregated per constraint in LDS (FrAgg, 6 KB per wave; the 256-thread workgroups of small systems)
-template <int kFS, bool kOld = false, bool kAgg = false>
-__global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -816,10 +745,8 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
   if (s.ctl[CTL_DONE])
     return;
   __shared__ FrSatLds<kFS> L;
-  __shared__ FrAgg agl[kAgg ? kFS / kWave : 1];
-  FrAgg* ag = kAgg ? agl : nullptr;
 #if LMM_ANAT
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, ag, an, &aa, wc);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -830,7 +757,7 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
       arec[10 + i] = wc[i];
   }
 #else
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, ag);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
 #endif
 }
 
@@ -848,7 +775,7 @@ __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bi
     const uint32_t ce = s.cnst_ptr[c + 1];
     const bool dup = s.cdup[c] != 0;
     for (uint32_t base = s.cnst_ptr[c] + uint32_t(k) * kWave; base < ce; base += uint32_t(bigw) * kWave)
-      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup, nullptr FR_ANAT_ARGS);
+      fr_sat_chunk(s, c, r, base, ce, round, lane, wpre, dup FR_ANAT_ARGS);
     if (k == 0 && lane == 0)
       s.ctouch[c] = 2;
   }

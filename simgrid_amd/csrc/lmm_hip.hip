@@ -1682,8 +1682,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   // fr_update: every constraint's state loaded with its key (one dependent level less) on the small systems, where the
   // 256-thread saturation workgroups run (LMMHIP_FR_UPDSPEC, A/B knob)
   const int upd_spec = env_int("LMMHIP_FR_UPDSPEC", sat_b == 256 ? 1 : 0);
-  // fr_sat<256>: pushes aggregated per constraint in LDS before the atomics (FrAgg; LMMHIP_FR_AGG, A/B knob)
-  const bool sat_agg = env_int("LMMHIP_FR_AGG", 1) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
@@ -1720,8 +1718,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       }
       if (sat_b == 256 && sat_old)
         LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
-      else if (sat_b == 256 && sat_agg)
-        LAUNCH(4, r, (fr_sat<256, false, true>), nblk, 256, d, int(r), bigch);
       else if (sat_b == 256)
         LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
       else if (sat_old)
