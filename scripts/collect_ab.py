@@ -32,6 +32,9 @@ PASSES = {
         "ag0": "LMMHIP_FR_AGG=0 (pushes straight to the constraint records)",
         "ag1": "pushes aggregated per constraint in LDS (default)",
         "tie": "FairBottleneck before the load reorder (abl/tie)", "new": "FB chain / increment loads before stores"}),
+    "abj_": ("J", "scripts/gpu_r06_j.sh", {
+        "u8": "frontier saturation 8 claimed-row elements per lane per pass (LMMHIP_FR_SATU16=0)",
+        "u16": "16 per lane per pass on the small systems (default)"}),
 }
 
 
