@@ -447,15 +447,12 @@ constexpr int kFrSatU = 8;
 // second pass's loads do not wait for the first pass's atomics — C4 3.27 ms against 3.14-3.19 without, same box; and
 // the pushes aggregated per constraint in a per-wave LDS hash table (CAS-probed slots, 64-bit LDS adds, one global
 // atomic per distinct constraint and pass) against the hot-address serialisation of a saturating host link's flows,
-// whose other links repeat ~50 times in a chunk — C4 3.63 ms against 3.12: the table's probing and flush cost more.)
+// whose other links repeat ~50 times in a chunk — C4 3.63 ms against 3.12: the table's probing and flush cost more;
+// and 16 claimed-row elements per lane per pass instead of 8, a C4 chunk's pushes in one pass — 3.28 against 3.12.)
 
 // (LMM_ANAT: `an` = the chunk's dependent levels into aa->lv: 2 CSC elements + variable states, 3 the claimed rows'
 // elements, 4 their constraints' words, 5 the pushes issued, 6 the claims / values stored; wc[1] chunks, wc[2] fixed
 // variables, wc[3] pushed elements)
-// U: claimed-row elements per lane per pass (U x 64 per pass; the 256-thread workgroups of small systems, one per CU,
-// take U = 16 — a C4 chunk's ~580-770 pushes in one pass instead of two, whose second pass's loads waited for the
-// first pass's atomics; register budget is no concern at one workgroup per CU)
-template <int U = kFrSatU>
 __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, uint32_t j0, uint32_t cend,
                                              int round, int lane, int* pre, bool dup
 #if LMM_ANAT
@@ -516,12 +513,12 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
   const int total = __shfl(incl, kWave - 1, kWave);
   pre[lane] = incl - len;  // exclusive prefix (non-decreasing in lane)
   __builtin_amdgcn_wave_barrier();
-  for (int f0 = 0; f0 < total; f0 += U * kWave) {  // wave-uniform (one pass up to U x 64 elements)
-    int32_t cc[U];
-    int ol[U];
-    double ww[U];
+  for (int f0 = 0; f0 < total; f0 += kFrSatU * kWave) {  // wave-uniform (one pass up to 512 elements)
+    int32_t cc[kFrSatU];
+    int ol[kFrSatU];
+    double ww[kFrSatU];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < kFrSatU; u++) {
       const int f = f0 + u * kWave + lane;
       int o = 0;  // owner lane: last lane with pre <= f
 #pragma unroll
@@ -537,28 +534,28 @@ __device__ __forceinline__ void fr_sat_chunk(const Dev& s, int32_t c, double r, 
     if (an) {
       double sw = 0.0;
 #pragma unroll
-      for (int u = 0; u < U; u++) {
+      for (int u = 0; u < kFrSatU; u++) {
         sw += ww[u] + double(cc[u]);
         wc[3] += unsigned(__popcll(__ballot(cc[u] >= 0)));
       }
       ANAT_LVL(*aa, 3, sw);
     }
 #endif
-    int32_t cx[U];
+    int32_t cx[kFrSatU];
 #pragma unroll
-    for (int u = 0; u < U; u++)
+    for (int u = 0; u < kFrSatU; u++)
       cx[u] = cc[u] >= 0 ? s.cexp[cc[u]] : kCexpDead;  // scales, policy and liveness in one word
 #if LMM_ANAT
     if (an) {
       int32_t sx = 0;
 #pragma unroll
-      for (int u = 0; u < U; u++)
+      for (int u = 0; u < kFrSatU; u++)
         sx += cx[u];
       ANAT_LVL(*aa, 4, sx);
     }
 #endif
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < kFrSatU; u++) {
       const double ox = __shfl(lx, ol[u], kWave);
       const double op = __shfl(lp, ol[u], kWave);
       bool fat = false;
@@ -620,7 +617,7 @@ template <int NB> struct FrSatLds {
   int pre[NB / kWave][kWave];  // fr_sat_chunk's per-wave row-length prefix
 };
 
-template <int NB, bool kOld, int U = kFrSatU>
+template <int NB, bool kOld>
 __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& L FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -637,8 +634,8 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& 
     if (kOld)  // (measurement: the multi-launch engine's chunk body)
       saturate_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0);
     else
-      fr_sat_chunk<U>(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0
-                      FR_ANAT_ARGS);
+      fr_sat_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0
+                   FR_ANAT_ARGS);
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -649,7 +646,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& 
 // (fr_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
 constexpr int kFS = 1024;
 
-template <int NB, bool kOld, int U = kFrSatU>
+template <int NB, bool kOld>
 __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, FrSatLds<NB>& L
                                            FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
@@ -734,11 +731,10 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   }
 #endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld, U>(s, round, L FR_ANAT_ARGS);
+    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
 }
 
-template <int kFS, bool kOld = false, int U = kFrSatU>
-__global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -751,7 +747,7 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
     return;
   __shared__ FrSatLds<kFS> L;
 #if LMM_ANAT
-  fr_sat_blk<kFS, kOld, U>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -762,7 +758,7 @@ __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
       arec[10 + i] = wc[i];
   }
 #else
-  fr_sat_blk<kFS, kOld, U>(s, round, bigch, blockIdx.x, L);
+  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
 #endif
 }
 

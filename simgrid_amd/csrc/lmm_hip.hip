@@ -1682,8 +1682,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   // fr_update: every constraint's state loaded with its key (one dependent level less) on the small systems, where the
   // 256-thread saturation workgroups run (LMMHIP_FR_UPDSPEC, A/B knob)
   const int upd_spec = env_int("LMMHIP_FR_UPDSPEC", sat_b == 256 ? 1 : 0);
-  // fr_sat<256>: 16 claimed-row elements per lane per pass instead of 8 (LMMHIP_FR_SATU16, A/B knob)
-  const bool sat_u16 = env_int("LMMHIP_FR_SATU16", 1) != 0;
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
   LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
@@ -1720,8 +1718,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       }
       if (sat_b == 256 && sat_old)
         LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
-      else if (sat_b == 256 && sat_u16)
-        LAUNCH(4, r, (fr_sat<256, false, 16>), nblk, 256, d, int(r), bigch);
       else if (sat_b == 256)
         LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
       else if (sat_old)
