@@ -49,6 +49,20 @@ def solve_traffic(workload):
     return int(t["solve_counter_bytes_fetch_x2"]), int(t["solve_counter_bytes_raw"]), os.path.relpath(p, ROOT)
 
 
+def kernel_class(e):
+    """The dominant request class of one kernel's counters: read, write or atomic."""
+    rd = e.get("TCC_EA0_RDREQ_sum_per_launch", 0.0)
+    wr = e.get("TCC_EA0_WRREQ_sum_per_launch", 0.0)
+    at = e.get("TCC_EA0_ATOMIC_sum_per_launch", 0.0)
+    return max((("read", rd), ("write", wr - at), ("atomic", at)), key=lambda kv: kv[1])[0]
+
+
+def class_frac(e, rates):
+    """A kernel's request rate over the calibrated rate of its dominant class (None without calibration)."""
+    r = rates.get({"read": "gather<double>", "write": "scatter_u8", "atomic": "atomics_f64"}[kernel_class(e)])
+    return round(e["requests_per_s"] / r, 3) if r and e.get("requests_per_s") else None
+
+
 def request_roofline(workload, ms):
     """The request-rate roofline: memory-side requests per solve (rocprofv3 TCC_EA0_RDREQ_sum +
     TCC_EA0_WRREQ_sum over the solve's kernels, scripts/profile.sh PARTS=req, scripts/parse_rocprof.py) over the
@@ -81,7 +95,7 @@ def request_roofline(workload, ms):
                  "class_rates_per_s": {k: round(r, 1) for k, (_, r) in cls.items()},
                  "frac_serial": round(sum(parts.values()) / ms, 4), "frac_overlap": round(max(parts.values()) / ms, 4)}
     best = max(rates, key=rates.get) if rates else None
-    upload = ("rs_", "rocprim", "__amd", "mm_elem_usage", "mm_dup_check", "fr_c2s")  # not the solve's kernels
+    upload = ("rs_", "rocprim", "__amd", "mm_elem_usage", "mm_dup_check", "fr_c2s", "fbp_")  # not the solve's kernels
     top = sorted(((k, e) for k, e in t["kernels"].items() if e.get("requests_per_s") and not k.startswith(upload)),
                  key=lambda kv: -(kv[1]["TCC_EA0_RDREQ_sum"] + kv[1]["TCC_EA0_WRREQ_sum"]))[:4]
     return {"unit": "requests/s", "per_solve": round(per), "rdreq_per_solve": round(float(t["solve_rdreq"])),
@@ -95,7 +109,11 @@ def request_roofline(workload, ms):
             "calibration_rates": {k: round(v, 1) for k, v in rates.items()},
             "per_kernel": {k: {"requests_per_launch": round(e["TCC_EA0_RDREQ_sum_per_launch"] +
                                                             e["TCC_EA0_WRREQ_sum_per_launch"]),
-                               "requests_per_s": round(e["requests_per_s"], 1), "avg_us": round(e["avg_ns"] / 1e3, 2)}
+                               "requests_per_s": round(e["requests_per_s"], 1), "avg_us": round(e["avg_ns"] / 1e3, 2),
+                               # (VERDICT r05 Next #5) the kernel's rate against the ceiling of its dominant class:
+                               # reads at the calibrated random-gather rate, writes / atomics at theirs
+                               "class": kernel_class(e),
+                               "class_frac": class_frac(e, rates)}
                            for k, e in top},
             "source": os.path.relpath(p, ROOT)}
 
