@@ -35,6 +35,9 @@ PASSES = {
     "abj_": ("J", "scripts/gpu_r06_j.sh", {
         "u8": "frontier saturation 8 claimed-row elements per lane per pass (LMMHIP_FR_SATU16=0)",
         "u16": "16 per lane per pass on the small systems (default)"}),
+    "abl_": ("L", "scripts/gpu_r06_l.sh", {
+        "h": "final build before the speculative queue-entry load (abl/h)",
+        "new": "fr_vote's first queue entry loaded with the count"}),
 }
 
 
