@@ -38,6 +38,8 @@ PASSES = {
     "abl_": ("L", "scripts/gpu_r06_l.sh", {
         "h": "final build before the speculative queue-entry load (abl/h)",
         "new": "fr_vote's first queue entry loaded with the count"}),
+    "abm_": ("M", "scripts/gpu_r06_m.sh", {
+        "base": "product build", "wt": "round kernels' state stores written through (LMM_WT=1, abl/wt)"}),
 }
 
 
