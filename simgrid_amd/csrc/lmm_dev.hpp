@@ -2,7 +2,6 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
-#include <type_traits>
 
 #include <cfloat>
 #include <climits>
@@ -97,20 +96,6 @@ template <class T> __device__ __forceinline__ T ld_rlx(const T* p) {
 template <class T> __device__ __forceinline__ void st_rlx(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// LMM_WT (build knob, round 6, measurement): the round kernels' scattered state stores written through (sc1) instead of
-// left dirty in the XCD's L2, so that the launch boundary's release has fewer lines to write back (C2's boundaries take
-// 3-4 us, C4's 1.6-1.9: the round anatomy)
-#ifndef LMM_WT
-#define LMM_WT 0
-#endif
-template <class T> __device__ __forceinline__ void st_wt(T* p, T v) {
-#if LMM_WT
-  st_rlx(p, v);
-#else
-  *p = v;
-#endif
-}
-#define STW(lv, v) st_wt(&(lv), static_cast<std::remove_reference_t<decltype(lv)>>(v))
 
 struct Dev {
   int32_t nV, nC;

@@ -660,7 +660,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
       sk = min(sk, k);
     mult_new += c == newt;
   }
-  STW(skey[row], row_floor(sk, mk, vb, p));
+  skey[row] = uint16_t(row_floor(sk, mk, vb, p));
   if (newt == t)
     return;
   if (t >= 0 && kt != kDeadKey)
@@ -677,7 +677,7 @@ __device__ __forceinline__ void vote_row(const Dev& s, int buf, int round, int64
   } else {
     atomicSub(&s.nvote[newt], mult_new);
   }
-  STW(rtgt[row], newt);
+  rtgt[row] = newt;
 }
 
 // Filter + re-vote of the rows [lo, hi) of buffer `buf` by the calling workgroup, every wave on its own
@@ -1132,14 +1132,14 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
     if (s.vstate[lv] != 0)
       lv = -1;
     else if (!dup)
-      STW(s.vstate[lv], round + 1);
+      s.vstate[lv] = round + 1;
     else if (atomicCAS(&s.vstate[lv], 0, round + 1) != 0)
       lv = -1;
   }
   int len = 0;
   if (lv >= 0) {
     lx = r / lp;
-    STW(s.x[lv], lx);
+    s.x[lv] = lx;
     len = int(re - rb);
   } else {
     rb = re = 0;
@@ -1199,7 +1199,7 @@ __device__ __forceinline__ void saturate_chunk(const Dev& s, int32_t c, double r
       if (cc[u] >= 0 && (cc[u] == c || (ce & kCexpDead)))
         cc[u] = -1;
       if (cc[u] >= 0) {
-        STW(s.ctouch[cc[u]], 1);  // receives decrements this round (mm_update reads its record)
+        s.ctouch[cc[u]] = 1;  // receives decrements this round (mm_update reads its record)
         fat[u] = ce & kCexpFat;
         const double w = ww[u];
         a0[u] = (long long)dec_q(w * ox, cexp_rem(ce));
@@ -1360,7 +1360,7 @@ template <int K> __device__ __forceinline__ void saturate_one_pre(const Dev& s, 
   for (uint32_t base = cb + uint32_t(k) * kWave; base < ce; base += K * kWave)  // wave-uniform
     saturate_chunk(s, c, r, base, ce, round, lane, pre, dup SC_ANAT_ARGS);
   if (k == 0 && lane == 0)
-    STW(s.ctouch[c], 2);
+    s.ctouch[c] = 2;
 }
 
 // K waves per ready constraint: every block rebuilds the exclusive prefix of the per-segment ready
@@ -1702,24 +1702,22 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     bool changed = false;
     CstRec* rec = s.cst + c;
     if (sat) {
-      STW(s.key[c], kDeadKey);
-      STW(s.cexp[c], kCexpDead);
-      STW(s.chg[c], round);
-      STW(s.ctouch[c], 0);
-      STW(rec->ratio, dinf());
+      s.key[c] = kDeadKey;
+      s.cexp[c] = kCexpDead;
+      s.chg[c] = uint16_t(round);
+      s.ctouch[c] = 0;
+      rec->ratio = dinf();
       changed = true;
     } else if (live) {
       if (!tch) {
         alive++;
       } else {
         *touch = true;
-        STW(s.ctouch[c], 0);
-        STW(rec->drem, 0);
-        STW(rec->duse, 0);
-        STW(rec->dcnt, 0);
+        s.ctouch[c] = 0;
+        rec->drem = rec->duse = rec->dcnt = 0;
         const int nvn = nv[k] - int(qz[k]);
-        STW(s.nvote[c], nvn);
-        STW(s.chg[c], round);
+        s.nvote[c] = nvn;
+        s.chg[c] = uint16_t(round);
         double r0 = rem[k], u0;
         if (!fat) {
           u0 = use[k] - dec_val(qy[k], cexp_use(ce[k]));
@@ -1731,18 +1729,18 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
         } else {
           u0 = fuse;
         }
-        STW(rec->rem, r0);
-        STW(rec->use, u0);
+        rec->rem = r0;
+        rec->use = u0;
         if (!(u0 > prec) || !(r0 > bnd[k] * prec)) {
-          STW(rec->ratio, dinf());
-          STW(s.key[c], kDeadKey);
-          STW(s.cexp[c], kCexpDead);
+          rec->ratio = dinf();
+          s.key[c] = kDeadKey;
+          s.cexp[c] = kCexpDead;
           changed = true;
         } else {
           const double r = r0 / u0;
-          STW(rec->ratio, r);
+          rec->ratio = r;
           const unsigned nk = ratio_key(r);
-          STW(s.key[c], nk);
+          s.key[c] = uint16_t(nk);
           changed = nk != okey[k];
           alive++;
           if (kRdq && nvn == 0) {  // its last elements voting elsewhere left with fixed variables: ready next
@@ -1755,7 +1753,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     }
     const unsigned long long word = __ballot(changed);
     if (lane == 0)
-      STW(s.chgbits[gbase >> 6], word);
+      s.chgbits[gbase >> 6] = word;
   }
 #if LMM_ANAT
   if (an)
