@@ -40,6 +40,8 @@ PASSES = {
         "new": "fr_vote's first queue entry loaded with the count"}),
     "abm_": ("M", "scripts/gpu_r06_m.sh", {
         "base": "product build", "wt": "round kernels' state stores written through (LMM_WT=1, abl/wt)"}),
+    "abn_": ("N", "scripts/gpu_r06_n.sh", {
+        "n0": "build before (abl/n0)", "new": "no single-address atomic drains (init count, FB counters, LASTR)"}),
 }
 
 

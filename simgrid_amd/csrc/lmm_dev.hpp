@@ -23,7 +23,7 @@ enum : int {
   CTL_ANY0 = 2,      // fair bottleneck: "some variable still listed", per round parity (2 words)
   CTL_NROWS = 4,     // alive-row buffer sizes (3 buffers)
   CTL_NELEM = 7,     // alive-row buffer element counts (3 buffers)
-  CTL_ALIVE_C = 10,  // maxmin: constraints still in the light table
+  CTL_ALIVE_C = 10,  // (unused since round 6)
   CTL_NREADY = 11,   // maxmin: ready-list length of the current round
   CTL_RDQ0 = 12,     // multi-launch maxmin: the vote's ready-queue lengths, per round parity (2 words; rdq)
   CTL_NCL0 = 14,     // maxmin: alive-constraint list lengths (2 buffers)
@@ -35,11 +35,16 @@ enum : int {
   CTL_BUF = 21,    // alive-row buffer of the next vote (0 = the CSR, 1 / 2 = compaction targets)
   CTL_CB = 22,     // alive-constraint list in use (0 / 1)
   CTL_CMPGO = 23,  // the last compaction count found the rewrite worth it (cmp_scan -> cmp_write, mm_flip)
-  // fair bottleneck: the reference's work summed over the rounds, three uint64 words:
-  // elements of the listed constraints, listed variables, listed constraints (words 24..29)
+  // fair bottleneck: the reference's work summed over the rounds, three uint64 counters —
+  // elements of the listed constraints, listed variables, listed constraints — each spread over kFbwSlots uint64
+  // slots after the control words (CTL_FBW_AT; round 6: one counter word took one atomic per wave, 8,192 per
+  // fb_var_inc launch, ~11 ns each on one address, drained after the grid's last wave)
   CTL_FBW = 24,
   CTL_WORDS = 32
 };
+constexpr int kFbwSlots = 64;
+constexpr int CTL_FBW_AT = CTL_WORDS;                    // first int32 word of the [3][kFbwSlots] uint64 slots
+constexpr int CTL_ALLOC = CTL_WORDS + 2 * 3 * kFbwSlots;  // int32 words of the control buffer
 
 // maxmin per-constraint state, one 64-B line per constraint (array-of-structs): a constraint touched
 // in a round dirties ONE line instead of one line in each of eight arrays (mm_update's write-back

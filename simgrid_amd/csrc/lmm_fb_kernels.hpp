@@ -119,13 +119,15 @@ __global__ void __launch_bounds__(kBlock) fbk_nb(Dev s, int par) {
     s.xnb[s.nC] = s.ctl[CTL_ANY0 + par];
 }
 
-// Per-wave sum of a work counter into ctl word pair CTL_FBW + 2 k (one atomic per wave).
+// Per-wave sum of work counter k into one of its kFbwSlots slots (one atomic per wave, the waves spread over the slots;
+// lmmhip_fb_work sums them).
 __device__ __forceinline__ void fb_work_add(const Dev& s, int k, unsigned long long v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
     v += __shfl_xor(v, o, kWave);
+  const int slot = int((blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) & (kFbwSlots - 1));
   if ((threadIdx.x & (kWave - 1)) == 0 && v)
-    atomicAdd(reinterpret_cast<unsigned long long*>(s.ctl + CTL_FBW) + k, v);
+    atomicAdd(reinterpret_cast<unsigned long long*>(s.ctl + CTL_FBW_AT) + k * kFbwSlots + slot, v);
 }
 
 // :65-87 — usage = remaining / nb (FATPIPE: nb -> 1); nb == 0 erases the constraint.  xnb holds the

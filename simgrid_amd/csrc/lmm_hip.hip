@@ -422,7 +422,7 @@ static int alloc_flat_exact(lmmhip_ctx* c, int64_t nV, int64_t nC, int64_t nnz, 
   rc |= dalloc(c, &d.clist[0], nC);
   rc |= dalloc(c, &d.clist[1], nC);
   rc |= dalloc(c, &d.bsum, 2 * nblk);
-  rc |= dalloc(c, &d.ctl, CTL_WORDS);
+  rc |= dalloc(c, &d.ctl, CTL_ALLOC);
   int32_t *chc, *cch;
   uint32_t* chb;
   rc |= dalloc(c, &chc, nch);
@@ -1302,7 +1302,7 @@ int lmmhip_solve(lmmhip_ctx* c, int kind, double precision) {
   c->launch_slot.clear();
   c->launch_round.clear();
   c->launch_ms.clear();
-  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_ALLOC * sizeof(int32_t), c->stream));
   const size_t stat_bytes = sizeof(int32_t) * 2 * size_t(kStatRounds) * kMaxBlocks;
   if (c->profiling && !c->vstat)
     HIPCHK(hipMalloc(&c->vstat, stat_bytes));
@@ -1826,7 +1826,7 @@ static int solve_maxmin_persist(lmmhip_ctx* c, double prec) {
     return rc;
   c->persist_fallbacks += 1;
   c->persist_cool = env_int("LMMHIP_PERSIST_COOLDOWN", 64);
-  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_ALLOC * sizeof(int32_t), c->stream));
   c->ev1_done = false;
   return solve_maxmin(c, prec);
 }
@@ -2374,7 +2374,7 @@ int lmmhip_fb_shard_begin(lmmhip_ctx* c, double precision, int32_t* xnb, double*
   c->launch_slot.clear();
   c->launch_round.clear();
   c->launch_ms.clear();
-  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_WORDS * sizeof(int32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->d.ctl, 0, CTL_ALLOC * sizeof(int32_t), c->stream));
   c->d.xnb = xnb;
   c->d.xmin = c->xmin_own;
   c->fbo.xmu = xmu;
@@ -2413,9 +2413,12 @@ int lmmhip_fb_work(lmmhip_ctx* c, int64_t* out3) {
   HIPCHK(hipSetDevice(c->device));
   if (int rc = poll_ctl(c))
     return rc;
+  uint64_t sl[3 * kFbwSlots];
+  HIPCHK(hipMemcpy(sl, c->d.ctl + CTL_FBW_AT, sizeof sl, hipMemcpyDeviceToHost));
   for (int k = 0; k < 3; k++) {
-    uint64_t v;
-    std::memcpy(&v, c->h_ctl + CTL_FBW + 2 * k, sizeof v);
+    uint64_t v = 0;
+    for (int i = 0; i < kFbwSlots; i++)
+      v += sl[k * kFbwSlots + i];
     out3[k] = int64_t(v);
   }
   return 0;

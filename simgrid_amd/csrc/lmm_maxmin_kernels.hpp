@@ -129,11 +129,12 @@ __device__ __forceinline__ int init_cnsts_waves(const Dev& s, double prec, int64
   return alive_cnt;
 }
 
+// (Round 6: the per-wave count of alive constraints this kernel used to add into one control word — read by nobody —
+// was 8,192 atomics on one address per solve, serialised in the memory-side unit after the grid's short work: the
+// whole 74-us init of C4 and ~70 us of C2's.)
 __global__ void __launch_bounds__(kBlock) mm_init_cnsts(Dev s, double prec) {
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int alive_cnt = grp_isum<kWave>(init_cnsts_waves(s, prec, wave, int64_t(gridDim.x) * (kBlock / kWave)));
-  if ((threadIdx.x & (kWave - 1)) == 0 && alive_cnt)
-    atomicAdd(&s.ctl[CTL_ALIVE_C], alive_cnt);
+  init_cnsts_waves(s, prec, wave, int64_t(gridDim.x) * (kBlock / kWave));
 }
 
 // kRec: also the packed row records of buffer 0 (the multi-launch engine's init only).
@@ -1547,9 +1548,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     SC_LVL(6, cur.r + double(cur.kc + unsigned(cur.nv) + cur.cb + cur.ce + unsigned(cur.dup)));
     const CandSt nxt = state_of(cnext);  // (issued before this task's chunk loads)
     cnext = g + 2 * nwaves < T ? cand_of(g + 2 * nwaves) : -1;
-    if (cur.kc != kDeadKey && cur.nv == 0) {
-      if (k == 0 && lane == 0)
-        s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
+    if (cur.kc != kDeadKey && cur.nv == 0) {  // (the round's CTL_LASTR: mm_update, from the constraints saturated here)
       saturate_one_pre<K>(s, cur.c, k, round, lane, wpre[w], cur.r, cur.cb, cur.ce, cur.dup SC_ANAT_ARGS);
     }
     cur = nxt;
@@ -1575,8 +1574,6 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     SC_LVL(6, r + double(kc + unsigned(nv) + cb + cend + unsigned(dup)));
     if (kc == kDeadKey || nv != 0)
       continue;
-    if (k == 0 && lane == 0)
-      s.ctl[CTL_LASTR] = round;  // plain store: this round fixes variables
     saturate_one_pre<K>(s, c, k, round, lane, wpre[w], r, cb, cend, dup SC_ANAT_ARGS);
   }
 #endif
@@ -1702,6 +1699,7 @@ __device__ __forceinline__ int update_groups(const Dev& s, int64_t base0, int64_
     bool changed = false;
     CstRec* rec = s.cst + c;
     if (sat) {
+      *touch = true;  // (a saturation this round: the round's CTL_LASTR, set here instead of by every ready task)
       s.key[c] = kDeadKey;
       s.cexp[c] = kCexpDead;
       s.chg[c] = uint16_t(round);
