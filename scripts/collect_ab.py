@@ -41,7 +41,8 @@ PASSES = {
     "abm_": ("M", "scripts/gpu_r06_m.sh", {
         "base": "product build", "wt": "round kernels' state stores written through (LMM_WT=1, abl/wt)"}),
     "abn_": ("N", "scripts/gpu_r06_n.sh", {
-        "n0": "build before (abl/n0)", "new": "no single-address atomic drains (init count, FB counters, LASTR)"}),
+        "n0": "build before (abl/n0)", "new0": "no single-address atomic drains (init count, FB counters, LASTR)",
+        "new": "+ the vote's ready segments (LMMHIP_VOTE_SEG=1, default)"}),
 }
 
 
