@@ -188,8 +188,6 @@ struct Dev {
   int32_t* rqst;     // [nC] the round a constraint was last queued for (one entry per constraint and round)
   int32_t* useg;     // [blocks x kUSeg] the update's ready candidates for the next round, a segment per workgroup
   int32_t* ucnt;     // [blocks] their counts
-  int32_t* vseg;     // [vote workgroups x kRqCap] the vote's ready constraints, a segment per workgroup (round 6)
-  int32_t* vcnt;     // [vote workgroups] their counts
   uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements

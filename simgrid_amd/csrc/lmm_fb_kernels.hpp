@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(kBlock) fb_var_inc(Dev s, int par, int round) 
       any |= var_inc_finish(s, v, __longlong_as_double((long long)wmn[lane]), round);
     __builtin_amdgcn_wave_barrier();
   }
-  if (__any(any) && (threadIdx.x & (kWave - 1)) == 0)
+  if (__syncthreads_or(any) && threadIdx.x == 0)  // (one store per workgroup on the flag word, not one per wave)
     s.ctl[CTL_ANY0 + (par ^ 1)] = 1;
   fb_work_add(s, 1, nvl);
 }

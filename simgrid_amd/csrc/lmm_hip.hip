@@ -177,7 +177,6 @@ struct lmmhip_ctx {
   Scr fr_c2s, fr_slot, fr_minfl, fr_qa, fr_qb, fr_qn, fr_md, fr_pvb, fr_key;
   Scr mm_crec[3];  // solve_maxmin: packed row records (LMMHIP_CREC)
   Scr mm_rdq[2], mm_rqst, mm_useg, mm_ucnt;  // solve_maxmin: ready queue / update segments (LMMHIP_RDQ)
-  Scr mm_vseg, mm_vcnt;                      // solve_maxmin: the vote's ready segments (one per vote workgroup)
   bool fr_map_ok = false;
   int fr_maxdeg = 0;
   Scr rs_stage[12], rs_pos, rs_list, rs_lpart, rs_lany, rs_dcl, rs_cdeg, rs_cptr, rs_vrst, rs_vm, rs_dv, rs_rl,
@@ -316,7 +315,7 @@ int lmmhip_ctx_destroy(lmmhip_ctx* c) {
                   (void*)c->res.c_fl})
     if (p)
       (void)hipFree(p);
-  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->mm_vseg, &c->mm_vcnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
+  for (lmmhip_ctx::Scr* b : {&c->sat_out, &c->tv_out, &c->fb_longl, &c->fbp_k0, &c->fbp_k1, &c->fbp_v0, &c->fbp_v1, &c->fbp_tmp, &c->fbp_perm, &c->fbp_cscvp, &c->fbp_mu, &c->fr_c2s, &c->fr_slot, &c->fr_minfl, &c->fr_qa, &c->fr_qb, &c->fr_qn, &c->fr_md, &c->fr_pvb, &c->fr_key, &c->mm_crec[0], &c->mm_crec[1], &c->mm_crec[2], &c->mm_rdq[0], &c->mm_rdq[1], &c->mm_rqst, &c->mm_useg, &c->mm_ucnt, &c->cc_par, &c->cc_flag, &c->cc_rank, &c->cc_out, &c->rs_pos, &c->rs_list, &c->rs_lpart, &c->rs_lany, &c->rs_dcl, &c->rs_cdeg,
                              &c->rs_cptr, &c->rs_vrst, &c->rs_vm, &c->rs_dv, &c->rs_rl, &c->rs_ro, &c->rs_rowid,
                              &c->rs_kidx, &c->rs_skey, &c->rs_sval, &c->rs_vout, &c->rs_tmp, &c->rs_lzero,
                              &c->rs_nck, &c->rs_cch, &c->rs_rowpen, &c->rs_posd, &c->rs_cls, &c->rs_lanyc, &c->rs_outc, &c->rs_vlist, &c->rs_c2c})
@@ -1410,9 +1409,7 @@ static int poll_ctl(lmmhip_ctx* c) {
 
 // The alive-row buffer in use is read by the vote on the device (ctl CTL_BUF); nrows (an upper bound of its
 // rows, refreshed at every poll) only sizes the grid-stride variants' grids.
-// *vblocks: the vote workgroups whose ready segments (vseg / vcnt) this round's saturation reads (0: none)
-static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int* vblocks) {
-  *vblocks = 0;
+static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows) {
   const Dev& d = c->d;
   const int G = c->group;
   const int grid = grid_for(nrows, kBlock);  // one lane per row in the work-queue scan
@@ -1427,10 +1424,8 @@ static int launch_vote(lmmhip_ctx* c, int64_t r, int64_t nrows, int* vblocks) {
         LAUNCH(7, r, (mm_vote_lane<kVBlock, true, 1>), c->n_cu, kVBlock, d, int(r));
         LAUNCH(7, r, mm_vote_diagcount, grid_for((int64_t(d.nC) + 63) / 64, kBlock), kBlock, d, int(r));
       }
-      if (d.rdq[0]) {
+      if (d.rdq[0])
         LAUNCH(2, r, (mm_vote_lane<kVBlock, true, 0, true, true>), c->n_cu, kVBlock, d, int(r));
-        *vblocks = d.vseg ? c->n_cu : 0;
-      }
       else if (d.crec[0])
         LAUNCH(2, r, (mm_vote_lane<kVBlock, true, 0, true>), c->n_cu, kVBlock, d, int(r));
       else
@@ -1466,7 +1461,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       d.crec[0] = d.crec[1] = d.crec[2] = nullptr;
       d.rdq[0] = d.rdq[1] = nullptr;
       d.rqst = d.useg = d.ucnt = nullptr;
-      d.vseg = d.vcnt = nullptr;
     }
   } rowof_off{d};
   // packed row records for the re-votes (vote_row: the row's variable and CSR range from one 8-B record and
@@ -1486,7 +1480,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // 25.07-25.22 vs 25.34-25.39 ms, stress 28.29 vs 28.46, same box; LMMHIP_RDQ=0: the mm_ready pass)
   d.rdq[0] = d.rdq[1] = nullptr;
   d.rqst = d.useg = d.ucnt = nullptr;
-  d.vseg = d.vcnt = nullptr;
   // (<= kMaxBlocks) Update workgroups: 4 per CU, each with a longer segment, so that the saturation's prefix over
   // the segment counts is shorter — but enough of them to keep every segment within kUSeg (LMMHIP_UPDQ_BLOCKS).
   // Round 5, same box: C2 24.52-24.54 ms against 24.84-24.85 with one per 256 constraints (2,048 at C2), stress
@@ -1509,16 +1502,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     d.rqst = st;
     d.useg = sg;
     d.ucnt = uc;
-    // the vote's ready constraints in one segment per vote workgroup (one 1024-thread workgroup per CU: the bitmap
-    // vote) when the saturation's prefix has room for them after the update's segments (LMMHIP_VOTE_SEG, A/B knob)
-    if (env_int("LMMHIP_VOTE_SEG", 1) && gU_rdq + c->n_cu <= kMaxBlocks) {
-      int32_t *vs = nullptr, *vc = nullptr;
-      if (int rc = scratch(c, c->mm_vseg, int64_t(c->n_cu) * kRqCap, &vs) | scratch(c, c->mm_vcnt, c->n_cu, &vc))
-        return rc;
-      HIPCHK(hipMemsetAsync(vc, 0, size_t(c->n_cu) * sizeof(int32_t), c->stream));
-      d.vseg = vs;
-      d.vcnt = vc;
-    }
   }
   c->vote_bits = env_int("LMMHIP_VOTE_BITS", 1) != 0;
   c->vote_bits_rows = env_int("LMMHIP_VOTE_BITS_ROWS", 0);
@@ -1585,16 +1568,15 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   for (;;) {
     const int gL = grid_for(ncl, kBlock);
     for (int k = 0; k < chunk; k++, r++) {
-      int vblocks = 0;
-      if (int rc = launch_vote(c, r, nrows, &vblocks))
+      if (int rc = launch_vote(c, r, nrows))
         return rc;
       if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
         if (sat_k == 1)
-          LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq, vblocks);
+          LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
         else if (sat_k == 2)
-          LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq, vblocks);
+          LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
         else
-          LAUNCH(4, r, mm_saturate_q<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq, vblocks);
+          LAUNCH(4, r, mm_saturate_q<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
         LAUNCH(5, r, mm_update<true>, gUq, kBlock, d, int(r), prec);
         continue;
       }

@@ -191,6 +191,8 @@ __device__ __forceinline__ void rdq_push(const Dev& s, int32_t c, int qround) {
 // entries a workgroup queues directly (the old path).  The queue's order does not matter: the saturation of one
 // round's ready constraints commutes (no shared alive variable, fixed-point integer decrements).
 constexpr int kRqCap = 2048;
+// (Round 6 measured the workgroup's list written to a segment of its own — plain stores, read by the saturation after
+// the update's segments — instead of the one returning add per workgroup: C2 23.59-23.60 ms against 23.48-23.58.)
 struct RdqLds {
   int n, base;
   int32_t buf[kRqCap];
@@ -205,18 +207,6 @@ __device__ __forceinline__ void rdq_push_lds(const Dev& s, int32_t c, int qround
       s.rdq[q][atomicAdd(&s.ctl[CTL_RDQ0 + q], 1)] = c;
     }
   }
-}
-// Round 6: with one vote workgroup per CU, the workgroup's list goes to its own segment (vseg / vcnt, plain stores), which
-// the saturation reads after the update's segments: no returning add on the queue's one counter word at the end of
-// every workgroup (256 of them per round, ~11 ns each on one address, all at the vote's end).
-__device__ __forceinline__ void rdq_flush_seg(const Dev& s, RdqLds* L) {
-  __syncthreads();
-  const int n = L->n < kRqCap ? L->n : kRqCap;
-  int32_t* dst = s.vseg + int64_t(blockIdx.x) * kRqCap;
-  for (int i = threadIdx.x; i < n; i += blockDim.x)
-    dst[i] = L->buf[i];
-  if (threadIdx.x == 0)
-    s.vcnt[blockIdx.x] = n;
 }
 // (every thread of the workgroup, after its last push)
 __device__ __forceinline__ void rdq_flush_lds(const Dev& s, int qround, RdqLds* L) {
@@ -1011,9 +1001,7 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
     nq = vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits,
                                                               q + (threadIdx.x / kWave) * kQW, &st_rows, &st_elems,
                                                               s.key, tt0, sk0, &rql, an, &aa, &ar, wcnt);
-  if (kRdq && kDiag == 0 && B == kVBlock && s.vseg)
-    rdq_flush_seg(s, &rql);
-  else if (kRdq && kDiag == 0)
+  if (kRdq && kDiag == 0)
     rdq_flush_lds(s, round, &rql);
   if (an) {  // the wave's record (vote_row's levels: the slowest lane of the wave)
     const unsigned long long t_out = anat_now();
@@ -1044,9 +1032,7 @@ __global__ void __launch_bounds__(B) mm_vote_lane(Dev s, int round) {
   if (lo < hi)
     vote_waves<kBits, 8, kFilt, kDiag, kRec, kRdq, kPre>(s, buf, round, lo, hi, bits, q + (threadIdx.x / kWave) * kQW,
                                                          &st_rows, &st_elems, s.key, tt0, sk0, &rql);
-  if (kRdq && kDiag == 0 && B == kVBlock && s.vseg)
-    rdq_flush_seg(s, &rql);
-  else if (kRdq && kDiag == 0)
+  if (kRdq && kDiag == 0)
     rdq_flush_lds(s, round, &rql);
 #endif
   if (s.vstat && kDiag == 0) {
@@ -1452,8 +1438,7 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate(Dev s, in
 #ifndef LMM_SATQ_PIPE
 #define LMM_SATQ_PIPE 1
 #endif
-// vblocks: the vote workgroups whose segments (vseg / vcnt) follow the update's (0: the vote queued globally)
-template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks, int vblocks) {
+template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, int round, int ublocks) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -1471,13 +1456,12 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
   __shared__ int pre[kMaxBlocks + 1];
   __shared__ int wsum[kBlock / kWave];
   constexpr int kPer = kMaxBlocks / kBlock;
-  const int nseg = ublocks + vblocks;  // (<= kMaxBlocks: the host's choice)
   int loc[kPer];
   int sum = 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int seg = threadIdx.x * kPer + k;
-    loc[k] = seg < ublocks ? s.ucnt[seg] : seg < nseg ? s.vcnt[seg - ublocks] : 0;
+    loc[k] = seg < ublocks ? s.ucnt[seg] : 0;
     sum += loc[k];
   }
   int incl = sum;
@@ -1517,10 +1501,9 @@ template <int K> __global__ void __launch_bounds__(kBlock) mm_saturate_q(Dev s, 
     int lo = 0;  // last segment with pre[seg] <= i
 #pragma unroll
     for (int step = kMaxBlocks / 2; step > 0; step >>= 1)
-      if (lo + step < nseg && pre[lo + step] <= i)
+      if (lo + step < ublocks && pre[lo + step] <= i)
         lo += step;
-    return lo < ublocks ? s.useg[int64_t(lo) * kUSeg + (i - pre[lo])]
-                        : s.vseg[int64_t(lo - ublocks) * kRqCap + (i - pre[lo])];
+    return s.useg[int64_t(lo) * kUSeg + (i - pre[lo])];
   };
 #if LMM_SATQ_PIPE
   // Software-pipelined over the wave's tasks (round 6): the next task's candidate state (key, vote count, ratio, CSC
