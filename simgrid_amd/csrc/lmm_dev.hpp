@@ -190,6 +190,10 @@ struct Dev {
   int32_t* ucnt;     // [blocks] their counts
   uint2* crec[3];    // round engine, short rows: per alive row {cvar, crow} in one 8-B record (vote_row)
   int32_t* ctl;     // control words
+  // one-context FairBottleneck: pinned host words fbk_share writes itself (system scope) — [0] rounds started, [1] 1
+  // once the solve is over — by which the host paces its rounds without a control-word copy kernel per round
+  // (solve_fair_rounds).  Null elsewhere (the max-min engines, the sharded FairBottleneck phases)
+  int32_t* hprog;
   int32_t* vstat;   // profiling only (else null): [round][block] re-evaluated rows / elements
   // round anatomy (diagnostic build LMM_ANAT=1 only, else null): per-wave stamps of the round engine's kernels in
   // the rounds anat_r[0..kAnatSlots) (lmm_anat below)

@@ -136,13 +136,18 @@ __global__ void __launch_bounds__(kBlock) fbk_share(Dev s, int par) {
   if (s.ctl[CTL_DONE])
     return;
   if (s.xnb[s.nC] == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       s.ctl[CTL_DONE] = 1;
+      if (s.hprog)  // the host's pacing words (solve_fair_rounds)
+        __hip_atomic_store(s.hprog + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ANY0 + (par ^ 1)] = 0;
     s.ctl[CTL_ROUNDS] += 1;
+    if (s.hprog)
+      __hip_atomic_store(s.hprog, s.ctl[CTL_ROUNDS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   unsigned long long ne = 0, nc = 0;  // this round's listed constraints and their elements (measurement)
   for (int c = blockIdx.x * kBlock + threadIdx.x; c < s.nC; c += gridDim.x * kBlock) {

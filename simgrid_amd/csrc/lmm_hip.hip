@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 
 #include <algorithm>
@@ -72,7 +73,8 @@ struct lmmhip_ctx {
   hipStream_t own_stream = nullptr;  // the context's own stream (back to it: lmmhip_ctx_use_own_stream)
   Dev d{};
   std::vector<void*> allocs;  // owned device allocations
-  int32_t* h_ctl = nullptr;   // pinned mirror of the control words (+ 2 slots: pipelined polls of solve_maxmin)
+  int32_t* h_ctl = nullptr;   // pinned mirror of the control words (+ 2 slots: pipelined polls of solve_maxmin;
+                              // + 1: the words the device writes itself, Dev::hprog)
   hipEvent_t ev_poll[2] = {nullptr, nullptr};  // completion of the pipelined control-word copies
   std::vector<hipEvent_t> ev_slice;  // lmmhip_res_values_sliced: completion of each slice's copy
   bool uploaded = false;
@@ -272,7 +274,7 @@ int lmmhip_ctx_create(int device, lmmhip_ctx** out) {
     e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   c->stream = c->own_stream;
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&c->h_ctl, 3 * CTL_WORDS * sizeof(int32_t), hipHostMallocDefault);
+    e = hipHostMalloc((void**)&c->h_ctl, 4 * CTL_WORDS * sizeof(int32_t), hipHostMallocDefault);
   if (e == hipSuccess)
     e = hipHostMalloc((void**)&c->h_rdv, 64, hipHostMallocMapped);
   if (e == hipSuccess)
@@ -1560,36 +1562,33 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
                                      int(int64_t(d.nV) * std::max(0, env_int("LMMHIP_CHUNK_TAIL_PCT", 5)) / 100));
   const int64_t ctail_cnst = env_int("LMMHIP_CHUNK_TAIL_CNST", 0);
   const int ctail = std::max(1, env_int("LMMHIP_CHUNK_TAIL", 4));
-  bool pending = false;
-  int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
-  int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
-  for (int k = 0; k < 2; k++)
-    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
-  for (;;) {
-    const int gL = grid_for(ncl, kBlock);
-    for (int k = 0; k < chunk; k++, r++) {
-      if (int rc = launch_vote(c, r, nrows))
-        return rc;
-      if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
-        if (sat_k == 1)
-          LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
-        else if (sat_k == 2)
-          LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        else
-          LAUNCH(4, r, mm_saturate_q<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
-        LAUNCH(5, r, mm_update<true>, gUq, kBlock, d, int(r), prec);
-        continue;
-      }
-      LAUNCH(3, r, mm_ready, gL, kBlock, d);
+  auto round_launches = [&](int64_t r) -> int {
+    if (int rc = launch_vote(c, r, nrows))
+      return rc;
+    if (d.rdq[0]) {  // no mm_ready pass: the update's segments (gUq workgroups) and the vote's queue
       if (sat_k == 1)
-        LAUNCH(4, r, mm_saturate<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gL);
+        LAUNCH(4, r, mm_saturate_q<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gUq);
       else if (sat_k == 2)
-        LAUNCH(4, r, mm_saturate<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gL);
+        LAUNCH(4, r, mm_saturate_q<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gUq);
       else
-        LAUNCH(4, r, mm_saturate<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gL);
-      LAUNCH(5, r, mm_update<false>, gU, kBlock, d, int(r), prec);
+        LAUNCH(4, r, mm_saturate_q<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gUq);
+      LAUNCH(5, r, mm_update<true>, gUq, kBlock, d, int(r), prec);
+      return 0;
     }
-    LAUNCH(6, r, mm_done, 1, kBlock, d, d.rdq[0] ? gUq : gU);
+    const int gL = grid_for(ncl, kBlock);
+    LAUNCH(3, r, mm_ready, gL, kBlock, d);
+    if (sat_k == 1)
+      LAUNCH(4, r, mm_saturate<1>, capped(sat_grid(ncl), cap_sat), kBlock, d, int(r), gL);
+    else if (sat_k == 2)
+      LAUNCH(4, r, mm_saturate<2>, capped(sat_grid(2 * ncl), cap_sat), kBlock, d, int(r), gL);
+    else
+      LAUNCH(4, r, mm_saturate<4>, capped(sat_grid(4 * ncl), cap_sat), kBlock, d, int(r), gL);
+    LAUNCH(5, r, mm_update<false>, gU, kBlock, d, int(r), prec);
+    return 0;
+  };
+  // the alive-constraint list and the alive-row compaction at the end of a chunk (their cadence is the chunks')
+  auto chunk_end = [&](int64_t r) -> int {
+    const int gL = grid_for(ncl, kBlock);
     bool cl = false, cm = false;
     if (r - last_clist >= cl_every && ncl > 4096) {  // alive-constraint list (order not preserved)
       LAUNCH(6, r, mm_clist, std::min(gL, 2 * c->n_cu), kBlock, d, 0);
@@ -1606,6 +1605,20 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
     }
     if (cl || cm)
       LAUNCH(6, r, mm_flip, 1, 1, d, int(cl), int(cm));
+    return 0;
+  };
+  bool pending = false;
+  int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
+  int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
+  for (int k = 0; k < 2; k++)
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
+  for (;;) {
+    for (int k = 0; k < chunk; k++, r++)
+      if (int rc = round_launches(r))
+        return rc;
+    LAUNCH(6, r, mm_done, 1, kBlock, d, d.rdq[0] ? gUq : gU);
+    if (int rc = chunk_end(r))
+      return rc;
     LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
     HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
     if (pending) {  // the previous chunk's words (this chunk is queued behind them)
@@ -1690,9 +1703,37 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   if (d.nC > 0)
     HIPCHK(hipMemsetAsync(d.minfl, 0xFF, sizeof(uint32_t) * size_t(d.nC), c->stream));
   const int64_t max_rounds = int64_t(d.nV) + 2;  // every round fixes a variable (progress)
+  const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
+  auto round_launches = [&](int64_t r) -> int {
+    if (r == 0) {
+      LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
+      LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
+    } else if (long_rows) {  // (LV08 routes: ~12 elements per row)
+      LAUNCH(2, r, (fr_vote<false, 16>), (nblk + spb - 1) / spb, kFB, d, int(r), spb);
+    } else if (mf_early) {
+      LAUNCH(2, r, fr_vote<true>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
+    } else {
+      LAUNCH(2, r, fr_vote<false>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
+    }
+    if (sat_b == 256 && sat_old)
+      LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
+    else if (sat_b == 256)
+      LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
+    else if (sat_old)
+      LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r), bigch);
+    else
+      LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
+    if (big)
+      LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r), bigw);
+    LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec, upd_spec);
+    return 0;
+  };
   int64_t r = 0;
   // pipelined termination polls, as solve_maxmin: chunk k's control words land in a pinned slot behind an
-  // event while chunk k + 1 is queued; rounds queued after the last one return at once (CTL_DONE)
+  // event while chunk k + 1 is queued; rounds queued after the last one return at once (CTL_DONE).  (Round 6,
+  // measured and not kept: fr_vote storing "done" into a pinned host word itself, so that a poll is the event
+  // alone without mm_ctl_out — C4 3.083-3.091 ms against 3.060-3.069, scripts/gpu_r06_p.sh; and the launches paced
+  // by a per-round progress word, 2-5 rounds queued ahead — 3.17-3.28 against 3.12, scripts/gpu_r06_o.sh.)
   int chunk = 2, slot = 0;
   // rounds queued per poll: the host learns of termination one chunk late, so up to 2 x chunk_max no-op
   // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C4 3.48 ms at 8, 3.51-3.53 at 4, 3.55 at 16
@@ -1703,31 +1744,10 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   int32_t* hcd[2] = {nullptr, nullptr};
   for (int k = 0; k < 2; k++)
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
-  const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
   for (;;) {
-    for (int k = 0; k < chunk; k++, r++) {
-      if (r == 0) {
-        LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
-        LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
-      } else if (long_rows) {  // (LV08 routes: ~12 elements per row)
-        LAUNCH(2, r, (fr_vote<false, 16>), (nblk + spb - 1) / spb, kFB, d, int(r), spb);
-      } else if (mf_early) {
-        LAUNCH(2, r, fr_vote<true>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
-      } else {
-        LAUNCH(2, r, fr_vote<false>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
-      }
-      if (sat_b == 256 && sat_old)
-        LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
-      else if (sat_b == 256)
-        LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
-      else if (sat_old)
-        LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r), bigch);
-      else
-        LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
-      if (big)
-        LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r), bigw);
-      LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec, upd_spec);
-    }
+    for (int k = 0; k < chunk; k++, r++)
+      if (int rc = round_launches(r))
+        return rc;
     LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
     HIPCHK(hipEventRecord(c->ev_poll[slot], c->stream));
     if (pending) {
@@ -2108,11 +2128,61 @@ static int solve_fair_rounds(lmmhip_ctx* c, double prec) {
   // The reference's rounds are not bounded by the system size (FATPIPE remaining can shrink
   // geometrically: millions of rounds on 60-variable systems); give up past this budget.
   const int64_t max_rounds = 64 * (int64_t(c->d.nV) + int64_t(c->d.nC)) + 4096;
-  // One round queued ahead of the termination poll: after round r the control words go to a pinned slot
-  // (mm_ctl_out), round r + 1 is queued, then the host waits for round r's words.  A FairBottleneck round is
+  // (LMMHIP_FB_PACE=0) One round queued ahead of the termination poll: after round r the control words go to a pinned
+  // slot (mm_ctl_out), round r + 1 is queued, then the host waits for round r's words.  A FairBottleneck round is
   // long (C5: 0.2-3 ms), so the GPU never waits on the host and at most one empty round (its launches return
   // at once) runs after the last one; chunks of 4, 8, ... rounds left up to 7 empty rounds (63 launches,
   // ~0.2 ms on C5) plus a host round trip between chunks.
+  // Pacing by progress words (default; LMMHIP_FB_PACE=0: the polls below): fbk_share stores the number of rounds
+  // it has started into a pinned host word, or "done" beside it when nothing is listed (lmm_fb_kernels.hpp), and the
+  // host queues round r + 1 once round r's fbk_share has started — the rest of round r (its chains: 0.1-1 ms on C5)
+  // covers the queueing, no copy kernel or event per round, and no returning round after the one that finds the
+  // solve over.  Round 6, C5: 7.94-7.96 ms against 7.99-8.00 with LMMHIP_FB_PACE=0 (one box, scripts/gpu_r06_o.sh),
+  // 7.82-7.93 against 7.92-7.93 for the previous build (scripts/gpu_r06_p.sh).
+  if (env_int("LMMHIP_FB_PACE", 1)) {
+    volatile int32_t* hp = c->h_ctl + 3 * CTL_WORDS;
+    hp[0] = 0;
+    hp[1] = 0;
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d.hprog), c->h_ctl + 3 * CTL_WORDS, 0));
+    struct HprogOff {  // (the context's Dev: the other engines and the sharded phases run without the words)
+      Dev& d;
+      ~HprogOff() { d.hprog = nullptr; }
+    } hprog_off{c->d};
+    // rounds shorter than the host's queueing of the next one (small systems: a round is its ~9 launches) would
+    // leave the GPU idle under this pacing, so when the rounds come faster than every 150 us one round stays queued
+    // ahead (lag 1), as with the polls below
+    int lag = 0;
+    auto t_last = std::chrono::steady_clock::now();
+    for (;;) {
+      for (int ph = 0; ph < 3; ph++)
+        if (int rc = fb_phase(c, ph))
+          return rc;
+      const int32_t want = int32_t(c->fb_round) - lag;  // rounds started, counting the one just queued
+      for (unsigned spin = 0;; spin++) {
+        if (hp[1] || hp[0] >= want) {
+          const auto t = std::chrono::steady_clock::now();
+          lag = t - t_last < std::chrono::microseconds(150) ? 1 : 0;
+          t_last = t;
+          break;
+        }
+        if ((spin & 1023) == 1023) {  // everything queued has run (a guard: the words should have said so)
+          const hipError_t q = hipStreamQuery(c->stream);
+          if (q == hipSuccess)
+            break;
+          if (q != hipErrorNotReady)
+            return fail(LMMHIP_E_HIP, std::string("fair-bottleneck pacing: ") + hipGetErrorString(q));
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+      if (hp[1])
+        break;
+      if (c->fb_round > max_rounds)
+        return fail(LMMHIP_E_NOCONVERGE, "fair-bottleneck round guard tripped");
+    }
+    return poll_ctl(c);
+  }
   int slot = 0;
   bool pending = false;
   int32_t* hc[2] = {c->h_ctl + CTL_WORDS, c->h_ctl + 2 * CTL_WORDS};
