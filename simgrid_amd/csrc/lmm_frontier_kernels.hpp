@@ -332,11 +332,8 @@ __global__ void __launch_bounds__(kBlock) fr_minfl_all(Dev s) {
 
 // Rounds >= 1: the variables fr_update queued in workgroup b's segment (the CSC range of its constraints).
 // Also the termination test (maxmin.cpp:680): no constraint alive after the last update -> CTL_DONE.
-// fr_vote_blk: the work of (virtual) workgroup vb — also run by the persistent frontier kernel (fr_persist), whose
-// workgroups loop over the virtual ones; the queue counts are read relaxed (written in the same launch there).
-// kP: called by the persistent kernel (fr_persist), where the counts were written in the same launch: read relaxed
-// (the multi-launch kernel's plain loads may come from the scalar cache, which a launch boundary keeps coherent).
-template <bool kEarly, int R, bool kP = false>
+// fr_vote_blk: the work of workgroup vb.
+template <int R>
 __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, int vb
 #if LMM_ANAT
                                             , bool an = false, AnatAcc* aa = nullptr, AnatAcc* ar = nullptr,
@@ -352,7 +349,7 @@ __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, in
 #pragma unroll
   for (int k = 0; k < kFVS; k++) {
     const int64_t sg = int64_t(vb) * spb + k;
-    n[k] = k < spb && sg < nseg ? (kP ? ld_rlx(&s.fq_n[sg]) : s.fq_n[sg]) : 0;
+    n[k] = k < spb && sg < nseg ? s.fq_n[sg] : 0;
     seg[k] = k < spb && sg < nseg ? s.cnst_ptr[sg * kFB] : 0u;
     pre[k + 1] = pre[k] + n[k];
   }
@@ -378,10 +375,10 @@ __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, in
 #if LMM_ANAT
     if (an)
       ANAT_LVL(*ar, 0, a + rw);
-    const int o = fr_revote<R, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
+    const int o = fr_revote<R, true, false>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
                                              uint32_t(rw >> 32), round, an, ar);
 #else
-    const int o = fr_revote<R, true, kEarly>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
+    const int o = fr_revote<R, true, false>(s, int(uint32_t(a)), int(uint32_t(a >> 32)), uint32_t(rw),
                                              uint32_t(rw >> 32), round);
 #endif
     if (s.vstat) {
@@ -392,7 +389,7 @@ __device__ __forceinline__ void fr_vote_blk(const Dev& s, int round, int spb, in
   }
 }
 
-template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
+template <int R = 8> __global__ void __launch_bounds__(kFB) fr_vote(Dev s, int round, int spb) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_VOTE);
   const bool an = arec != nullptr;
@@ -411,7 +408,7 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
   if (blockIdx.x == 0 && threadIdx.x == 0)
     s.ctl[CTL_PALIVE0 + (round & 1)] = 0;  // this round's fr_update raises it
 #if LMM_ANAT
-  fr_vote_blk<kEarly, R>(s, round, spb, blockIdx.x, an, &aa, &ar, wc);
+  fr_vote_blk<R>(s, round, spb, blockIdx.x, an, &aa, &ar, wc);
   if (an) {  // the wave's record: queue-count level (lane 0), the re-vote levels of its slowest lane
     const unsigned long long t_out = anat_now();
     unsigned lv[5];
@@ -431,7 +428,7 @@ template <bool kEarly = true, int R = 8> __global__ void __launch_bounds__(kFB) 
     }
   }
 #else
-  fr_vote_blk<kEarly, R>(s, round, spb, blockIdx.x);
+  fr_vote_blk<R>(s, round, spb, blockIdx.x);
 #endif
 }
 
@@ -617,7 +614,7 @@ template <int NB> struct FrSatLds {
   int pre[NB / kWave][kWave];  // fr_sat_chunk's per-wave row-length prefix
 };
 
-template <int NB, bool kOld>
+template <int NB>
 __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& L FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -631,11 +628,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& 
     const int32_t cc = L.rc[k];
     const int ch = g - L.rr[k];
     const double r = L.rt[k];
-    if (kOld)  // (measurement: the multi-launch engine's chunk body)
-      saturate_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0);
-    else
-      fr_sat_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0
-                   FR_ANAT_ARGS);
+    fr_sat_chunk(s, cc, r, L.rb[k] + uint32_t(ch) * kWave, L.re[k], round, lane, L.pre[w], L.rd[k] != 0 FR_ANAT_ARGS);
     if (ch == 0 && lane == 0)
       s.ctouch[cc] = 2;
   }
@@ -646,7 +639,7 @@ __device__ __forceinline__ void fr_flush(const Dev& s, int round, FrSatLds<NB>& 
 // (fr_flush).  A constraint of more than kFrBigCh chunks is listed for fr_sat_big instead.
 constexpr int kFS = 1024;
 
-template <int NB, bool kOld>
+template <int NB>
 __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, int vb, FrSatLds<NB>& L
                                            FR_ANAT_PARAMS) {
   constexpr int NBW = NB / kWave;
@@ -731,10 +724,10 @@ __device__ __forceinline__ void fr_sat_blk(const Dev& s, int round, int bigch, i
   }
 #endif
   if (ta)  // workgroup-uniform
-    fr_flush<NB, kOld>(s, round, L FR_ANAT_ARGS);
+    fr_flush<NB>(s, round, L FR_ANAT_ARGS);
 }
 
-template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
+template <int kFS> __global__ void __launch_bounds__(kFS) fr_sat(Dev s, int round, int bigch) {
 #if LMM_ANAT
   unsigned long long* arec = anat_rec(s, anat_slot(s, round), ANAT_SAT);
   const bool an = arec != nullptr;
@@ -747,7 +740,7 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
     return;
   __shared__ FrSatLds<kFS> L;
 #if LMM_ANAT
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
+  fr_sat_blk<kFS>(s, round, bigch, blockIdx.x, L, an, &aa, wc);
   if (an && (threadIdx.x & (kWave - 1)) == 0) {
     arec[0] = t_in;
     arec[1] = anat_now();
@@ -758,19 +751,18 @@ template <int kFS, bool kOld = false> __global__ void __launch_bounds__(kFS) fr_
       arec[10 + i] = wc[i];
   }
 #else
-  fr_sat_blk<kFS, kOld>(s, round, bigch, blockIdx.x, L);
+  fr_sat_blk<kFS>(s, round, bigch, blockIdx.x, L);
 #endif
 }
 
 // The big ready constraints listed by fr_sat (count CTL_NREADY, reset by fr_update): kFrBigWaves waves per
 // constraint over the whole grid, wave k taking chunks k, k + kFrBigWaves, ...
 // (the grid's waves over the list: wave / nwaves; wpre = the calling wave's 64-int LDS scratch)
-template <bool kP = false>
 __device__ __forceinline__ void fr_sat_big_waves(const Dev& s, int round, int bigw, int nb, int64_t wave,
                                                  int64_t nwaves, int* wpre FR_ANAT_PARAMS) {
   const int lane = threadIdx.x & (kWave - 1);
   for (int64_t g = wave; g < int64_t(nb) * bigw; g += nwaves) {
-    const int32_t c = kP ? ld_rlx(&s.ready[g / bigw]) : s.ready[g / bigw];
+    const int32_t c = s.ready[g / bigw];
     const int k = int(g % bigw);
     const double r = ld_rlx(&s.cst[c].ratio);
     const uint32_t ce = s.cnst_ptr[c + 1];
@@ -841,13 +833,10 @@ struct FrUpdLds {
   uint32_t mf[kFB];
 };
 
-// kP: called by fr_persist (the control words another workgroup reads or adds to in the same launch: relaxed
-// atomic stores; the multi-launch kernel keeps its plain stores).
 // (LMM_ANAT: `an` = the levels into aa->lv: 0 keys + touch flags, 1 touched records, 2 arithmetic + scan prefix +
 // barrier, 3 slots, 4 queued voters' variable and row, 5 stores + barriers; wc[0] scanned slots)
 // spec (round 6, small systems): a constraint's record, scales, votes, floor and CSC range are loaded with its key and
 // touch flag whether or not it was touched (coalesced, one constraint per lane), one dependent level instead of two.
-template <bool kP = false>
 __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double prec, int vb, FrUpdLds& U, bool spec
                                               FR_ANAT_PARAMS) {
   int& qn = U.qn;
@@ -858,10 +847,7 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
     qn = 0;
   if (vb == 0 && threadIdx.x == 0) {
     s.ctl[CTL_ROUNDS] += 1;
-    if (kP)
-      st_rlx(&s.ctl[CTL_NREADY], 0);  // fr_sat_big's list of the next round (its adds are atomics: no cached copy)
-    else
-      s.ctl[CTL_NREADY] = 0;
+    s.ctl[CTL_NREADY] = 0;  // fr_sat_big's list of the next round
   }
   const int64_t gbase = int64_t(vb) * kFB + int64_t(w) * kWave;
   const int64_t c = gbase + lane;
@@ -1066,10 +1052,7 @@ __device__ __forceinline__ void fr_update_blk(const Dev& s, int round, double pr
   if (threadIdx.x == 0) {
     s.fq_n[vb] = qn;
     if (any_alive) {
-      if (kP)
-        st_rlx(&s.ctl[CTL_PALIVE0 + (round & 1)], 1);
-      else
-        s.ctl[CTL_PALIVE0 + (round & 1)] = 1;
+      s.ctl[CTL_PALIVE0 + (round & 1)] = 1;
     }
   }
   if (__syncthreads_or(tch || sat) && threadIdx.x == 0)

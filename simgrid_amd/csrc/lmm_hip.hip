@@ -1680,9 +1680,8 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int bigch = std::max(1, env_int("LMMHIP_FR_BIGCH", kFrBigCh));
   const bool big = c->fr_maxdeg > bigch * kWave;
   const int bigw = std::max(1, env_int("LMMHIP_FR_BIGW", kFrBigWaves));  // waves per big constraint (A/B knob)
-  // measurement knobs (defaults = the measured best): the re-vote reads the floors with the keys; the
-  // saturation's workgroup size and chunk body (the round engine's saturate_chunk)
-  const bool mf_early = env_int("LMMHIP_FR_MFEARLY", 0) != 0;
+  // (round 6, removed after their A/Bs: the re-vote reading the floors with the keys, LMMHIP_FR_MFEARLY, and the round
+  // engine's chunk body in fr_sat, LMMHIP_FR_SATOLD — both slower on C2 and C4, scripts/gpu_fr_ab.sh)
   // re-votes keep 16 row elements in registers when the mean row is longer than 8 (LMMHIP_FR_R16=0: 8)
   const bool long_rows = c->group > 8 && env_int("LMMHIP_FR_R16", 1) != 0;
   // fr_vote: segments per workgroup, so that the grid still covers the chip twice (C2: 4, small systems: 1)
@@ -1691,7 +1690,6 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   // idle — C4 (25 workgroups of kFS): 3.37-3.40 ms with 256-thread workgroups against 3.49
   const int sat_b0 = int64_t(nblkS) >= 2 * int64_t(c->n_cu) ? kFS : 256;
   const int sat_b = env_int("LMMHIP_FR_SATB", sat_b0) == 256 ? 256 : kFS;
-  const bool sat_old = env_int("LMMHIP_FR_SATOLD", 0) != 0;
   // fr_update: every constraint's state loaded with its key (one dependent level less) on the small systems, where the
   // 256-thread saturation workgroups run (LMMHIP_FR_UPDSPEC, A/B knob)
   const int upd_spec = env_int("LMMHIP_FR_UPDSPEC", sat_b == 256 ? 1 : 0);
@@ -1709,20 +1707,14 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       LAUNCH(2, r, fr_vote_all, grid_for(d.nV, kBlock), kBlock, d);
       LAUNCH(2, r, fr_minfl_all, grid_for(d.nC, kBlock / 16), kBlock, d);
     } else if (long_rows) {  // (LV08 routes: ~12 elements per row)
-      LAUNCH(2, r, (fr_vote<false, 16>), (nblk + spb - 1) / spb, kFB, d, int(r), spb);
-    } else if (mf_early) {
-      LAUNCH(2, r, fr_vote<true>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
+      LAUNCH(2, r, fr_vote<16>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
     } else {
-      LAUNCH(2, r, fr_vote<false>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
+      LAUNCH(2, r, fr_vote<8>, (nblk + spb - 1) / spb, kFB, d, int(r), spb);
     }
-    if (sat_b == 256 && sat_old)
-      LAUNCH(4, r, (fr_sat<256, true>), nblk, 256, d, int(r), bigch);
-    else if (sat_b == 256)
-      LAUNCH(4, r, (fr_sat<256, false>), nblk, 256, d, int(r), bigch);
-    else if (sat_old)
-      LAUNCH(4, r, (fr_sat<kFS, true>), nblkS, kFS, d, int(r), bigch);
+    if (sat_b == 256)
+      LAUNCH(4, r, fr_sat<256>, nblk, 256, d, int(r), bigch);
     else
-      LAUNCH(4, r, (fr_sat<kFS, false>), nblkS, kFS, d, int(r), bigch);
+      LAUNCH(4, r, fr_sat<kFS>, nblkS, kFS, d, int(r), bigch);
     if (big)
       LAUNCH(4, r, fr_sat_big, gbig, kBlock, d, int(r), bigw);
     LAUNCH(5, r, fr_update, nblk, kFB, d, int(r), prec, upd_spec);
