@@ -123,6 +123,10 @@ struct lmmhip_ctx {
   int64_t bt_cap = 0;
   // fair bottleneck round state (lmmhip_solve and the sharded lmmhip_fb_shard_* protocol)
   int64_t fb_round = 0;
+  // rounds the previous solve of this context had to queue before its termination test could fire (round engine:
+  // LASTR + 1, mm_done at the end of the chunk; frontier: ROUNDS + 1, the vote after the last update): a hint for
+  // where to end a chunk and wait for it (round_hint_chunk); 0 = none
+  int64_t hint_rounds_mm = 0, hint_rounds_fr = 0;
   uint32_t fb_longmin = 0;  // solve_fair: shared constraints with >= this many elements use fbk_acc's increments
   int fb_nlb = 128;          // solve_fair: fbk_update_seq workgroups for the long chains
   double fb_prec = 0;
@@ -728,6 +732,19 @@ static int env_int(const char* name, int dflt) {
 }
 
 // Flags and crossing list of the delta batches (lmmhip_ctx::res_dirty), zeroed on first use.
+// Chunk length under a round-count hint: a chunk that would cross the hinted end E is cut to end at it, and the
+// caller waits for that chunk before queueing more (*stop), so a solve as long as the previous one runs no returning
+// rounds after its last one; a longer one pays one host round trip there, a shorter one is caught by the usual polls.
+// Consecutive solves of a simulation change little, so their round counts do too.  LMMHIP_ROUND_HINT=0: off.
+static int round_hint_chunk(int64_t r, int chunk, int64_t hint, bool* stop) {
+  *stop = false;
+  if (hint > r && r + chunk >= hint) {
+    *stop = true;
+    return int(hint - r);
+  }
+  return chunk;
+}
+
 static int res_dirty_alloc(lmmhip_ctx* c) {
   if (c->res_dirty)
     return 0;
@@ -1612,8 +1629,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
   for (int k = 0; k < 2; k++)
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
+  const int64_t hint = env_int("LMMHIP_ROUND_HINT", 1) ? c->hint_rounds_mm : 0;
   for (;;) {
-    for (int k = 0; k < chunk; k++, r++)
+    bool stop = false;
+    const int n = round_hint_chunk(r, chunk, hint, &stop);
+    for (int k = 0; k < n; k++, r++)
       if (int rc = round_launches(r))
         return rc;
     LAUNCH(6, r, mm_done, 1, kBlock, d, d.rdq[0] ? gUq : gU);
@@ -1629,16 +1649,29 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
       ncl = h[CTL_NCL0 + h[CTL_CB]];
       nrows = h[CTL_NROWS + h[CTL_BUF]];
     }
-    pending = true;
+    pending = !stop;
+    if (stop) {  // the hinted end: this chunk's words before anything more is queued
+      HIPCHK(hipEventSynchronize(c->ev_poll[slot]));
+      const int32_t* h = hc[slot];
+      if (h[CTL_DONE])
+        break;
+      ncl = h[CTL_NCL0 + h[CTL_CB]];
+      nrows = h[CTL_NROWS + h[CTL_BUF]];
+    }
     slot ^= 1;
     if (r > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
     if (chunk < chunk_max)
       chunk = std::min(2 * chunk, chunk_max);
+    // (the short tail chunks stay under a hint too: dropping them measured 23.10 against 23.05-23.08 ms,
+    // scripts/gpu_r06_t.sh)
     if ((nrows <= ctail_rows || ncl <= ctail_cnst) && chunk > ctail)
       chunk = ctail;
   }
-  return poll_ctl(c);  // (the queued tail has run: final words for the stats)
+  if (int rc = poll_ctl(c))  // (the queued tail has run: final words for the stats)
+    return rc;
+  c->hint_rounds_mm = int64_t(c->h_ctl[CTL_LASTR]) + 1;
+  return 0;
 }
 
 // Frontier engine (lmm_frontier_kernels.hpp): three launches per round, work proportional to the touched
@@ -1736,8 +1769,14 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   int32_t* hcd[2] = {nullptr, nullptr};
   for (int k = 0; k < 2; k++)
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
+  const int64_t hint = env_int("LMMHIP_ROUND_HINT", 1) ? c->hint_rounds_fr : 0;
+  // with a hint the returning rounds after the last one are gone, and what longer chunks cost is with them: fewer
+  // polls (mm_ctl_out, 3.6 us of kernel each) up to the hinted end (LMMHIP_HINT_CHUNK_MAX, A/B knob)
+  const int chunk_cap = hint > 0 ? std::max(chunk_max, env_int("LMMHIP_HINT_CHUNK_MAX", 32)) : chunk_max;
   for (;;) {
-    for (int k = 0; k < chunk; k++, r++)
+    bool stop = false;
+    const int n = round_hint_chunk(r, chunk, hint, &stop);
+    for (int k = 0; k < n; k++, r++)
       if (int rc = round_launches(r))
         return rc;
     LAUNCH(6, r, mm_ctl_out, 1, kWave, d, hcd[slot]);
@@ -1747,14 +1786,22 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
       if (hc[slot ^ 1][CTL_DONE])
         break;
     }
-    pending = true;
+    pending = !stop;
+    if (stop) {  // the hinted end: this chunk's words before anything more is queued
+      HIPCHK(hipEventSynchronize(c->ev_poll[slot]));
+      if (hc[slot][CTL_DONE])
+        break;
+    }
     slot ^= 1;
     if (r > max_rounds)
       return fail(LMMHIP_E_NOCONVERGE, "maxmin round guard tripped");
-    if (chunk < chunk_max)
-      chunk = std::min(2 * chunk, chunk_max);
+    if (chunk < chunk_cap)
+      chunk = std::min(2 * chunk, chunk_cap);
   }
-  return poll_ctl(c);
+  if (int rc = poll_ctl(c))
+    return rc;
+  c->hint_rounds_fr = int64_t(c->h_ctl[CTL_ROUNDS]) + 1;
+  return 0;
 }
 
 static int engine_of(const lmmhip_ctx* c) {

@@ -329,3 +329,38 @@ def test_frontier_duplicate_elements_on_a_high_degree_constraint():
     assert xf.tobytes() == xr.tobytes(), float(np.max(np.abs(xf - xr)))
     assert first < 2.0, first
 
+
+
+def _hint_steps(s, ids, step):
+    """Mutations of the round-hint test: step 1 bounds a third of the variables tightly (early bound fixes: a
+    different round count), step 2 lifts them again (the first system back)."""
+    if step == 0:
+        return
+    for h in ids[::3]:
+        s.update_variable_bound(L.Variable(s, int(h)), 1e-4 if step == 1 else -1.0)
+
+
+@pytest.mark.parametrize("engine", [L.System.ENGINE_ROUNDS, L.System.ENGINE_FRONTIER])
+def test_round_hint_other_round_counts_bit_identical(engine):
+    """The chunked polls end a chunk where the previous solve of the context ended (round_hint_chunk, lmm_hip.hip):
+    a solve that takes more or fewer rounds than the previous one must still give a fresh context's bytes."""
+    build = _synthetic(20000, 200000, 5, False)
+    s = L.System(False)
+    ids = build(s)
+    s.set_engine(engine)
+    rounds = []
+    for step in (0, 1, 2, 1):
+        _hint_steps(s, ids, step)
+        s.solve()
+        x, r = s.values_of(ids), s.last_stats()["rounds"]
+        f = L.System(False)  # fresh context: the same system, no hint
+        fids = build(f)
+        for k in range(1, step + 1 if step < 2 else 3):
+            _hint_steps(f, fids, k)
+        f.set_engine(engine)
+        f.solve()
+        xf, rf = f.values_of(fids), f.last_stats()["rounds"]
+        assert r == rf, (step, r, rf)
+        assert x.tobytes() == xf.tobytes(), (step, float(np.max(np.abs(x - xf))))
+        rounds.append(r)
+    assert len(set(rounds)) > 1, rounds  # (the hint was wrong at least once)
