@@ -88,13 +88,23 @@ __global__ void __launch_bounds__(kBlock) fr_c2s(Dev s, int2* cs, int32_t* maxde
 }
 
 // Per-solve variable state (mm_init_vars) + the (bound, penalty) record the re-votes read in one line.
+// (with the slots' and floors' kNoVoter fill: two copy-engine fills and their launch gaps less per solve)
 __global__ void __launch_bounds__(kBlock) fr_init_vars(Dev s) {
-  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += int64_t(gridDim.x) * kBlock) {
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < s.nV; v += stride) {
     s.x[v] = 0.0;
     s.vstate[v] = 0;
     s.rtgt[0][v] = kUnvoted;
     s.pvb[v] = make_double2(s.vbound[v], s.pen[v]);
   }
+  uint4* vs4 = reinterpret_cast<uint4*>(s.vslot);  // (scratch allocations: 256-B aligned)
+  const uint4 none = make_uint4(kNoVoter, kNoVoter, kNoVoter, kNoVoter);
+  for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz / 4; j += stride)
+    vs4[j] = none;
+  for (int64_t j = (s.nnz & ~int64_t(3)) + int64_t(blockIdx.x) * kBlock + threadIdx.x; j < s.nnz; j += stride)
+    s.vslot[j] = kNoVoter;
+  for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < s.nC; c += stride)
+    s.minfl[c] = kNoVoter;
 }
 
 // Diagnostic counters (profiling mode only, vstat's kDiagSlot words of each round): 0 touched constraints,

@@ -1728,11 +1728,7 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   const int upd_spec = env_int("LMMHIP_FR_UPDSPEC", sat_b == 256 ? 1 : 0);
   const int gC4 = grid_for(d.nC, kBlock / kWave);
   LAUNCH(0, -1, mm_init_cnsts, gC4, kBlock, d, prec);
-  LAUNCH(1, -1, fr_init_vars, grid_for(d.nV, kBlock), kBlock, d);
-  if (d.nnz > 0)
-    HIPCHK(hipMemsetAsync(d.vslot, 0xFF, sizeof(uint32_t) * size_t(d.nnz), c->stream));  // kNoVoter
-  if (d.nC > 0)
-    HIPCHK(hipMemsetAsync(d.minfl, 0xFF, sizeof(uint32_t) * size_t(d.nC), c->stream));
+  LAUNCH(1, -1, fr_init_vars, grid_for(std::max<int64_t>(std::max<int64_t>(d.nV, d.nC), d.nnz / 4), kBlock), kBlock, d);
   const int64_t max_rounds = int64_t(d.nV) + 2;  // every round fixes a variable (progress)
   const int gbig = std::min(kMaxBlocks, 4 * c->n_cu);
   auto round_launches = [&](int64_t r) -> int {
@@ -1773,6 +1769,9 @@ static int solve_maxmin_frontier(lmmhip_ctx* c, double prec) {
   // with a hint the returning rounds after the last one are gone, and what longer chunks cost is with them: fewer
   // polls (mm_ctl_out, 3.6 us of kernel each) up to the hinted end (LMMHIP_HINT_CHUNK_MAX, A/B knob)
   const int chunk_cap = hint > 0 ? std::max(chunk_max, env_int("LMMHIP_HINT_CHUNK_MAX", 32)) : chunk_max;
+  // and the first chunk need not be short either (its point is an early poll for systems of few rounds)
+  if (hint > 0)
+    chunk = std::max(chunk, std::min(chunk_cap, env_int("LMMHIP_HINT_CHUNK0", chunk_cap)));
   for (;;) {
     bool stop = false;
     const int n = round_hint_chunk(r, chunk, hint, &stop);
