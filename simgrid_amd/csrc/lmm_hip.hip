@@ -1567,7 +1567,11 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   // rounds queued per poll: the host learns of termination one chunk late, so up to 2 x chunk_max no-op
   // rounds run after the last one (LMMHIP_CHUNK_MAX, A/B knob): C2 25.96-25.99 ms at 16, 26.01 at 8,
   // 26.15-26.20 at 4; round 5, with compactions every 48 rounds: 25.03-25.06 at 32 against 25.07-25.08 at 16
-  const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", 32));
+  const int64_t hint = env_int("LMMHIP_ROUND_HINT", 1) ? c->hint_rounds_mm : 0;  // (round_hint_chunk)
+  // under a hint no returning rounds follow the last one, and 64-round chunks (fewer polls, a sparser list / compaction
+  // cadence) measured 23.13-23.36 ms against 23.21-23.47 at 32 over five same-box pairs, stress 26.85 vs 26.88
+  // (scripts/gpu_r06_v.sh, _w.sh)
+  const int chunk_max = std::max(2, env_int("LMMHIP_CHUNK_MAX", hint > 0 ? 64 : 32));
   // Near the end of the solve, short chunks: the rounds queued after the last one are no-op launches of the full
   // grids (~32 of them after C2's last round with 32-round chunks, rocprofv3 trace of round 5), so once the alive rows
   // (host view: refreshed at each compaction) fall to LMMHIP_CHUNK_TAIL_PCT % of the variables (default 5), or below
@@ -1629,7 +1633,6 @@ static int solve_maxmin(lmmhip_ctx* c, double prec) {
   int32_t* hcd[2] = {nullptr, nullptr};  // the same slots as the device sees them (mm_ctl_out)
   for (int k = 0; k < 2; k++)
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcd[k]), hc[k], 0));
-  const int64_t hint = env_int("LMMHIP_ROUND_HINT", 1) ? c->hint_rounds_mm : 0;
   for (;;) {
     bool stop = false;
     const int n = round_hint_chunk(r, chunk, hint, &stop);
